@@ -1,0 +1,157 @@
+/*
+ * seb_bloom.h — C ABI of the MI355X-native bloom-filter build + probe path.
+ *
+ * Drop-in boundary for intellect4all/storage-engines lsm/bloom.go.  The reference is Go; its
+ * callers are lsm/sstable_builder.go:30,53,217 (build at flush/compaction) and
+ * lsm/sstable.go:129,206 (decode at open, probe on Get).  A cgo shim
+ * (storage-engines_amd/go/lsm/bloom.go) binds the "Go API mirror" group
+ * below one-for-one, so those callers compile unchanged.  Every entry point takes plain C types
+ * (pointers and sizes); no torch or HIP types appear in a signature (streams are `void*`
+ * holding a hipStream_t, NULL = the library's own stream / the null stream).
+ *
+ * Results are bit-exact with the reference: identical bit array (byte h>>3, bit h&7 — on the
+ * little-endian device this is u32 word h>>5, bit h&31) and identical MayContain answers.
+ *
+ * Errors: every int-returning function returns SEB_OK (0) or a negative SEB_ERR_* code, and
+ * seb_last_error() gives a thread-local message.  The reference has no error returns (bad input
+ * panics or yields nil); the Go shim turns a negative code into the same panic.
+ */
+#ifndef SEB_BLOOM_H
+#define SEB_BLOOM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SEB_ABI_VERSION 1
+
+enum seb_status {
+    SEB_OK = 0,
+    SEB_ERR_INVALID = -1, /* bad argument; the reference would panic (e.g. % 0, index out of range) */
+    SEB_ERR_DEVICE = -2,  /* HIP runtime error / no gfx950 device / kernel fault */
+    SEB_ERR_NOMEM = -3,   /* host or device allocation failed */
+    SEB_ERR_RANGE = -4,   /* sizing outside the reference's defined float->int range */
+    SEB_ERR_SHORT = -5,   /* a decoded filter's bits are shorter than ceil(numBits/8) */
+};
+
+/* A batch of keys.  Fixed-length keys: offsets == NULL, key i = data[i*stride, (i+1)*stride).
+ * Variable-length keys: offsets holds n+1 non-decreasing byte offsets (offsets[0] may be != 0),
+ * key i = data[offsets[i], offsets[i+1]).  Host or device memory per the entry point. */
+typedef struct seb_keys {
+    const uint8_t *data;
+    const uint64_t *offsets;
+    uint64_t n;
+    uint32_t stride;
+    uint32_t reserved; /* must be 0 */
+} seb_keys;
+
+/* One filter for the multi-filter probe.  `bits` is host bytes (ceil(num_bits/8)) for
+ * seb_probe_multi and device u32 words (seb_words_bytes(num_bits) bytes) for
+ * seb_dev_probe_multi. */
+typedef struct seb_filter_ref {
+    const void *bits;
+    uint64_t num_bits;
+    uint32_t num_hashes;
+    uint32_t reserved; /* must be 0 */
+} seb_filter_ref;
+
+/* ---------------------------------------------------------------- sizing (host only) ---- */
+
+/* m and k exactly as NewBloomFilter computes them (lsm/bloom.go:19-31): float64 Go math.Log,
+ * const-folded Ln2*Ln2, Ceil, k forced to >= 1.  n == 0 gives m = 0, k = 1 (as in Go). */
+int seb_params(int64_t expected_keys, double false_positive_rate, uint64_t *num_bits,
+               uint32_t *num_hashes);
+/* ceil(m/8): the reference's len(bits) (lsm/bloom.go:34). */
+uint64_t seb_num_bytes(uint64_t num_bits);
+/* Bytes of the device word array for m bits: ceil(m/128)*16 (u32 words, 16-B padded, pad = 0). */
+uint64_t seb_words_bytes(uint64_t num_bits);
+
+int seb_abi_version(void);
+const char *seb_last_error(void);
+/* 0 if a gfx950 device is usable, else SEB_ERR_DEVICE (message in seb_last_error). */
+int seb_device_check(int device);
+
+/* ------------------------------------------------- device-resident entry points ---------- */
+/* All pointers are device memory; work is enqueued on `stream` and NOT synchronised.
+ * seb_dev_build ORs the keys into `words` (clear first with seb_dev_clear for a fresh filter),
+ * the device form of the reference's Add loop (sstable_builder.go:53 -> bloom.go:70-77). */
+int seb_dev_clear(uint32_t *words, uint64_t num_bits, void *stream);
+int seb_dev_build(const seb_keys *keys, uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
+                  void *stream);
+/* out[i] = MayContain(key i) as 0/1 bytes (bloom.go:82-92; Go []bool layout). */
+int seb_dev_probe(const seb_keys *keys, const uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
+                  uint8_t *out, void *stream);
+/* Multi-filter probe: bit f of mask[i] = MayContain of filters[f] on key i.  mask_bytes is the
+ * width of one mask element (1, 2, 4 or 8) and must cover num_filters bits (<= 64). `filters`
+ * is a HOST array whose .bits are device word arrays. */
+int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *filters, uint32_t num_filters,
+                        void *mask, uint32_t mask_bytes, void *stream);
+/* Batched build of many independent filters in one launch (compaction output files,
+ * lsm/compaction.go:286): keys [key_begin[f], key_begin[f+1]) of `keys` go into filter f.
+ * `filters` is a HOST array whose .bits are device word arrays (cleared by the caller);
+ * key_begin is a HOST array of num_filters+1 entries. */
+int seb_dev_build_many(const seb_keys *keys, const uint64_t *key_begin, const seb_filter_ref *filters,
+                       uint32_t num_filters, void *stream);
+
+/* Small device/stream helpers for hosts without their own HIP binding (ctypes, cgo). */
+int seb_dev_alloc(void **ptr, uint64_t bytes);
+int seb_dev_free(void *ptr);
+int seb_host_alloc(void **ptr, uint64_t bytes); /* pinned host memory */
+int seb_host_free(void *ptr);
+int seb_memcpy_h2d(void *dst, const void *src, uint64_t bytes, void *stream);
+int seb_memcpy_d2h(void *dst, const void *src, uint64_t bytes, void *stream);
+int seb_stream_sync(void *stream);
+
+/* ------------------------------------------- host-buffer batched entry points ------------ */
+/* Keys and bits in host memory: H2D, kernels and D2H on the context's streams, synchronous.
+ * A context owns a device, streams and grow-only scratch buffers; one context per thread
+ * (contexts are cheap; calls on one context are serialised by a lock). */
+typedef struct seb_ctx seb_ctx;
+int seb_ctx_create(int device, seb_ctx **out);
+void seb_ctx_destroy(seb_ctx *ctx);
+
+#define SEB_BUILD_FRESH 1u /* `bits` is output only: start from an all-zero filter */
+/* bits: ceil(num_bits/8) host bytes, OR-accumulated (or written fresh with SEB_BUILD_FRESH). */
+int seb_build(seb_ctx *ctx, const seb_keys *keys, uint8_t *bits, uint64_t num_bits, uint32_t num_hashes,
+              uint32_t flags);
+int seb_probe(seb_ctx *ctx, const seb_keys *keys, const uint8_t *bits, uint64_t num_bits,
+              uint32_t num_hashes, uint8_t *out);
+int seb_probe_multi(seb_ctx *ctx, const seb_keys *keys, const seb_filter_ref *filters, uint32_t num_filters,
+                    uint64_t *mask);
+
+/* ----------------------------------- Go API mirror (lsm/bloom.go, one call per Go method) ---- */
+/* A filter handle.  Its bit array lives in HBM (device-resident filter registry); a host copy is
+ * materialised on Encode.  Add() defers: keys are appended to a host arena and built in one
+ * batched launch at the next Encode / MayContain / flush (or when the arena passes a size cap).
+ * All functions are thread-safe; MayContain may be called concurrently on one filter. */
+typedef struct seb_filter seb_filter;
+
+/* NewBloomFilter(expectedKeys, falsePositiveRate)          lsm/bloom.go:19   (NULL + last_error
+ * when the sizing leaves the defined range, where Go's behaviour is implementation-defined) */
+seb_filter *seb_filter_new(int64_t expected_keys, double false_positive_rate);
+void seb_filter_free(seb_filter *f);
+/* (*BloomFilter).Add(key)                                    lsm/bloom.go:70 */
+int seb_filter_add(seb_filter *f, const uint8_t *key, uint64_t len);
+int seb_filter_add_batch(seb_filter *f, const seb_keys *keys);
+/* (*BloomFilter).MayContain(key) -> 1 / 0, or < 0 on error  lsm/bloom.go:82 */
+int seb_filter_may_contain(seb_filter *f, const uint8_t *key, uint64_t len);
+int seb_filter_may_contain_batch(seb_filter *f, const seb_keys *keys, uint8_t *out);
+/* (*BloomFilter).Encode() -> 12 + len(bits) bytes           lsm/bloom.go:96 */
+uint64_t seb_filter_encoded_size(seb_filter *f);
+int seb_filter_encode(seb_filter *f, uint8_t *out, uint64_t cap);
+/* DecodeBloomFilter(data) -> NULL when len < 12 (Go: nil)   lsm/bloom.go:105 */
+seb_filter *seb_filter_decode(const uint8_t *data, uint64_t len);
+/* Accessors and an explicit flush of deferred Adds. */
+uint64_t seb_filter_num_bits(const seb_filter *f);
+uint32_t seb_filter_num_hashes(const seb_filter *f);
+uint64_t seb_filter_pending(seb_filter *f);
+int seb_filter_flush(seb_filter *f);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SEB_BLOOM_H */

@@ -1,0 +1,738 @@
+// seb_host.cpp — the C ABI (include/seb_bloom.h): device-resident entry points, host-buffer
+// batched entry points with a chunked H2D -> kernel -> D2H pipeline, and the handle API that
+// mirrors lsm/bloom.go method for method.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/seb_bloom.h"
+#include "seb_kernels.h"
+
+namespace seb {
+int params(int64_t n, double p, uint64_t *m_out, uint32_t *k_out);
+}
+
+using namespace seb;
+
+// ------------------------------------------------------------------ errors ------------------
+
+static thread_local std::string t_err;
+
+static int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_err = buf;
+    return code;
+}
+
+#define HIP_OR_FAIL(expr)                                                                              \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess) return fail(SEB_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_));    \
+    } while (0)
+
+extern "C" const char *seb_last_error(void) { return t_err.c_str(); }
+extern "C" int seb_abi_version(void) { return SEB_ABI_VERSION; }
+
+// ------------------------------------------------------------------ helpers -----------------
+
+extern "C" uint64_t seb_num_bytes(uint64_t m) { return m / 8 + (m % 8 != 0); }
+extern "C" uint64_t seb_words_bytes(uint64_t m) { return (m / 128 + (m % 128 != 0)) * 16; }
+
+extern "C" int seb_params(int64_t n, double p, uint64_t *m, uint32_t *k) {
+    if (!m || !k) return fail(SEB_ERR_INVALID, "seb_params: null output");
+    if (seb::params(n, p, m, k) != 0)
+        return fail(SEB_ERR_RANGE, "seb_params: n=%lld p=%g outside the reference's defined range", (long long)n, p);
+    return SEB_OK;
+}
+
+static ModArg mod_arg(uint64_t m, uint32_t k) {
+    ModArg a{};
+    a.m = m;
+    a.k = k;
+    a.mu = UINT64_MAX / m;
+    a.c = (UINT64_MAX % m + 1) % m;  // 2^64 mod m
+    return a;
+}
+
+static int check_filter_args(uint64_t m, uint32_t k, const char *who) {
+    if (m == 0) return fail(SEB_ERR_INVALID, "%s: numBits == 0 (the reference panics: integer divide by zero)", who);
+    if (k > 4096) return fail(SEB_ERR_INVALID, "%s: numHashes %u > 4096", who, k);
+    return SEB_OK;
+}
+
+static int check_keys(const seb_keys *kb, const char *who) {
+    if (!kb) return fail(SEB_ERR_INVALID, "%s: null keys", who);
+    if (kb->reserved != 0) return fail(SEB_ERR_INVALID, "%s: keys.reserved must be 0", who);
+    if (kb->n > 0 && !kb->data && (kb->offsets || kb->stride != 0))
+        return fail(SEB_ERR_INVALID, "%s: null key data", who);
+    return SEB_OK;
+}
+
+static KeyBatch key_batch(const seb_keys *kb) {
+    return KeyBatch{kb->data, kb->offsets, kb->n, kb->stride};
+}
+
+static bool env_flag(const char *name, long *out) {
+    const char *v = getenv(name);
+    if (!v || !*v) return false;
+    *out = strtol(v, nullptr, 0);
+    return true;
+}
+
+static std::once_flag g_env_once;
+static void load_env() {
+    long cap;
+    if (env_flag("SEB_GRID_CAP", &cap)) set_grid_cap((unsigned)cap);
+}
+
+extern "C" int seb_device_check(int device) {
+    std::call_once(g_env_once, load_env);
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0)
+        return fail(SEB_ERR_DEVICE, "no HIP device (%s)", e != hipSuccess ? hipGetErrorString(e) : "count 0");
+    if (device < 0 || device >= count) return fail(SEB_ERR_DEVICE, "device %d out of range (count %d)", device, count);
+    hipDeviceProp_t prop;
+    HIP_OR_FAIL(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SEB_ERR_DEVICE, "device %d is %s; this library is built for gfx950 only", device, prop.gcnArchName);
+    return SEB_OK;
+}
+
+// ------------------------------------------------------- device-resident entry points --------
+
+extern "C" int seb_dev_clear(uint32_t *words, uint64_t m, void *stream) {
+    if (!words && m) return fail(SEB_ERR_INVALID, "seb_dev_clear: null words");
+    if (m == 0) return SEB_OK;
+    HIP_OR_FAIL(hipMemsetAsync(words, 0, seb_words_bytes(m), (hipStream_t)stream));
+    return SEB_OK;
+}
+
+extern "C" int seb_dev_build(const seb_keys *keys, uint32_t *words, uint64_t m, uint32_t k, void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc;
+    if ((rc = check_keys(keys, "seb_dev_build")) || (rc = check_filter_args(m, k, "seb_dev_build"))) return rc;
+    if (!words) return fail(SEB_ERR_INVALID, "seb_dev_build: null words");
+    HIP_OR_FAIL(launch_build(key_batch(keys), words, mod_arg(m, k), (hipStream_t)stream));
+    return SEB_OK;
+}
+
+extern "C" int seb_dev_probe(const seb_keys *keys, const uint32_t *words, uint64_t m, uint32_t k, uint8_t *out,
+                             void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc;
+    if ((rc = check_keys(keys, "seb_dev_probe")) || (rc = check_filter_args(m, k, "seb_dev_probe"))) return rc;
+    if (!words || (!out && keys->n)) return fail(SEB_ERR_INVALID, "seb_dev_probe: null words/out");
+    HIP_OR_FAIL(launch_probe(key_batch(keys), words, mod_arg(m, k), out, (hipStream_t)stream));
+    return SEB_OK;
+}
+
+static int fill_multi(const seb_filter_ref *filters, uint32_t nf, uint32_t mask_bytes, MultiArg *ma,
+                      const char *who) {
+    if (!filters || nf == 0) return fail(SEB_ERR_INVALID, "%s: no filters", who);
+    if (nf > (uint32_t)kMaxMulti) return fail(SEB_ERR_INVALID, "%s: %u filters > %d", who, nf, kMaxMulti);
+    if (!(mask_bytes == 1 || mask_bytes == 2 || mask_bytes == 4 || mask_bytes == 8) || nf > 8 * mask_bytes)
+        return fail(SEB_ERR_INVALID, "%s: mask_bytes %u cannot hold %u filters", who, mask_bytes, nf);
+    memset(ma, 0, sizeof *ma);
+    ma->nf = nf;
+    for (uint32_t f = 0; f < nf; ++f) {
+        int rc = check_filter_args(filters[f].num_bits, filters[f].num_hashes, who);
+        if (rc) return rc;
+        if (!filters[f].bits || filters[f].reserved) return fail(SEB_ERR_INVALID, "%s: bad filter %u", who, f);
+        ma->f[f].words = (const uint32_t *)filters[f].bits;
+        ma->f[f].md = mod_arg(filters[f].num_bits, filters[f].num_hashes);
+    }
+    return SEB_OK;
+}
+
+extern "C" int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *filters, uint32_t nf, void *mask,
+                                   uint32_t mask_bytes, void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc;
+    MultiArg ma;
+    if ((rc = check_keys(keys, "seb_dev_probe_multi")) ||
+        (rc = fill_multi(filters, nf, mask_bytes, &ma, "seb_dev_probe_multi")))
+        return rc;
+    if (!mask && keys->n) return fail(SEB_ERR_INVALID, "seb_dev_probe_multi: null mask");
+    HIP_OR_FAIL(launch_probe_multi(key_batch(keys), ma, mask, mask_bytes, (hipStream_t)stream));
+    return SEB_OK;
+}
+
+static const uint32_t kLdsMax = 160 * 1024;
+
+extern "C" int seb_dev_build_many(const seb_keys *keys, const uint64_t *key_begin, const seb_filter_ref *filters,
+                                  uint32_t nf, void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc;
+    if ((rc = check_keys(keys, "seb_dev_build_many"))) return rc;
+    if (!key_begin || (!filters && nf)) return fail(SEB_ERR_INVALID, "seb_dev_build_many: null arrays");
+    hipStream_t s = (hipStream_t)stream;
+    KeyBatch kb = key_batch(keys);
+    ManyArg ma;
+    memset(&ma, 0, sizeof ma);
+    uint32_t lds = 0;
+    auto flush = [&]() -> int {
+        if (ma.nf == 0) return SEB_OK;
+        HIP_OR_FAIL(launch_build_many_lds(kb, ma, lds, s));
+        memset(&ma, 0, sizeof ma);
+        lds = 0;
+        return SEB_OK;
+    };
+    for (uint32_t f = 0; f < nf; ++f) {
+        const uint64_t m = filters[f].num_bits;
+        const uint32_t k = filters[f].num_hashes;
+        if ((rc = check_filter_args(m, k, "seb_dev_build_many"))) return rc;
+        if (!filters[f].bits || key_begin[f + 1] < key_begin[f] || key_begin[f + 1] > keys->n)
+            return fail(SEB_ERR_INVALID, "seb_dev_build_many: bad filter %u", f);
+        const uint64_t wb = seb_words_bytes(m);
+        if (wb <= kLdsMax) {
+            ManyFilter &F = ma.f[ma.nf++];
+            F.words = (uint32_t *)filters[f].bits;
+            F.nwords = wb / 4;
+            F.key_begin = key_begin[f];
+            F.key_end = key_begin[f + 1];
+            F.md = mod_arg(m, k);
+            lds = std::max<uint32_t>(lds, (uint32_t)wb);
+            if (ma.nf == (uint32_t)kMaxMany && (rc = flush())) return rc;
+        } else {  // too large for one CU's LDS: grid-wide atomics over this filter's key range
+            KeyBatch sub = kb;
+            sub.n = key_begin[f + 1] - key_begin[f];
+            if (kb.offsets)
+                sub.offsets = kb.offsets + key_begin[f];
+            else
+                sub.data = kb.data + key_begin[f] * (uint64_t)kb.stride;
+            HIP_OR_FAIL(launch_build(sub, (uint32_t *)filters[f].bits, mod_arg(m, k), s));
+        }
+    }
+    return flush();
+}
+
+extern "C" int seb_dev_alloc(void **ptr, uint64_t bytes) {
+    if (!ptr) return fail(SEB_ERR_INVALID, "seb_dev_alloc: null");
+    hipError_t e = hipMalloc(ptr, bytes ? bytes : 16);
+    if (e != hipSuccess) return fail(SEB_ERR_NOMEM, "hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
+    return SEB_OK;
+}
+extern "C" int seb_dev_free(void *ptr) {
+    HIP_OR_FAIL(hipFree(ptr));
+    return SEB_OK;
+}
+extern "C" int seb_host_alloc(void **ptr, uint64_t bytes) {
+    if (!ptr) return fail(SEB_ERR_INVALID, "seb_host_alloc: null");
+    hipError_t e = hipHostMalloc(ptr, bytes ? bytes : 16, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(SEB_ERR_NOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
+    return SEB_OK;
+}
+extern "C" int seb_host_free(void *ptr) {
+    HIP_OR_FAIL(hipHostFree(ptr));
+    return SEB_OK;
+}
+extern "C" int seb_memcpy_h2d(void *dst, const void *src, uint64_t bytes, void *stream) {
+    HIP_OR_FAIL(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+    return SEB_OK;
+}
+extern "C" int seb_memcpy_d2h(void *dst, const void *src, uint64_t bytes, void *stream) {
+    HIP_OR_FAIL(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    return SEB_OK;
+}
+extern "C" int seb_stream_sync(void *stream) {
+    HIP_OR_FAIL(hipStreamSynchronize((hipStream_t)stream));
+    return SEB_OK;
+}
+
+// ------------------------------------------------------- contexts (host-buffer API) ----------
+
+struct DevBuf {
+    void *p = nullptr;
+    uint64_t cap = 0;
+    int reserve(uint64_t bytes) {
+        if (bytes <= cap) return SEB_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        uint64_t want = std::max<uint64_t>(bytes, 4096);
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) return fail(SEB_ERR_NOMEM, "hipMalloc(%llu): %s", (unsigned long long)want, hipGetErrorString(e));
+        cap = want;
+        return SEB_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct seb_ctx {
+    int device = 0;
+    std::mutex mu;
+    hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr;
+    hipEvent_t ev_h2d[2] = {}, ev_comp[2] = {}, ev_d2h[2] = {};
+    DevBuf keys[2], offs[2], out[2], words, filt;
+    uint64_t chunk_bytes = 64ull << 20;
+    std::vector<uint64_t> off_tmp[2];
+};
+
+extern "C" int seb_ctx_create(int device, seb_ctx **out) {
+    if (!out) return fail(SEB_ERR_INVALID, "seb_ctx_create: null out");
+    int rc = seb_device_check(device);
+    if (rc) return rc;
+    HIP_OR_FAIL(hipSetDevice(device));
+    seb_ctx *c = new seb_ctx();
+    c->device = device;
+    long cb;
+    if (env_flag("SEB_CHUNK_BYTES", &cb) && cb > 0) c->chunk_bytes = (uint64_t)cb;
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking);
+    for (int b = 0; b < 2 && e == hipSuccess; ++b) {
+        e = hipEventCreateWithFlags(&c->ev_h2d[b], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_comp[b], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_d2h[b], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) {
+        seb_ctx_destroy(c);
+        return fail(SEB_ERR_DEVICE, "seb_ctx_create: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return SEB_OK;
+}
+
+extern "C" void seb_ctx_destroy(seb_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->s_comp) (void)hipStreamSynchronize(c->s_comp);
+    for (int b = 0; b < 2; ++b) {
+        c->keys[b].release();
+        c->offs[b].release();
+        c->out[b].release();
+        if (c->ev_h2d[b]) (void)hipEventDestroy(c->ev_h2d[b]);
+        if (c->ev_comp[b]) (void)hipEventDestroy(c->ev_comp[b]);
+        if (c->ev_d2h[b]) (void)hipEventDestroy(c->ev_d2h[b]);
+    }
+    c->words.release();
+    c->filt.release();
+    if (c->s_h2d) (void)hipStreamDestroy(c->s_h2d);
+    if (c->s_comp) (void)hipStreamDestroy(c->s_comp);
+    if (c->s_d2h) (void)hipStreamDestroy(c->s_d2h);
+    delete c;
+}
+
+// Host key batch -> sequence of chunks [i0, i1) whose key bytes fit the chunk budget.
+struct Chunk {
+    uint64_t i0, i1, byte0, byte1;
+};
+
+static void plan_chunks(const seb_keys *kb, uint64_t budget, std::vector<Chunk> &out) {
+    out.clear();
+    const uint64_t n = kb->n;
+    if (n == 0) return;
+    if (!kb->offsets) {
+        uint64_t per = kb->stride ? std::max<uint64_t>(1, budget / kb->stride) : n;
+        for (uint64_t i = 0; i < n; i += per) {
+            uint64_t j = std::min(n, i + per);
+            out.push_back({i, j, i * kb->stride, j * kb->stride});
+        }
+        return;
+    }
+    const uint64_t *o = kb->offsets;
+    uint64_t i = 0;
+    while (i < n) {
+        // largest j with o[j] - o[i] <= budget (at least one key)
+        uint64_t lo = i + 1, hi = n;
+        while (lo < hi) {
+            uint64_t mid = lo + (hi - lo + 1) / 2;
+            if (o[mid] - o[i] <= budget) lo = mid; else hi = mid - 1;
+        }
+        out.push_back({i, lo, o[i], o[lo]});
+        i = lo;
+    }
+}
+
+static int validate_offsets(const seb_keys *kb, const char *who) {
+    if (!kb->offsets) return SEB_OK;
+    for (uint64_t i = 0; i < kb->n; ++i)
+        if (kb->offsets[i + 1] < kb->offsets[i]) return fail(SEB_ERR_INVALID, "%s: offsets decrease at %llu", who, (unsigned long long)i);
+    return SEB_OK;
+}
+
+// Stage one chunk of host keys into buffer b on s_h2d; returns the device KeyBatch for it.
+static int stage_chunk(seb_ctx *c, const seb_keys *kb, const Chunk &ch, int b, KeyBatch *dk) {
+    int rc;
+    const uint64_t bytes = ch.byte1 - ch.byte0;
+    if ((rc = c->keys[b].reserve(bytes + 16))) return rc;
+    HIP_OR_FAIL(hipStreamWaitEvent(c->s_h2d, c->ev_comp[b], 0));  // buffer b no longer read
+    if (bytes) HIP_OR_FAIL(hipMemcpyAsync(c->keys[b].p, kb->data + ch.byte0, bytes, hipMemcpyHostToDevice, c->s_h2d));
+    dk->n = ch.i1 - ch.i0;
+    dk->stride = kb->stride;
+    if (kb->offsets) {
+        const uint64_t cnt = dk->n + 1;
+        if ((rc = c->offs[b].reserve(cnt * 8))) return rc;
+        HIP_OR_FAIL(hipMemcpyAsync(c->offs[b].p, kb->offsets + ch.i0, cnt * 8, hipMemcpyHostToDevice, c->s_h2d));
+        dk->offsets = (const uint64_t *)c->offs[b].p;
+        dk->data = (const uint8_t *)c->keys[b].p - ch.byte0;  // offsets are absolute
+    } else {
+        dk->offsets = nullptr;
+        dk->data = (const uint8_t *)c->keys[b].p;
+    }
+    HIP_OR_FAIL(hipEventRecord(c->ev_h2d[b], c->s_h2d));
+    HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_h2d[b], 0));
+    return SEB_OK;
+}
+
+// OR host keys into device words (all on c->s_comp ordering), chunked + double buffered.
+static int build_device_from_host(seb_ctx *c, const seb_keys *kb, uint32_t *dwords, const ModArg &md) {
+    std::vector<Chunk> chunks;
+    plan_chunks(kb, c->chunk_bytes, chunks);
+    for (size_t j = 0; j < chunks.size(); ++j) {
+        const int b = (int)(j & 1);
+        KeyBatch dk{};
+        int rc = stage_chunk(c, kb, chunks[j], b, &dk);
+        if (rc) return rc;
+        HIP_OR_FAIL(launch_build(dk, dwords, md, c->s_comp));
+        HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
+    }
+    return SEB_OK;
+}
+
+static int probe_device_to_host(seb_ctx *c, const seb_keys *kb, const uint32_t *dwords, const ModArg &md,
+                                uint8_t *out) {
+    std::vector<Chunk> chunks;
+    plan_chunks(kb, c->chunk_bytes, chunks);
+    for (size_t j = 0; j < chunks.size(); ++j) {
+        const int b = (int)(j & 1);
+        KeyBatch dk{};
+        int rc = stage_chunk(c, kb, chunks[j], b, &dk);
+        if (rc) return rc;
+        const uint64_t cnt = dk.n;
+        if ((rc = c->out[b].reserve(cnt))) return rc;
+        HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));  // out[b] drained
+        HIP_OR_FAIL(launch_probe(dk, dwords, md, (uint8_t *)c->out[b].p, c->s_comp));
+        HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
+        HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
+        HIP_OR_FAIL(hipMemcpyAsync(out + chunks[j].i0, c->out[b].p, cnt, hipMemcpyDeviceToHost, c->s_d2h));
+        HIP_OR_FAIL(hipEventRecord(c->ev_d2h[b], c->s_d2h));
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(c->s_d2h));
+    return SEB_OK;
+}
+
+extern "C" int seb_build(seb_ctx *c, const seb_keys *kb, uint8_t *bits, uint64_t m, uint32_t k, uint32_t flags) {
+    int rc;
+    if (!c) return fail(SEB_ERR_INVALID, "seb_build: null ctx");
+    if ((rc = check_keys(kb, "seb_build")) || (rc = check_filter_args(m, k, "seb_build")) ||
+        (rc = validate_offsets(kb, "seb_build")))
+        return rc;
+    if (!bits) return fail(SEB_ERR_INVALID, "seb_build: null bits");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OR_FAIL(hipSetDevice(c->device));
+    const uint64_t wb = seb_words_bytes(m), nb = seb_num_bytes(m);
+    if ((rc = c->words.reserve(wb))) return rc;
+    uint32_t *dw = (uint32_t *)c->words.p;
+    HIP_OR_FAIL(hipMemsetAsync(dw, 0, wb, c->s_comp));
+    if (!(flags & SEB_BUILD_FRESH)) HIP_OR_FAIL(hipMemcpyAsync(dw, bits, nb, hipMemcpyHostToDevice, c->s_comp));
+    if ((rc = build_device_from_host(c, kb, dw, mod_arg(m, k)))) return rc;
+    HIP_OR_FAIL(hipMemcpyAsync(bits, dw, nb, hipMemcpyDeviceToHost, c->s_comp));
+    HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));
+    return SEB_OK;
+}
+
+extern "C" int seb_probe(seb_ctx *c, const seb_keys *kb, const uint8_t *bits, uint64_t m, uint32_t k, uint8_t *out) {
+    int rc;
+    if (!c) return fail(SEB_ERR_INVALID, "seb_probe: null ctx");
+    if ((rc = check_keys(kb, "seb_probe")) || (rc = check_filter_args(m, k, "seb_probe")) ||
+        (rc = validate_offsets(kb, "seb_probe")))
+        return rc;
+    if (!bits || (!out && kb->n)) return fail(SEB_ERR_INVALID, "seb_probe: null bits/out");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OR_FAIL(hipSetDevice(c->device));
+    const uint64_t wb = seb_words_bytes(m), nb = seb_num_bytes(m);
+    if ((rc = c->words.reserve(wb))) return rc;
+    uint32_t *dw = (uint32_t *)c->words.p;
+    HIP_OR_FAIL(hipMemsetAsync(dw, 0, wb, c->s_comp));
+    HIP_OR_FAIL(hipMemcpyAsync(dw, bits, nb, hipMemcpyHostToDevice, c->s_comp));
+    return probe_device_to_host(c, kb, dw, mod_arg(m, k), out);
+}
+
+extern "C" int seb_probe_multi(seb_ctx *c, const seb_keys *kb, const seb_filter_ref *filters, uint32_t nf,
+                               uint64_t *mask) {
+    int rc;
+    if (!c) return fail(SEB_ERR_INVALID, "seb_probe_multi: null ctx");
+    if ((rc = check_keys(kb, "seb_probe_multi")) || (rc = validate_offsets(kb, "seb_probe_multi"))) return rc;
+    if (!mask && kb->n) return fail(SEB_ERR_INVALID, "seb_probe_multi: null mask");
+    if (!filters || nf == 0 || nf > (uint32_t)kMaxMulti) return fail(SEB_ERR_INVALID, "seb_probe_multi: bad filter count");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OR_FAIL(hipSetDevice(c->device));
+    uint64_t total = 0;
+    std::vector<uint64_t> at(nf);
+    for (uint32_t f = 0; f < nf; ++f) {
+        if ((rc = check_filter_args(filters[f].num_bits, filters[f].num_hashes, "seb_probe_multi"))) return rc;
+        if (!filters[f].bits) return fail(SEB_ERR_INVALID, "seb_probe_multi: null bits %u", f);
+        at[f] = total;
+        total += seb_words_bytes(filters[f].num_bits);
+    }
+    if ((rc = c->filt.reserve(total))) return rc;
+    HIP_OR_FAIL(hipMemsetAsync(c->filt.p, 0, total, c->s_comp));
+    std::vector<seb_filter_ref> dref(filters, filters + nf);
+    for (uint32_t f = 0; f < nf; ++f) {
+        uint8_t *d = (uint8_t *)c->filt.p + at[f];
+        HIP_OR_FAIL(hipMemcpyAsync(d, filters[f].bits, seb_num_bytes(filters[f].num_bits), hipMemcpyHostToDevice, c->s_comp));
+        dref[f].bits = d;
+    }
+    MultiArg ma;
+    if ((rc = fill_multi(dref.data(), nf, 8, &ma, "seb_probe_multi"))) return rc;
+    std::vector<Chunk> chunks;
+    plan_chunks(kb, c->chunk_bytes, chunks);
+    for (size_t j = 0; j < chunks.size(); ++j) {
+        const int b = (int)(j & 1);
+        KeyBatch dk{};
+        if ((rc = stage_chunk(c, kb, chunks[j], b, &dk))) return rc;
+        if ((rc = c->out[b].reserve(dk.n * 8))) return rc;
+        HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));
+        HIP_OR_FAIL(launch_probe_multi(dk, ma, c->out[b].p, 8, c->s_comp));
+        HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
+        HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
+        HIP_OR_FAIL(hipMemcpyAsync(mask + chunks[j].i0, c->out[b].p, dk.n * 8, hipMemcpyDeviceToHost, c->s_d2h));
+        HIP_OR_FAIL(hipEventRecord(c->ev_d2h[b], c->s_d2h));
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(c->s_d2h));
+    return SEB_OK;
+}
+
+// ------------------------------------------------ Go API mirror (lsm/bloom.go handles) -------
+
+static std::mutex g_pool_mu;
+static std::vector<seb_ctx *> g_pool;
+
+static int default_device() {
+    long d;
+    return env_flag("SEB_DEVICE", &d) ? (int)d : 0;
+}
+
+struct CtxLease {  // borrow a context from the process pool (concurrent filters do not serialise)
+    seb_ctx *c = nullptr;
+    int rc = SEB_OK;
+    explicit CtxLease(int device) {
+        {
+            std::lock_guard<std::mutex> g(g_pool_mu);
+            for (size_t i = 0; i < g_pool.size(); ++i)
+                if (g_pool[i]->device == device) {
+                    c = g_pool[i];
+                    g_pool.erase(g_pool.begin() + i);
+                    break;
+                }
+        }
+        if (!c) rc = seb_ctx_create(device, &c);
+    }
+    ~CtxLease() {
+        if (c) {
+            std::lock_guard<std::mutex> g(g_pool_mu);
+            g_pool.push_back(c);
+        }
+    }
+};
+
+struct seb_filter {
+    std::mutex mu;
+    uint64_t m = 0;
+    uint32_t k = 0;
+    uint64_t nbytes = 0;  // len(bits): ceil(m/8) for New, len(data)-12 for Decode
+    int device = 0;
+    uint32_t *dwords = nullptr;  // HBM copy, authoritative once allocated
+    uint64_t dbytes = 0;
+    std::vector<uint8_t> host;  // host copy (valid when host_ok)
+    bool host_ok = true;
+    std::vector<uint8_t> pend;       // deferred Add arena
+    std::vector<uint64_t> pend_off;  // n+1 offsets into pend
+    uint64_t pend_cap = 64ull << 20;
+};
+
+static int ensure_device_copy(seb_filter *f) {
+    if (f->dwords) return SEB_OK;
+    HIP_OR_FAIL(hipSetDevice(f->device));
+    f->dbytes = std::max<uint64_t>(seb_words_bytes(f->m), (f->nbytes + 15) / 16 * 16);
+    if (f->dbytes == 0) f->dbytes = 16;
+    hipError_t e = hipMalloc((void **)&f->dwords, f->dbytes);
+    if (e != hipSuccess) {
+        f->dwords = nullptr;
+        return fail(SEB_ERR_NOMEM, "filter: hipMalloc(%llu): %s", (unsigned long long)f->dbytes, hipGetErrorString(e));
+    }
+    HIP_OR_FAIL(hipMemset(f->dwords, 0, f->dbytes));
+    if (f->nbytes) HIP_OR_FAIL(hipMemcpy(f->dwords, f->host.data(), f->nbytes, hipMemcpyHostToDevice));
+    return SEB_OK;
+}
+
+static int usable(seb_filter *f, const char *who) {
+    int rc = check_filter_args(f->m, f->k, who);
+    if (rc) return rc;
+    if (f->nbytes < seb_num_bytes(f->m))
+        return fail(SEB_ERR_SHORT, "%s: decoded bits (%llu B) shorter than ceil(numBits/8) (%llu B); the reference "
+                    "panics (index out of range)", who, (unsigned long long)f->nbytes,
+                    (unsigned long long)seb_num_bytes(f->m));
+    return SEB_OK;
+}
+
+static int flush_locked(seb_filter *f) {
+    if (f->pend_off.size() <= 1) return SEB_OK;
+    int rc = usable(f, "BloomFilter.Add");
+    if (rc) return rc;
+    if ((rc = ensure_device_copy(f))) return rc;
+    CtxLease L(f->device);
+    if (L.rc) return L.rc;
+    seb_keys kb{f->pend.data(), f->pend_off.data(), f->pend_off.size() - 1, 0, 0};
+    std::lock_guard<std::mutex> g(L.c->mu);
+    HIP_OR_FAIL(hipSetDevice(f->device));
+    if ((rc = build_device_from_host(L.c, &kb, f->dwords, mod_arg(f->m, f->k)))) return rc;
+    HIP_OR_FAIL(hipStreamSynchronize(L.c->s_comp));
+    f->pend.clear();
+    f->pend_off.assign(1, 0);
+    f->host_ok = false;
+    return SEB_OK;
+}
+
+extern "C" seb_filter *seb_filter_new(int64_t n, double p) {
+    uint64_t m;
+    uint32_t k;
+    if (seb_params(n, p, &m, &k) != SEB_OK) return nullptr;
+    seb_filter *f = new (std::nothrow) seb_filter();
+    if (!f) return nullptr;
+    f->m = m;
+    f->k = k;
+    f->nbytes = seb_num_bytes(m);
+    f->device = default_device();
+    f->host.assign(f->nbytes, 0);
+    f->pend_off.assign(1, 0);
+    long cap;
+    if (env_flag("SEB_PENDING_CAP", &cap) && cap > 0) f->pend_cap = (uint64_t)cap;
+    return f;
+}
+
+extern "C" void seb_filter_free(seb_filter *f) {
+    if (!f) return;
+    if (f->dwords) {
+        (void)hipSetDevice(f->device);
+        (void)hipFree(f->dwords);
+    }
+    delete f;
+}
+
+extern "C" int seb_filter_add(seb_filter *f, const uint8_t *key, uint64_t len) {
+    if (!f || (!key && len)) return fail(SEB_ERR_INVALID, "BloomFilter.Add: null argument");
+    std::lock_guard<std::mutex> g(f->mu);
+    int rc = usable(f, "BloomFilter.Add");
+    if (rc) return rc;
+    f->pend.insert(f->pend.end(), key, key + len);
+    f->pend_off.push_back(f->pend.size());
+    if (f->pend.size() >= f->pend_cap) return flush_locked(f);
+    return SEB_OK;
+}
+
+extern "C" int seb_filter_add_batch(seb_filter *f, const seb_keys *kb) {
+    if (!f) return fail(SEB_ERR_INVALID, "BloomFilter.Add: null filter");
+    int rc;
+    if ((rc = check_keys(kb, "BloomFilter.Add")) || (rc = validate_offsets(kb, "BloomFilter.Add"))) return rc;
+    std::lock_guard<std::mutex> g(f->mu);
+    if ((rc = usable(f, "BloomFilter.Add"))) return rc;
+    if ((rc = flush_locked(f))) return rc;  // keep Add order: earlier single Adds first
+    if ((rc = ensure_device_copy(f))) return rc;
+    CtxLease L(f->device);
+    if (L.rc) return L.rc;
+    std::lock_guard<std::mutex> g2(L.c->mu);
+    HIP_OR_FAIL(hipSetDevice(f->device));
+    if ((rc = build_device_from_host(L.c, kb, f->dwords, mod_arg(f->m, f->k)))) return rc;
+    HIP_OR_FAIL(hipStreamSynchronize(L.c->s_comp));
+    f->host_ok = false;
+    return SEB_OK;
+}
+
+extern "C" int seb_filter_may_contain_batch(seb_filter *f, const seb_keys *kb, uint8_t *out) {
+    if (!f) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: null filter");
+    int rc;
+    if ((rc = check_keys(kb, "BloomFilter.MayContain")) || (rc = validate_offsets(kb, "BloomFilter.MayContain")))
+        return rc;
+    if (!out && kb->n) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: null out");
+    std::lock_guard<std::mutex> g(f->mu);
+    if ((rc = usable(f, "BloomFilter.MayContain"))) return rc;
+    if ((rc = flush_locked(f))) return rc;
+    if ((rc = ensure_device_copy(f))) return rc;
+    CtxLease L(f->device);
+    if (L.rc) return L.rc;
+    std::lock_guard<std::mutex> g2(L.c->mu);
+    HIP_OR_FAIL(hipSetDevice(f->device));
+    return probe_device_to_host(L.c, kb, f->dwords, mod_arg(f->m, f->k), out);
+}
+
+extern "C" int seb_filter_may_contain(seb_filter *f, const uint8_t *key, uint64_t len) {
+    if (!key && len) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: null key");
+    static const uint8_t empty = 0;
+    seb_keys kb{key ? key : &empty, nullptr, 1, (uint32_t)len, 0};
+    if (len > 0xffffffffull) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: key too long");
+    uint8_t ans = 0;
+    int rc = seb_filter_may_contain_batch(f, &kb, &ans);
+    return rc ? rc : (int)ans;
+}
+
+static int sync_host_locked(seb_filter *f) {
+    if (f->host_ok) return SEB_OK;
+    HIP_OR_FAIL(hipSetDevice(f->device));
+    f->host.resize(f->nbytes);
+    if (f->nbytes) HIP_OR_FAIL(hipMemcpy(f->host.data(), f->dwords, f->nbytes, hipMemcpyDeviceToHost));
+    f->host_ok = true;
+    return SEB_OK;
+}
+
+extern "C" uint64_t seb_filter_encoded_size(seb_filter *f) { return f ? 12 + f->nbytes : 0; }
+
+extern "C" int seb_filter_encode(seb_filter *f, uint8_t *out, uint64_t cap) {
+    if (!f || !out) return fail(SEB_ERR_INVALID, "BloomFilter.Encode: null argument");
+    std::lock_guard<std::mutex> g(f->mu);
+    if (cap < 12 + f->nbytes) return fail(SEB_ERR_INVALID, "BloomFilter.Encode: buffer too small");
+    int rc;
+    if ((rc = flush_locked(f)) || (rc = sync_host_locked(f))) return rc;
+    for (int b = 0; b < 8; ++b) out[b] = (uint8_t)(f->m >> (8 * b));  // binary.LittleEndian
+    for (int b = 0; b < 4; ++b) out[8 + b] = (uint8_t)(f->k >> (8 * b));
+    if (f->nbytes) memcpy(out + 12, f->host.data(), f->nbytes);
+    return SEB_OK;
+}
+
+extern "C" seb_filter *seb_filter_decode(const uint8_t *data, uint64_t len) {
+    if (!data || len < 12) {
+        fail(SEB_ERR_INVALID, "DecodeBloomFilter: %llu bytes < 12 (Go returns nil)", (unsigned long long)len);
+        return nullptr;
+    }
+    seb_filter *f = new (std::nothrow) seb_filter();
+    if (!f) return nullptr;
+    for (int b = 0; b < 8; ++b) f->m |= (uint64_t)data[b] << (8 * b);
+    for (int b = 0; b < 4; ++b) f->k |= (uint32_t)data[8 + b] << (8 * b);
+    f->nbytes = len - 12;
+    f->device = default_device();
+    f->host.assign(data + 12, data + len);
+    f->pend_off.assign(1, 0);
+    return f;
+}
+
+extern "C" uint64_t seb_filter_num_bits(const seb_filter *f) { return f ? f->m : 0; }
+extern "C" uint32_t seb_filter_num_hashes(const seb_filter *f) { return f ? f->k : 0; }
+extern "C" uint64_t seb_filter_pending(seb_filter *f) {
+    if (!f) return 0;
+    std::lock_guard<std::mutex> g(f->mu);
+    return f->pend_off.size() - 1;
+}
+extern "C" int seb_filter_flush(seb_filter *f) {
+    if (!f) return fail(SEB_ERR_INVALID, "flush: null filter");
+    std::lock_guard<std::mutex> g(f->mu);
+    return flush_locked(f);
+}

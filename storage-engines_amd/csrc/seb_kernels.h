@@ -1,0 +1,55 @@
+// seb_kernels.h — internal interface between the C-ABI host layer and the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace seb {
+
+// Reduction constants for one filter, computed on the host (seb_host.cpp: mod_arg()).
+struct ModArg {
+    uint64_t m;   // numBits (>= 1)
+    uint64_t mu;  // floor((2^64 - 1) / m)
+    uint64_t c;   // 2^64 mod m
+    uint32_t k;   // numHashes
+    uint32_t pad;
+};
+
+struct KeyBatch {  // device pointers
+    const uint8_t *data;
+    const uint64_t *offsets;  // n+1 or nullptr
+    uint64_t n;
+    uint32_t stride;
+};
+
+constexpr int kMaxMulti = 64;
+struct MultiFilter {
+    const uint32_t *words;
+    ModArg md;
+};
+struct MultiArg {  // passed by value (kernel arguments), <= 64 filters
+    MultiFilter f[kMaxMulti];
+    uint32_t nf;
+    uint32_t pad;
+};
+
+constexpr int kMaxMany = 32;
+struct ManyFilter {
+    uint32_t *words;
+    uint64_t nwords;
+    uint64_t key_begin, key_end;
+    ModArg md;
+};
+struct ManyArg {
+    ManyFilter f[kMaxMany];
+    uint32_t nf;
+    uint32_t pad;
+};
+
+hipError_t launch_build(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s);
+hipError_t launch_probe(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s);
+hipError_t launch_probe_multi(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes,
+                              hipStream_t s);
+hipError_t launch_build_many_lds(const KeyBatch &kb, const ManyArg &ma, uint32_t lds_bytes, hipStream_t s);
+void set_grid_cap(unsigned cap);
+
+}  // namespace seb

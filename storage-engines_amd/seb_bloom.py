@@ -1,0 +1,342 @@
+"""Python host binding of libseb_bloom.so (the C ABI in include/seb_bloom.h), via ctypes.
+
+`BloomFilter` mirrors the reference's Go API (lsm/bloom.go) one method per method, so the
+parity tests read like the reference's own call sequences:
+
+    NewBloomFilter(expectedKeys, fpr)  lsm/bloom.go:19   -> BloomFilter(n, p)
+    (*BloomFilter).Add(key)            lsm/bloom.go:70   -> .add(key)            (deferred, batched)
+    (*BloomFilter).MayContain(key)     lsm/bloom.go:82   -> .may_contain(key)
+    (*BloomFilter).Encode()            lsm/bloom.go:96   -> .encode()
+    DecodeBloomFilter(data)            lsm/bloom.go:105  -> BloomFilter.decode(data)  (None if < 12 B)
+
+Every computation runs in the HIP library on the GPU.  There is no CPU fallback: if the
+library is missing or no gfx950 device is present, calls raise SebError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libseb_bloom.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "seb_bloom.h")
+
+SEB_OK = 0
+SEB_BUILD_FRESH = 1
+ERRORS = {-1: "SEB_ERR_INVALID", -2: "SEB_ERR_DEVICE", -3: "SEB_ERR_NOMEM", -4: "SEB_ERR_RANGE", -5: "SEB_ERR_SHORT"}
+
+
+class SebError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class seb_keys(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("offsets", C.c_void_p), ("n", C.c_uint64), ("stride", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+class seb_filter_ref(C.Structure):
+    _fields_ = [("bits", C.c_void_p), ("num_bits", C.c_uint64), ("num_hashes", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+_lib = None
+_vp = C.c_void_p
+_u64 = C.c_uint64
+_u32 = C.c_uint32
+_i = C.c_int
+
+_SIGS = {
+    "seb_params": (_i, [C.c_int64, C.c_double, C.POINTER(_u64), C.POINTER(_u32)]),
+    "seb_num_bytes": (_u64, [_u64]),
+    "seb_words_bytes": (_u64, [_u64]),
+    "seb_abi_version": (_i, []),
+    "seb_last_error": (C.c_char_p, []),
+    "seb_device_check": (_i, [_i]),
+    "seb_dev_clear": (_i, [_vp, _u64, _vp]),
+    "seb_dev_build": (_i, [C.POINTER(seb_keys), _vp, _u64, _u32, _vp]),
+    "seb_dev_probe": (_i, [C.POINTER(seb_keys), _vp, _u64, _u32, _vp, _vp]),
+    "seb_dev_probe_multi": (_i, [C.POINTER(seb_keys), C.POINTER(seb_filter_ref), _u32, _vp, _u32, _vp]),
+    "seb_dev_build_many": (_i, [C.POINTER(seb_keys), C.POINTER(_u64), C.POINTER(seb_filter_ref), _u32, _vp]),
+    "seb_dev_alloc": (_i, [C.POINTER(_vp), _u64]),
+    "seb_dev_free": (_i, [_vp]),
+    "seb_host_alloc": (_i, [C.POINTER(_vp), _u64]),
+    "seb_host_free": (_i, [_vp]),
+    "seb_memcpy_h2d": (_i, [_vp, _vp, _u64, _vp]),
+    "seb_memcpy_d2h": (_i, [_vp, _vp, _u64, _vp]),
+    "seb_stream_sync": (_i, [_vp]),
+    "seb_ctx_create": (_i, [_i, C.POINTER(_vp)]),
+    "seb_ctx_destroy": (None, [_vp]),
+    "seb_build": (_i, [_vp, C.POINTER(seb_keys), _vp, _u64, _u32, _u32]),
+    "seb_probe": (_i, [_vp, C.POINTER(seb_keys), _vp, _u64, _u32, _vp]),
+    "seb_probe_multi": (_i, [_vp, C.POINTER(seb_keys), C.POINTER(seb_filter_ref), _u32, _vp]),
+    "seb_filter_new": (_vp, [C.c_int64, C.c_double]),
+    "seb_filter_free": (None, [_vp]),
+    "seb_filter_add": (_i, [_vp, _vp, _u64]),
+    "seb_filter_add_batch": (_i, [_vp, C.POINTER(seb_keys)]),
+    "seb_filter_may_contain": (_i, [_vp, _vp, _u64]),
+    "seb_filter_may_contain_batch": (_i, [_vp, C.POINTER(seb_keys), _vp]),
+    "seb_filter_encoded_size": (_u64, [_vp]),
+    "seb_filter_encode": (_i, [_vp, _vp, _u64]),
+    "seb_filter_decode": (_vp, [_vp, _u64]),
+    "seb_filter_num_bits": (_u64, [_vp]),
+    "seb_filter_num_hashes": (_u32, [_vp]),
+    "seb_filter_pending": (_u64, [_vp]),
+    "seb_filter_flush": (_i, [_vp]),
+}
+
+
+def build_library() -> str:
+    """Compile libseb_bloom.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(_HERE, "csrc")], check=True)
+    return LIB_PATH
+
+
+def lib():
+    """Load the HIP library; raises if it was not built (no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SebError(-2, f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
+        try:  # share torch's HIP runtime when torch is in the process (same SONAME)
+            import torch  # noqa: F401
+        except Exception:
+            pass
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return (lib().seb_last_error() or b"").decode()
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise SebError(rc, last_error())
+    return rc
+
+
+def params(n: int, p: float) -> tuple[int, int]:
+    m, k = _u64(), _u32()
+    check(lib().seb_params(n, p, C.byref(m), C.byref(k)))
+    return m.value, k.value
+
+
+def num_bytes(m: int) -> int:
+    return lib().seb_num_bytes(m)
+
+
+def words_bytes(m: int) -> int:
+    return lib().seb_words_bytes(m)
+
+
+def device_check(device: int = 0) -> None:
+    check(lib().seb_device_check(device))
+
+
+# ------------------------------------------------------------------ key batches (host) ----
+
+class HostKeys:
+    """A host key batch: fixed-stride (n, L) uint8 array, or (data, offsets) variable-length."""
+
+    def __init__(self, data: np.ndarray, offsets: np.ndarray | None = None):
+        if offsets is None:
+            arr = np.ascontiguousarray(data, dtype=np.uint8)
+            if arr.ndim != 2:
+                raise ValueError("fixed-length keys must be a 2-D (n, L) uint8 array")
+            self.n, self.stride = arr.shape
+            self.data = arr
+            self.offsets = None
+        else:
+            self.data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+            self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+            self.n = self.offsets.shape[0] - 1
+            self.stride = 0
+        self._s = seb_keys(self.data.ctypes.data if self.data.size else None,
+                           self.offsets.ctypes.data if self.offsets is not None else None,
+                           self.n, self.stride, 0)
+
+    @property
+    def ref(self):
+        return C.byref(self._s)
+
+
+def as_keys(keys) -> HostKeys:
+    if isinstance(keys, HostKeys):
+        return keys
+    if isinstance(keys, tuple):
+        return HostKeys(keys[0], keys[1])
+    if isinstance(keys, (list,)):
+        lens = np.array([len(k) for k in keys], dtype=np.uint64)
+        off = np.zeros(len(keys) + 1, dtype=np.uint64)
+        np.cumsum(lens, out=off[1:])
+        data = np.frombuffer(b"".join(keys), dtype=np.uint8) if len(keys) else np.zeros(0, np.uint8)
+        return HostKeys(data, off)
+    return HostKeys(keys)
+
+
+# ------------------------------------------------------------------ host-buffer API ------
+
+class Ctx:
+    """seb_ctx: streams + scratch on one device; host-buffer build / probe (PCIe-inclusive)."""
+
+    def __init__(self, device: int = 0):
+        p = _vp()
+        check(lib().seb_ctx_create(device, C.byref(p)))
+        self._p = p
+
+    def close(self):
+        if self._p:
+            lib().seb_ctx_destroy(self._p)
+            self._p = None
+
+    __del__ = close
+
+    def build(self, keys, m: int, k: int, bits: np.ndarray | None = None) -> np.ndarray:
+        kb = as_keys(keys)
+        fresh = bits is None
+        out = np.zeros(num_bytes(m), dtype=np.uint8) if fresh else bits
+        check(lib().seb_build(self._p, kb.ref, out.ctypes.data, m, k, SEB_BUILD_FRESH if fresh else 0))
+        return out
+
+    def probe(self, keys, bits: np.ndarray, m: int, k: int) -> np.ndarray:
+        kb = as_keys(keys)
+        out = np.zeros(max(kb.n, 1), dtype=np.uint8)
+        bits = np.ascontiguousarray(bits, dtype=np.uint8)
+        check(lib().seb_probe(self._p, kb.ref, bits.ctypes.data, m, k, out.ctypes.data))
+        return out[: kb.n]
+
+    def probe_multi(self, keys, filters: list[tuple[np.ndarray, int, int]]) -> np.ndarray:
+        kb = as_keys(keys)
+        keep = [np.ascontiguousarray(b, dtype=np.uint8) for b, _, _ in filters]
+        refs = (seb_filter_ref * len(filters))(*[seb_filter_ref(b.ctypes.data, m, k, 0)
+                                                  for b, (_, m, k) in zip(keep, filters)])
+        out = np.zeros(max(kb.n, 1), dtype=np.uint64)
+        check(lib().seb_probe_multi(self._p, kb.ref, refs, len(filters), out.ctypes.data))
+        return out[: kb.n]
+
+
+# ------------------------------------------------------------- Go API mirror (handles) ----
+
+class BloomFilter:
+    """lsm/bloom.go's BloomFilter, backed by an HBM-resident bit array in libseb_bloom."""
+
+    def __init__(self, expected_keys: int | None = None, fpr: float = 0.01, *, _handle=None):
+        if _handle is None:
+            _handle = lib().seb_filter_new(expected_keys, fpr)
+            if not _handle:
+                raise SebError(-4, last_error())
+        self._h = _handle
+
+    @classmethod
+    def decode(cls, data: bytes):
+        buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+        h = lib().seb_filter_decode(buf.ctypes.data, len(data))
+        return cls(_handle=h) if h else None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().seb_filter_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    @property
+    def num_bits(self) -> int:
+        return lib().seb_filter_num_bits(self._h)
+
+    @property
+    def num_hashes(self) -> int:
+        return lib().seb_filter_num_hashes(self._h)
+
+    @property
+    def pending(self) -> int:
+        return lib().seb_filter_pending(self._h)
+
+    def add(self, key: bytes) -> None:
+        check(lib().seb_filter_add(self._h, key, len(key)))
+
+    def add_batch(self, keys) -> None:
+        kb = as_keys(keys)
+        check(lib().seb_filter_add_batch(self._h, kb.ref))
+
+    def may_contain(self, key: bytes) -> bool:
+        return bool(check(lib().seb_filter_may_contain(self._h, key, len(key))))
+
+    def may_contain_batch(self, keys) -> np.ndarray:
+        kb = as_keys(keys)
+        out = np.zeros(max(kb.n, 1), dtype=np.uint8)
+        check(lib().seb_filter_may_contain_batch(self._h, kb.ref, out.ctypes.data))
+        return out[: kb.n]
+
+    def flush(self) -> None:
+        check(lib().seb_filter_flush(self._h))
+
+    def encode(self) -> bytes:
+        size = lib().seb_filter_encoded_size(self._h)
+        out = np.zeros(size, dtype=np.uint8)
+        check(lib().seb_filter_encode(self._h, out.ctypes.data, size))
+        return out.tobytes()
+
+
+# ------------------------------------------------- device-resident API (torch tensors) ----
+
+def _stream(stream=None) -> int:
+    import torch
+    s = torch.cuda.current_stream() if stream is None else stream
+    return s.cuda_stream
+
+
+def dev_keys(data, offsets=None, n: int | None = None, stride: int = 16) -> seb_keys:
+    """seb_keys over device tensors (uint8 data; optional uint64/int64 offsets of n+1)."""
+    if offsets is not None:
+        nn = offsets.numel() - 1
+        return seb_keys(data.data_ptr(), offsets.data_ptr(), nn, 0, 0)
+    nn = n if n is not None else data.numel() // stride
+    return seb_keys(data.data_ptr(), None, nn, stride, 0)
+
+
+def dev_clear(words, m: int, stream=None) -> None:
+    check(lib().seb_dev_clear(words.data_ptr(), m, _stream(stream)))
+
+
+def dev_build(keys: seb_keys, words, m: int, k: int, stream=None) -> None:
+    check(lib().seb_dev_build(C.byref(keys), words.data_ptr(), m, k, _stream(stream)))
+
+
+def dev_probe(keys: seb_keys, words, m: int, k: int, out, stream=None) -> None:
+    check(lib().seb_dev_probe(C.byref(keys), words.data_ptr(), m, k, out.data_ptr(), _stream(stream)))
+
+
+def dev_probe_multi(keys: seb_keys, filters: list[tuple[object, int, int]], mask, stream=None) -> None:
+    refs = (seb_filter_ref * len(filters))(*[seb_filter_ref(w.data_ptr(), m, k, 0) for w, m, k in filters])
+    check(lib().seb_dev_probe_multi(C.byref(keys), refs, len(filters), mask.data_ptr(), mask.element_size(),
+                                    _stream(stream)))
+
+
+def dev_build_many(keys: seb_keys, key_begin: list[int], filters: list[tuple[object, int, int]],
+                   stream=None) -> None:
+    kbeg = (_u64 * len(key_begin))(*key_begin)
+    refs = (seb_filter_ref * len(filters))(*[seb_filter_ref(w.data_ptr(), m, k, 0) for w, m, k in filters])
+    check(lib().seb_dev_build_many(C.byref(keys), kbeg, refs, len(filters), _stream(stream)))
+
+
+def new_words(m: int, device="cuda"):
+    """Zeroed device word array for an m-bit filter (torch uint32 view, 16-B padded)."""
+    import torch
+    return torch.zeros(max(words_bytes(m) // 4, 4), dtype=torch.int32, device=device)
+
+
+def words_to_bits(words, m: int) -> np.ndarray:
+    """First ceil(m/8) bytes of a device word array = the reference's bits slice."""
+    return words.cpu().numpy().view(np.uint8)[: (m + 7) // 8].copy()

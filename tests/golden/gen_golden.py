@@ -1,0 +1,173 @@
+"""Generate tests/golden/golden.json — the committed parity fixtures of the bloom path.
+
+Run in the build container:  python tests/golden/gen_golden.py
+Every vector is computed by BOTH CPU restatements (oracle/bloom_oracle.c via ctypes and
+oracle/bloom_np.py) and written only if they agree.  The FNV known-answer vectors are NOT
+generated: they are transcribed from the public FNV / Go hash/fnv test suites (go1.25.5
+src/hash/fnv/fnv_test.go golden64 / golden64a) and the survey's pins, and the generator
+asserts the restatements reproduce them.  The Go reference itself cannot run here (no Go
+toolchain in this image or on the GPU box), so bloom-level vectors are restatement-derived;
+the six (n, sha256) digests also match SURVEY.md §8(c), computed independently earlier.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "storage-engines_amd"))
+
+from oracle import bloom_np as bn  # noqa: E402
+from oracle import oracle_c as oc  # noqa: E402
+import keygen as kg  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.json")
+
+# Public known answers: (input, FNV-1 64, FNV-1a 64).
+FNV_KATS = [
+    (b"", 0xCBF29CE484222325, 0xCBF29CE484222325),
+    (b"a", 0xAF63BD4C8601B7BE, 0xAF63DC4C8601EC8C),
+    (b"ab", 0x08326707B4EB37B8, 0x089C4407B545986A),
+    (b"abc", 0xD8DCCA186BAFADCB, 0xE71FA2190541574B),
+    (b"foobar", 0x340D8765A4DDA9C2, 0x85944171F73967E8),
+    (b"key00000", 0x2690F21B0FD13716, 0x508D8E346F2092D4),
+]
+
+# SURVEY.md §8(c) digests (computed in the survey session by an independent restatement).
+SURVEY_DIGESTS = {
+    1: "3bcd5868911330c5f376e7acfd935aa6b4bb1a6f248a5a1047482397466b953a",
+    7: "1dfdebb0a91048d61d5e77e6fee8a095a44b7f996bc1fbb80545d97830430290",
+    1000: "25634be83b98dfef704a4cc6c4848b9256328bc53c9ce4820c28c893bd007d64",
+    5000: "77ce61b651bc283c77bea1d3c7007eb9de58b57756b7ef199a00eeb447939d81",
+    100000: "5c339ef1b8a07e85ae0afd0e623f6a329efc05be098f110c28ff5757bc8b5064",
+    10000000: "a86f3c69041ea0caac1dc559cfb36b06d5d5513d4ee203d22878715f612a0c3a",
+}
+SURVEY_PROBE = {100000: "57825ba55ce1b903dc04c6c923923fa63462f80b7a39bdefec54ff3ba92ec15e",
+                10000000: "aba77536fae51d566de525f519cd4c573799880d63000d88a2ce3052d0b90f95"}
+
+
+def sha(b) -> str:
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def fixed_case(n: int, p: float, check_np: bool) -> dict:
+    m, k = oc.params(n, p)
+    assert (m, k) == bn.params(n, p)
+    keys = kg.key16(np.arange(n))
+    bits = oc.build(m, k, keys, n, stride=16)
+    probe_keys = kg.key16(kg.probe_indices(n))
+    ans = oc.probe(bits, m, k, probe_keys, n, stride=16)
+    if check_np:
+        h1, h2 = bn.fnv_fixed(keys)
+        assert np.array_equal(bn.build(h1, h2, m, k), bits)
+        q1, q2 = bn.fnv_fixed(probe_keys)
+        assert np.array_equal(bn.probe(bits, q1, q2, m, k), ans)
+    enc = bn.encode(bits, m, k)
+    present = ans[0::2]
+    assert present.all(), "false negative in restatement"
+    return {"n": n, "p": p, "m": m, "k": k, "encode_len": len(enc), "encode_sha256": sha(enc),
+            "popcount": int(np.unpackbits(bits).sum()), "probe_positives": int(ans.sum()),
+            "probe_sha256": sha(ans.tobytes()), "false_positives": int(ans[1::2].sum()),
+            **({"encode_hex": enc.hex()} if len(enc) <= 8192 else {})}
+
+
+def varlen_case(n: int, p: float, check_np: bool) -> dict:
+    m, k = oc.params(n, p)
+    data, off = kg.varlen_keys(np.arange(n))
+    bits = oc.build(m, k, data, n, offsets=off)
+    pdata, poff = kg.varlen_keys(kg.probe_indices(n))
+    ans = oc.probe(bits, m, k, pdata, n, offsets=poff)
+    if check_np:
+        h1, h2 = bn.fnv_varlen(data, off)
+        assert np.array_equal(bn.build(h1, h2, m, k), bits)
+        q1, q2 = bn.fnv_varlen(pdata, poff)
+        assert np.array_equal(bn.probe(bits, q1, q2, m, k), ans)
+    assert ans[0::2].all()
+    enc = bn.encode(bits, m, k)
+    return {"n": n, "p": p, "m": m, "k": k, "key_bytes": int(off[-1]), "keys_sha256": sha(data.tobytes()),
+            "offsets_sha256": sha(off.tobytes()), "encode_sha256": sha(enc),
+            "probe_positives": int(ans.sum()), "probe_sha256": sha(ans.tobytes())}
+
+
+def multi_case(nf: int, per: int, nprobe: int, p: float) -> dict:
+    """C5 shape: filter f holds key16(f*per + j); probe q even -> key16((q/2 % nf)*per + (q/2)/nf)
+    (present in exactly one filter), q odd -> key16(nf*per + q) (absent from all)."""
+    m, k = oc.params(per, p)
+    filters = []
+    for f in range(nf):
+        keys = kg.key16(f * per + np.arange(per))
+        filters.append((oc.build(m, k, keys, per, stride=16), m, k))
+    q = np.arange(nprobe, dtype=np.int64)
+    half = q // 2
+    idx = np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q)
+    pk = kg.key16(idx)
+    mask = oc.probe_multi(filters, pk, nprobe, stride=16)
+    owner = (half % nf)
+    assert nprobe // 2 <= nf * per
+    assert np.all(((mask[0::2] >> owner[0::2].astype(np.uint64)) & np.uint64(1)) == 1)
+    return {"filters": nf, "keys_per_filter": per, "probes": nprobe, "p": p, "m": m, "k": k,
+            "filter_sha256": [sha(bn.encode(b, m, k)) for b, _, _ in filters],
+            "mask_sha256": sha(mask.astype("<u8").tobytes()), "mask_popcount": int(
+                np.unpackbits(mask.astype("<u8").view(np.uint8)).sum())}
+
+
+def main():
+    out: dict = {"generator": "tests/golden/gen_golden.py", "key_format": "key16(i) = b'user%010d' % i + "
+                 "bytes([i & 0xff, (i + 1) & 0xff]) (common/benchmark/keygen.go:89-109)",
+                 "probe_rule": "q even -> key(q) present; q odd -> key(n + q) absent"}
+    kats = []
+    for key, f1, f1a in FNV_KATS:
+        c1a, c1 = oc.fnv(key)
+        n1a, n1 = bn.fnv_bytes(key)
+        assert (c1a, c1) == (f1a, f1) == (n1a, n1), key
+        kats.append({"key_hex": key.hex(), "fnv1_64": f"{f1:016x}", "fnv1a_64": f"{f1a:016x}"})
+    out["fnv_kats"] = kats
+
+    sizing = []
+    for p in [0.01, 0.001, 0.05, 0.1, 0.5, 1e-6, 1e-10, 0.3]:
+        for n in [0, 1, 2, 3, 7, 100, 1000, 5000, 100000, 5912651, 10000000, 123456789]:
+            m, k = oc.params(n, p)
+            assert (m, k) == bn.params(n, p)
+            sizing.append({"n": n, "p": p, "m": m, "k": k, "bytes": (m + 7) // 8})
+    out["sizing"] = sizing
+
+    out["positions"] = [
+        {"key_hex": b"key00000".hex(), "m": 9586, "k": 7, "pos": oc.positions(b"key00000", 9586, 7)},
+        {"key_hex": kg.key16_bytes(0).hex(), "m": 95850584, "k": 7, "pos": oc.positions(kg.key16_bytes(0), 95850584, 7)},
+        {"key_hex": kg.key16_bytes(12345).hex(), "m": 2**40 + 12345, "k": 9,
+         "pos": oc.positions(kg.key16_bytes(12345), 2**40 + 12345, 9)},
+        {"key_hex": b"".hex(), "m": 1, "k": 3, "pos": oc.positions(b"", 1, 3)},
+        {"key_hex": b"wrap".hex(), "m": (2**64 - 59), "k": 7, "pos": oc.positions(b"wrap", 2**64 - 59, 7)},
+    ]
+    for e in out["positions"]:
+        h1, h2 = bn.fnv_bytes(bytes.fromhex(e["key_hex"]))
+        ref = [int(x) for x in bn.positions(np.array([h1], np.uint64), np.array([h2], np.uint64), e["m"], e["k"])[0]]
+        assert ref == e["pos"], e
+
+    fixed = []
+    for n in [1, 7, 1000, 5000, 100000, 10000000]:
+        c = fixed_case(n, 0.01, check_np=n <= 100000)
+        assert c["encode_sha256"] == SURVEY_DIGESTS[n], n
+        if n in SURVEY_PROBE:
+            assert c["probe_sha256"] == SURVEY_PROBE[n], n
+        fixed.append(c)
+        print("fixed", n, c["encode_sha256"][:16], c["probe_positives"], flush=True)
+    for p in [0.001, 0.1, 0.5]:
+        fixed.append(fixed_case(100000, p, check_np=True))
+    out["fixed16"] = fixed
+
+    out["varlen"] = [varlen_case(n, 0.01, check_np=n <= 100000) for n in [1000, 100000, 1000000]]
+    print("varlen done", flush=True)
+    out["multi"] = [multi_case(8, 10000, 160000, 0.01), multi_case(64, 2000, 256000, 0.01)]
+    with open(OUT, "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", OUT)
+
+
+if __name__ == "__main__":
+    main()
