@@ -298,12 +298,15 @@ def _stream(stream=None) -> int:
 
 
 def dev_keys(data, offsets=None, n: int | None = None, stride: int = 16) -> seb_keys:
-    """seb_keys over device tensors (uint8 data; optional uint64/int64 offsets of n+1)."""
+    """seb_keys over device tensors (uint8 data; optional uint64/int64 offsets of n+1).
+    The returned struct keeps the tensors alive (the C struct holds raw device pointers)."""
     if offsets is not None:
-        nn = offsets.numel() - 1
-        return seb_keys(data.data_ptr(), offsets.data_ptr(), nn, 0, 0)
-    nn = n if n is not None else data.numel() // stride
-    return seb_keys(data.data_ptr(), None, nn, stride, 0)
+        kd = seb_keys(data.data_ptr(), offsets.data_ptr(), offsets.numel() - 1, 0, 0)
+    else:
+        nn = n if n is not None else data.numel() // stride
+        kd = seb_keys(data.data_ptr(), None, nn, stride, 0)
+    kd._keep = (data, offsets)
+    return kd
 
 
 def dev_clear(words, m: int, stream=None) -> None:

@@ -373,17 +373,17 @@ def test_build_many_compaction_batch(seb, golden, torch_cuda):
     torch = torch_cuda
     row = golden["multi"][0]
     nf, per, m, k = row["filters"], row["keys_per_filter"], row["m"], row["k"]
-    keys = to_dev(torch, kg.key16(np.arange(nf * per)))
-    kd = seb.dev_keys(keys, n=nf * per, stride=16)
+    keys = to_dev(torch, kg.key16(np.arange((nf + 1) * per)))
+    kd = seb.dev_keys(keys, n=(nf + 1) * per, stride=16)
     filters = [(seb.new_words(m), m, k) for _ in range(nf)]
     big_m, big_k = oc.params(2 * per * 10, 0.01)  # > 160 KiB of words -> global atomics path
     filters.append((seb.new_words(big_m), big_m, big_k))
-    begin = [f * per for f in range(nf)] + [nf * per - per, nf * per]
+    begin = [f * per for f in range(nf + 2)]  # filter f <- keys [begin[f], begin[f+1])
     seb.dev_build_many(kd, begin, filters)
     torch.cuda.synchronize()
     for f in range(nf):
-        assert sha(bn.encode(seb.words_to_bits(filters[f][0], m), m, k)) == row["filter_sha256"][f]
-    last = kg.key16(np.arange(nf * per - per, nf * per))
+        assert sha(bn.encode(seb.words_to_bits(filters[f][0], m), m, k)) == row["filter_sha256"][f], f
+    last = kg.key16(np.arange(nf * per, (nf + 1) * per))
     assert np.array_equal(seb.words_to_bits(filters[-1][0], big_m), oc.build(big_m, big_k, last, per, stride=16))
     # C1-size compaction filters (100K keys, 119,814 B each) fit the LDS path
     m1, k1 = oc.params(100000, 0.01)
