@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--build-algo", type=int, default=None, help="0 auto, 1 atomic, 2 bucketed")
+    ap.add_argument("--probe-split", type=int, default=None)
     return ap.parse_args()
 
 
@@ -71,6 +73,10 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
     seb.device_check(dev.index)
+    if args.build_algo is not None:
+        seb.set_option("build_algo", args.build_algo)
+    if args.probe_split is not None:
+        seb.set_option("probe_split", args.probe_split)
 
     n = args.keys
     p = 0.01
@@ -201,6 +207,7 @@ def main():
                          "other": {d: {"ms": round(v[0], 4), "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 2)}
                                    for d, v in kern.items()}},
             "parity": parity,
+            "options": {o: seb.get_option(o) for o in ("build_algo", "probe_split", "bucket_min_keys")},
         }
         if world == 1 and args.config == "c2c3" and not args.no_host_inclusive:
             result["host_inclusive"] = host_inclusive(seb, build_host, probe_host, m, k)

@@ -70,6 +70,15 @@ uint64_t seb_num_bytes(uint64_t num_bits);
 uint64_t seb_words_bytes(uint64_t num_bits);
 
 int seb_abi_version(void);
+/* Process-wide tuning knobs (results never change, only speed):
+ *   "build_algo"      0 auto, 1 device-scope atomic OR, 2 radix-partitioned LDS build
+ *   "probe_split"     k == 7 probes: words gathered before the first test (0 = all 7 at once)
+ *   "bucket_min_keys" auto build_algo: radix-partitioned from this many keys on
+ *   "grid_cap"        maximum workgroups of the grid-stride kernels
+ * Environment variables SEB_BUILD_ALGO, SEB_PROBE_SPLIT, SEB_BUCKET_MIN_KEYS, SEB_GRID_CAP set the
+ * initial values. */
+int seb_set_option(const char *name, int64_t value);
+int seb_get_option(const char *name, int64_t *value);
 const char *seb_last_error(void);
 /* 0 if a gfx950 device is usable, else SEB_ERR_DEVICE (message in seb_last_error). */
 int seb_device_check(int device);
@@ -81,6 +90,11 @@ int seb_device_check(int device);
 int seb_dev_clear(uint32_t *words, uint64_t num_bits, void *stream);
 int seb_dev_build(const seb_keys *keys, uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
                   void *stream);
+/* Same, with caller-owned scratch (graph-capture friendly: no allocation inside the call).
+ * seb_dev_build_workspace_size gives the bytes needed for n keys (0: this build needs none). */
+uint64_t seb_dev_build_workspace_size(uint64_t n, uint64_t num_bits, uint32_t num_hashes);
+int seb_dev_build_ws(const seb_keys *keys, uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
+                     void *workspace, uint64_t workspace_bytes, void *stream);
 /* out[i] = MayContain(key i) as 0/1 bytes (bloom.go:82-92; Go []bool layout). */
 int seb_dev_probe(const seb_keys *keys, const uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
                   uint8_t *out, void *stream);

@@ -93,8 +93,36 @@ static bool env_flag(const char *name, long *out) {
 
 static std::once_flag g_env_once;
 static void load_env() {
-    long cap;
-    if (env_flag("SEB_GRID_CAP", &cap)) set_grid_cap((unsigned)cap);
+    long v;
+    Options &o = options();
+    if (env_flag("SEB_GRID_CAP", &v) && v > 0) o.grid_cap = (unsigned)v;
+    if (env_flag("SEB_BUILD_ALGO", &v)) o.build_algo = (int)v;
+    if (env_flag("SEB_PROBE_SPLIT", &v)) o.probe_split = (int)v;
+    if (env_flag("SEB_BUCKET_MIN_KEYS", &v) && v >= 0) o.bucket_min_keys = (uint64_t)v;
+}
+
+extern "C" int seb_set_option(const char *name, int64_t value) {
+    std::call_once(g_env_once, load_env);
+    if (!name) return fail(SEB_ERR_INVALID, "seb_set_option: null name");
+    Options &o = options();
+    if (!strcmp(name, "build_algo") && value >= 0 && value <= 2) o.build_algo = (int)value;
+    else if (!strcmp(name, "probe_split") && value >= 0 && value <= 7) o.probe_split = (int)value;
+    else if (!strcmp(name, "grid_cap") && value > 0 && value <= (1 << 30)) o.grid_cap = (unsigned)value;
+    else if (!strcmp(name, "bucket_min_keys") && value >= 0) o.bucket_min_keys = (uint64_t)value;
+    else return fail(SEB_ERR_INVALID, "seb_set_option: bad option %s=%lld", name, (long long)value);
+    return SEB_OK;
+}
+
+extern "C" int seb_get_option(const char *name, int64_t *value) {
+    std::call_once(g_env_once, load_env);
+    if (!name || !value) return fail(SEB_ERR_INVALID, "seb_get_option: null argument");
+    const Options &o = options();
+    if (!strcmp(name, "build_algo")) *value = o.build_algo;
+    else if (!strcmp(name, "probe_split")) *value = o.probe_split;
+    else if (!strcmp(name, "grid_cap")) *value = o.grid_cap;
+    else if (!strcmp(name, "bucket_min_keys")) *value = (int64_t)o.bucket_min_keys;
+    else return fail(SEB_ERR_INVALID, "seb_get_option: unknown option %s", name);
+    return SEB_OK;
 }
 
 extern "C" int seb_device_check(int device) {
@@ -120,13 +148,95 @@ extern "C" int seb_dev_clear(uint32_t *words, uint64_t m, void *stream) {
     return SEB_OK;
 }
 
+// Workspace for the bucketed build: grow-only scratch owned by the library, one per
+// (device, stream) so concurrent streams never share it (stream order protects reuse).
+struct WsKey {
+    int device;
+    hipStream_t stream;
+};
+struct WsEntry {
+    WsKey key;
+    void *p;
+    uint64_t bytes;
+};
+static std::mutex g_ws_mu;
+static std::vector<WsEntry> g_ws;
+
+static int cached_workspace(hipStream_t s, uint64_t bytes, void **out) {
+    int dev = 0;
+    HIP_OR_FAIL(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    for (auto &e : g_ws)
+        if (e.key.device == dev && e.key.stream == s) {
+            if (e.bytes >= bytes) {
+                *out = e.p;
+                return SEB_OK;
+            }
+            HIP_OR_FAIL(hipStreamSynchronize(s));
+            HIP_OR_FAIL(hipFree(e.p));
+            e.p = nullptr;
+            e.bytes = 0;
+            hipError_t a = hipMalloc(&e.p, bytes);
+            if (a != hipSuccess) return fail(SEB_ERR_NOMEM, "workspace hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(a));
+            e.bytes = bytes;
+            *out = e.p;
+            return SEB_OK;
+        }
+    void *p = nullptr;
+    hipError_t a = hipMalloc(&p, bytes);
+    if (a != hipSuccess) return fail(SEB_ERR_NOMEM, "workspace hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(a));
+    g_ws.push_back({{dev, s}, p, bytes});
+    *out = p;
+    return SEB_OK;
+}
+
+// Build dispatcher: bucketed (LDS, no global atomics) or device-scope atomics.  `ws`/`ws_bytes`
+// may be null/0, in which case `grow` supplies scratch (or the atomic path runs).
+template <typename Grow>
+static int build_dispatch(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s, void *ws,
+                          uint64_t ws_bytes, Grow &&grow) {
+    if (kb.n == 0 || md.k == 0) return SEB_OK;
+    if (choose_build_algo(kb.n, md.m, md.k) == 2) {
+        const uint64_t need = bucketed_workspace_bytes(kb.n, md.m, md.k);
+        if (ws_bytes < need) {
+            int rc = grow(need, &ws);
+            if (rc) return rc;
+            ws_bytes = need;
+        }
+        HIP_OR_FAIL(launch_build_bucketed(kb, words, md, ws, ws_bytes, s));
+        return SEB_OK;
+    }
+    HIP_OR_FAIL(launch_build(kb, words, md, s));
+    return SEB_OK;
+}
+
+extern "C" uint64_t seb_dev_build_workspace_size(uint64_t n, uint64_t m, uint32_t k) {
+    std::call_once(g_env_once, load_env);
+    if (m == 0 || choose_build_algo(n, m, k) != 2) return 0;
+    return bucketed_workspace_bytes(n, m, k);
+}
+
+extern "C" int seb_dev_build_ws(const seb_keys *keys, uint32_t *words, uint64_t m, uint32_t k, void *ws,
+                                uint64_t ws_bytes, void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc;
+    if ((rc = check_keys(keys, "seb_dev_build_ws")) || (rc = check_filter_args(m, k, "seb_dev_build_ws"))) return rc;
+    if (!words) return fail(SEB_ERR_INVALID, "seb_dev_build_ws: null words");
+    return build_dispatch(key_batch(keys), words, mod_arg(m, k), (hipStream_t)stream, ws, ws_bytes,
+                          [&](uint64_t need, void **) -> int {
+                              return fail(SEB_ERR_INVALID, "seb_dev_build_ws: workspace %llu B < %llu B",
+                                          (unsigned long long)ws_bytes, (unsigned long long)need);
+                          });
+}
+
 extern "C" int seb_dev_build(const seb_keys *keys, uint32_t *words, uint64_t m, uint32_t k, void *stream) {
     std::call_once(g_env_once, load_env);
     int rc;
     if ((rc = check_keys(keys, "seb_dev_build")) || (rc = check_filter_args(m, k, "seb_dev_build"))) return rc;
     if (!words) return fail(SEB_ERR_INVALID, "seb_dev_build: null words");
-    HIP_OR_FAIL(launch_build(key_batch(keys), words, mod_arg(m, k), (hipStream_t)stream));
-    return SEB_OK;
+    hipStream_t s = (hipStream_t)stream;
+    return build_dispatch(key_batch(keys), words, mod_arg(m, k), s, nullptr, 0,
+                          [&](uint64_t need, void **out) { return cached_workspace(s, need, out); });
 }
 
 extern "C" int seb_dev_probe(const seb_keys *keys, const uint32_t *words, uint64_t m, uint32_t k, uint8_t *out,
@@ -280,7 +390,7 @@ struct seb_ctx {
     std::mutex mu;
     hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr;
     hipEvent_t ev_h2d[2] = {}, ev_comp[2] = {}, ev_d2h[2] = {};
-    DevBuf keys[2], offs[2], out[2], words, filt;
+    DevBuf keys[2], offs[2], out[2], words, filt, ws;
     uint64_t chunk_bytes = 64ull << 20;
     std::vector<uint64_t> off_tmp[2];
 };
@@ -325,6 +435,7 @@ extern "C" void seb_ctx_destroy(seb_ctx *c) {
     }
     c->words.release();
     c->filt.release();
+    c->ws.release();
     if (c->s_h2d) (void)hipStreamDestroy(c->s_h2d);
     if (c->s_comp) (void)hipStreamDestroy(c->s_comp);
     if (c->s_d2h) (void)hipStreamDestroy(c->s_d2h);
@@ -402,7 +513,13 @@ static int build_device_from_host(seb_ctx *c, const seb_keys *kb, uint32_t *dwor
         KeyBatch dk{};
         int rc = stage_chunk(c, kb, chunks[j], b, &dk);
         if (rc) return rc;
-        HIP_OR_FAIL(launch_build(dk, dwords, md, c->s_comp));
+        rc = build_dispatch(dk, dwords, md, c->s_comp, c->ws.p, c->ws.cap, [&](uint64_t need, void **out) -> int {
+            HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));  // previous chunks may still use it
+            int r = c->ws.reserve(need);
+            *out = c->ws.p;
+            return r;
+        });
+        if (rc) return rc;
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
     }
     return SEB_OK;

@@ -45,11 +45,25 @@ struct ManyArg {
     uint32_t pad;
 };
 
+// Process-wide tuning knobs (seb_set_option).
+struct Options {
+    int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed)
+    int probe_split = 3;          // k == 7 probes: gathers in the first round (0 or >= 7: all at once)
+    uint64_t bucket_min_keys = 1u << 18;  // auto: bucketed build from this many keys on
+    unsigned grid_cap = 1u << 20;
+};
+Options &options();
+
 hipError_t launch_build(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s);
+bool bucketed_supported(uint64_t m, uint32_t k);
+uint64_t bucketed_workspace_bytes(uint64_t n, uint64_t m, uint32_t k);
+hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModArg &md, void *ws, uint64_t ws_bytes,
+                                 hipStream_t s);
+// 1 = atomic, 2 = bucketed, for a batch of n keys into an m-bit filter.
+int choose_build_algo(uint64_t n, uint64_t m, uint32_t k);
 hipError_t launch_probe(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s);
 hipError_t launch_probe_multi(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes,
                               hipStream_t s);
 hipError_t launch_build_many_lds(const KeyBatch &kb, const ManyArg &ma, uint32_t lds_bytes, hipStream_t s);
-void set_grid_cap(unsigned cap);
 
 }  // namespace seb

@@ -15,154 +15,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "seb_device.h"
 #include "seb_kernels.h"
 
 namespace seb {
-
-constexpr uint64_t kFnvOffset = 0xcbf29ce484222325ull;
-constexpr uint64_t kFnvPrime = 0x100000001b3ull;
-
-// ------------------------------------------------------------------ hashing ----------------
-
-__device__ __forceinline__ void fnv_byte(uint32_t b, uint64_t &h1, uint64_t &h2) {
-    h1 = (h1 ^ (uint64_t)b) * kFnvPrime;  // FNV-1a (hash1)
-    h2 = (h2 * kFnvPrime) ^ (uint64_t)b;  // FNV-1  (hash2)
-}
-
-__device__ __forceinline__ void fnv_word(uint32_t w, uint64_t &h1, uint64_t &h2) {
-    fnv_byte(w & 0xffu, h1, h2);
-    fnv_byte((w >> 8) & 0xffu, h1, h2);
-    fnv_byte((w >> 16) & 0xffu, h1, h2);
-    fnv_byte(w >> 24, h1, h2);
-}
-
-// Bytes [lo, hi) of word w (0 <= lo <= hi <= 4), predicated so a wave stays converged.
-__device__ __forceinline__ void fnv_word_part(uint32_t w, uint32_t lo, uint32_t hi, uint64_t &h1,
-                                              uint64_t &h2) {
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-        uint32_t b = (w >> (8 * j)) & 0xffu;
-        uint64_t a1 = (h1 ^ (uint64_t)b) * kFnvPrime;
-        uint64_t a2 = (h2 * kFnvPrime) ^ (uint64_t)b;
-        bool on = (j >= lo) & (j < hi);
-        h1 = on ? a1 : h1;
-        h2 = on ? a2 : h2;
-    }
-}
-
-// Key sources.  Each provides hash(i, h1, h2) for key i.
-struct Keys16 {  // fixed 16-B keys, 16-B aligned: one dwordx4 per lane, 1 KiB per wave, coalesced
-    const uint4 *p;
-    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
-        uint4 v = p[i];
-        h1 = kFnvOffset;
-        h2 = kFnvOffset;
-        fnv_word(v.x, h1, h2);
-        fnv_word(v.y, h1, h2);
-        fnv_word(v.z, h1, h2);
-        fnv_word(v.w, h1, h2);
-    }
-};
-
-struct KeysStrideW {  // fixed stride, multiple of 4 bytes, 4-B aligned
-    const uint32_t *p;
-    uint32_t words;
-    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
-        const uint32_t *k = p + i * words;
-        h1 = kFnvOffset;
-        h2 = kFnvOffset;
-        for (uint32_t j = 0; j < words; ++j) fnv_word(k[j], h1, h2);
-    }
-};
-
-struct KeysStrideB {  // any fixed stride (including 0)
-    const uint8_t *p;
-    uint32_t stride;
-    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
-        const uint8_t *k = p + i * stride;
-        h1 = kFnvOffset;
-        h2 = kFnvOffset;
-        for (uint32_t j = 0; j < stride; ++j) fnv_byte(k[j], h1, h2);
-    }
-};
-
-struct KeysVar {  // variable length: key i = p[off[i], off[i+1])
-    const uint8_t *p;
-    const uint64_t *off;
-    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
-        uint64_t s = off[i], e = off[i + 1];
-        h1 = kFnvOffset;
-        h2 = kFnvOffset;
-        // Walk the aligned dwords that cover [s, e).  A dword holding at least one byte of
-        // the buffer never crosses a page, so the over-read at either end cannot fault.
-        uintptr_t a = ((uintptr_t)(p + s)) & ~(uintptr_t)3;
-        uintptr_t end = (uintptr_t)(p + e);
-        uintptr_t beg = (uintptr_t)(p + s);
-        for (; a < end; a += 4) {
-            uint32_t w = *(const uint32_t *)a;
-            uint32_t lo = beg > a ? (uint32_t)(beg - a) : 0u;
-            uint32_t hi = end - a < 4 ? (uint32_t)(end - a) : 4u;
-            if (lo == 0 && hi == 4)
-                fnv_word(w, h1, h2);
-            else
-                fnv_word_part(w, lo, hi, h1, h2);
-        }
-    }
-};
-
-// --------------------------------------------------------------- positions -----------------
-
-// Exact x mod m for any m >= 1 with mu = floor((2^64-1)/m): the estimate q is at most 2 low.
-__device__ __forceinline__ uint64_t mod64(uint64_t x, uint64_t m, uint64_t mu) {
-    uint64_t q = __umul64hi(x, mu);
-    uint64_t r = x - q * m;
-    r = r >= m ? r - m : r;
-    r = r >= m ? r - m : r;
-    return r;
-}
-
-// Calls f(i, pos_i) for i < k with pos_i = (h1 + i*h2 mod 2^64) mod m, bit-exact with
-// lsm/bloom.go:64.  Residues advance incrementally: r_{i+1} = r_i + (h2 mod m), minus
-// (2^64 mod m) whenever the u64 sum h1 + (i+1)*h2 wraps.  M32: m < 2^32 -> u32 residues.
-template <int KFIX, bool M32, typename F>
-__device__ __forceinline__ void for_positions(uint64_t h1, uint64_t h2, const ModArg &md, uint32_t krt, F &&f) {
-    const uint32_t k = KFIX > 0 ? (uint32_t)KFIX : krt;
-    if (k == 0) return;
-    uint64_t x = h1;
-    if constexpr (M32) {
-        const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
-        uint32_t r = (uint32_t)mod64(h1, md.m, md.mu);
-        const uint32_t b = (uint32_t)mod64(h2, md.m, md.mu);
-        f(0u, (uint64_t)r);
-#pragma unroll
-        for (uint32_t i = 1; i < k; ++i) {
-            uint64_t xn = x + h2;
-            bool carry = xn < x;
-            x = xn;
-            uint32_t s = r + b;
-            s = (s < r || s >= m) ? s - m : s;
-            uint32_t t = s >= c ? s - c : s + (m - c);
-            r = carry ? t : s;
-            f(i, (uint64_t)r);
-        }
-    } else {
-        const uint64_t m = md.m, c = md.c;
-        uint64_t r = mod64(h1, md.m, md.mu);
-        const uint64_t b = mod64(h2, md.m, md.mu);
-        f(0u, r);
-#pragma unroll
-        for (uint32_t i = 1; i < k; ++i) {
-            uint64_t xn = x + h2;
-            bool carry = xn < x;
-            x = xn;
-            uint64_t s = r + b;
-            s = (s < r || s >= m) ? s - m : s;
-            uint64_t t = s >= c ? s - c : s + (m - c);
-            r = carry ? t : s;
-            f(i, r);
-        }
-    }
-}
 
 // ------------------------------------------------------------------ kernels -----------------
 
@@ -180,9 +36,11 @@ __global__ __launch_bounds__(256) void k_build(Src src, uint64_t n, uint32_t *__
     }
 }
 
-// Probe: one thread per key, all k word gathers issued before the AND (the answer equals the
-// reference's early-exit loop), 0/1 byte out.
-template <typename Src, int KFIX, bool M32>
+// Probe: one thread per key, 0/1 byte out; the answer is the AND of the k bits, as the
+// reference's early-exit loop returns.  KFIX == 7 computes all 7 positions first, gathers the
+// first SPLIT words, and gathers the rest only where those bits are all set (a key whose first
+// bits are clear is already "absent": fewer fabric reads, same answer).  SPLIT == 0: all at once.
+template <typename Src, int KFIX, bool M32, int SPLIT>
 __global__ __launch_bounds__(256) void k_probe(Src src, uint64_t n, const uint32_t *__restrict__ words, ModArg md,
                                                uint8_t *__restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -190,8 +48,19 @@ __global__ __launch_bounds__(256) void k_probe(Src src, uint64_t n, const uint32
         uint64_t h1, h2;
         src.hash(i, h1, h2);
         uint32_t acc = 1u;
-        for_positions<KFIX, M32>(h1, h2, md, md.k,
-                                 [&](uint32_t, uint64_t p) { acc &= words[p >> 5] >> (uint32_t)(p & 31); });
+        if constexpr (KFIX > 0 && SPLIT > 0 && SPLIT < KFIX) {
+            uint64_t pos[KFIX];
+            for_positions<KFIX, M32>(h1, h2, md, KFIX, [&](uint32_t q, uint64_t p) { pos[q] = p; });
+#pragma unroll
+            for (int q = 0; q < SPLIT; ++q) acc &= words[pos[q] >> 5] >> (uint32_t)(pos[q] & 31);
+            if (acc & 1u) {
+#pragma unroll
+                for (int q = SPLIT; q < KFIX; ++q) acc &= words[pos[q] >> 5] >> (uint32_t)(pos[q] & 31);
+            }
+        } else {
+            for_positions<KFIX, M32>(h1, h2, md, md.k,
+                                     [&](uint32_t, uint64_t p) { acc &= words[p >> 5] >> (uint32_t)(p & 31); });
+        }
         out[i] = (uint8_t)(acc & 1u);
     }
 }
@@ -263,40 +132,50 @@ static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
     return (unsigned)(g > cap ? cap : g);
 }
 
-static unsigned g_grid_cap = 1u << 20;  // launch one thread per key by default
-void set_grid_cap(unsigned cap) { g_grid_cap = cap ? cap : (1u << 20); }
+Options &options() {
+    static Options o;
+    return o;
+}
+
+int choose_build_algo(uint64_t n, uint64_t m, uint32_t k) {
+    const Options &o = options();
+    if (o.build_algo == 1 || !bucketed_supported(m, k)) return 1;
+    if (o.build_algo == 2) return 2;
+    return n >= o.bucket_min_keys ? 2 : 1;
+}
 
 template <typename Src, int KFIX, bool M32>
 static hipError_t launch_build_t(const Src &src, uint64_t n, uint32_t *words, const ModArg &md, hipStream_t s) {
-    unsigned g = grid_for(n, 256, g_grid_cap);
+    unsigned g = grid_for(n, 256, options().grid_cap);
     hipLaunchKernelGGL((k_build<Src, KFIX, M32>), dim3(g), dim3(256), 0, s, src, n, words, md);
     return hipGetLastError();
 }
 
-template <typename Src, int KFIX, bool M32>
+template <typename Src, int KFIX, bool M32, int SPLIT>
 static hipError_t launch_probe_t(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
                                  hipStream_t s) {
-    unsigned g = grid_for(n, 256, g_grid_cap);
-    hipLaunchKernelGGL((k_probe<Src, KFIX, M32>), dim3(g), dim3(256), 0, s, src, n, words, md, out);
+    unsigned g = grid_for(n, 256, options().grid_cap);
+    hipLaunchKernelGGL((k_probe<Src, KFIX, M32, SPLIT>), dim3(g), dim3(256), 0, s, src, n, words, md, out);
     return hipGetLastError();
+}
+
+template <typename Src, bool M32>
+static hipError_t launch_probe7(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
+                                hipStream_t s) {
+    switch (options().probe_split) {
+        case 2: return launch_probe_t<Src, 7, M32, 2>(src, n, words, md, out, s);
+        case 3: return launch_probe_t<Src, 7, M32, 3>(src, n, words, md, out, s);
+        case 4: return launch_probe_t<Src, 7, M32, 4>(src, n, words, md, out, s);
+        default: return launch_probe_t<Src, 7, M32, 0>(src, n, words, md, out, s);
+    }
 }
 
 template <typename Src, typename MaskT, bool SAME, int KFIX, bool M32>
 static hipError_t launch_multi_t(const Src &src, uint64_t n, const MultiArg &ma, void *mask, hipStream_t s) {
-    unsigned g = grid_for(n, 256, g_grid_cap);
+    unsigned g = grid_for(n, 256, options().grid_cap);
     hipLaunchKernelGGL((k_probe_multi<Src, MaskT, SAME, KFIX, M32>), dim3(g), dim3(256), 0, s, src, n, ma,
                        (MaskT *)mask);
     return hipGetLastError();
-}
-
-// Dispatch on the key source.  Fixed 16-B aligned keys take the vector path.
-template <typename Fn>
-static hipError_t with_src(const KeyBatch &kb, Fn &&fn) {
-    if (kb.offsets) return fn(KeysVar{kb.data, kb.offsets});
-    if (kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0) return fn(Keys16{(const uint4 *)kb.data});
-    if (kb.stride % 4 == 0 && ((uintptr_t)kb.data & 3) == 0)
-        return fn(KeysStrideW{(const uint32_t *)kb.data, kb.stride / 4});
-    return fn(KeysStrideB{kb.data, kb.stride});
 }
 
 hipError_t launch_build(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s) {
@@ -317,8 +196,8 @@ hipError_t launch_probe(const KeyBatch &kb, const uint32_t *words, const ModArg 
     const bool k7 = md.k == 7;
     return with_src(kb, [&](auto src) {
         using S = decltype(src);
-        if (m32) return k7 ? launch_probe_t<S, 7, true>(src, kb.n, words, md, out, s) : launch_probe_t<S, 0, true>(src, kb.n, words, md, out, s);
-        return k7 ? launch_probe_t<S, 7, false>(src, kb.n, words, md, out, s) : launch_probe_t<S, 0, false>(src, kb.n, words, md, out, s);
+        if (m32) return k7 ? launch_probe7<S, true>(src, kb.n, words, md, out, s) : launch_probe_t<S, 0, true, 0>(src, kb.n, words, md, out, s);
+        return k7 ? launch_probe7<S, false>(src, kb.n, words, md, out, s) : launch_probe_t<S, 0, false, 0>(src, kb.n, words, md, out, s);
     });
 }
 

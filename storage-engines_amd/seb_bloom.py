@@ -57,6 +57,10 @@ _SIGS = {
     "seb_words_bytes": (_u64, [_u64]),
     "seb_abi_version": (_i, []),
     "seb_last_error": (C.c_char_p, []),
+    "seb_set_option": (_i, [C.c_char_p, C.c_int64]),
+    "seb_get_option": (_i, [C.c_char_p, C.POINTER(C.c_int64)]),
+    "seb_dev_build_workspace_size": (_u64, [_u64, _u64, _u32]),
+    "seb_dev_build_ws": (_i, [C.POINTER(seb_keys), _vp, _u64, _u32, _vp, _u64, _vp]),
     "seb_device_check": (_i, [_i]),
     "seb_dev_clear": (_i, [_vp, _u64, _vp]),
     "seb_dev_build": (_i, [C.POINTER(seb_keys), _vp, _u64, _u32, _vp]),
@@ -138,6 +142,31 @@ def num_bytes(m: int) -> int:
 
 def words_bytes(m: int) -> int:
     return lib().seb_words_bytes(m)
+
+
+def set_option(name: str, value: int) -> None:
+    """Tuning knob (build_algo, probe_split, bucket_min_keys, grid_cap); results never change."""
+    check(lib().seb_set_option(name.encode(), int(value)))
+
+
+def get_option(name: str) -> int:
+    v = C.c_int64()
+    check(lib().seb_get_option(name.encode(), C.byref(v)))
+    return v.value
+
+
+class option:
+    """Context manager: temporarily set a tuning knob."""
+
+    def __init__(self, name: str, value: int):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        self.old = get_option(self.name)
+        set_option(self.name, self.value)
+
+    def __exit__(self, *exc):
+        set_option(self.name, self.old)
 
 
 def device_check(device: int = 0) -> None:
@@ -315,6 +344,15 @@ def dev_clear(words, m: int, stream=None) -> None:
 
 def dev_build(keys: seb_keys, words, m: int, k: int, stream=None) -> None:
     check(lib().seb_dev_build(C.byref(keys), words.data_ptr(), m, k, _stream(stream)))
+
+
+def dev_build_workspace_size(n: int, m: int, k: int) -> int:
+    return lib().seb_dev_build_workspace_size(n, m, k)
+
+
+def dev_build_ws(keys: seb_keys, words, m: int, k: int, ws, stream=None) -> None:
+    check(lib().seb_dev_build_ws(C.byref(keys), words.data_ptr(), m, k, ws.data_ptr() if ws is not None else None,
+                                 ws.numel() * ws.element_size() if ws is not None else 0, _stream(stream)))
 
 
 def dev_probe(keys: seb_keys, words, m: int, k: int, out, stream=None) -> None:

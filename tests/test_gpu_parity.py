@@ -165,8 +165,21 @@ def test_host_api_chunked_pipeline(seb, monkeypatch, torch_cuda):
 
 # --------------------------------------------------------- device-resident API --------------
 
-def test_c2_c3_10m_device_resident(seb, golden, torch_cuda):
-    """BASELINE C2 (build 10M x 16B @1%) and C3 (probe 10M, 50% present), digests + properties."""
+@pytest.fixture(params=[1, 2], ids=["atomic", "bucketed"])
+def build_algo(request, seb):
+    with seb.option("build_algo", request.param):
+        yield request.param
+
+
+@pytest.fixture(params=[0, 2, 3, 4], ids=lambda v: f"split{v}")
+def probe_split(request, seb):
+    with seb.option("probe_split", request.param):
+        yield request.param
+
+
+def test_c2_c3_10m_device_resident(seb, golden, torch_cuda, build_algo):
+    """BASELINE C2 (build 10M x 16B @1%) and C3 (probe 10M, 50% present), digests + properties,
+    for both build algorithms (device-scope atomics and the radix-partitioned LDS build)."""
     torch = torch_cuda
     row = next(r for r in golden["fixed16"] if r["n"] == 10_000_000)
     n, m, k = row["n"], row["m"], row["k"]
@@ -205,7 +218,7 @@ def test_c2_c3_10m_device_resident(seb, golden, torch_cuda):
 
 
 @pytest.mark.parametrize("n", [1000, 100000, 1000000])
-def test_c4_varlen_device(seb, golden, torch_cuda, n):
+def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
     torch = torch_cuda
     row = next(r for r in golden["varlen"] if r["n"] == n)
     m, k = row["m"], row["k"]
@@ -237,7 +250,7 @@ def test_c4_varlen_10m_properties(seb, torch_cuda):
 
 
 @pytest.mark.parametrize("stride", [0, 1, 3, 13, 16, 24, 33, 64])
-def test_fixed_strides_and_alignment(seb, torch_cuda, stride):
+def test_fixed_strides_and_alignment(seb, torch_cuda, stride, build_algo):
     torch = torch_cuda
     rng = np.random.default_rng(stride)
     n = 20000
@@ -257,11 +270,14 @@ def test_fixed_strides_and_alignment(seb, torch_cuda, stride):
         assert bool(out.all())
 
 
+@pytest.mark.parametrize("algo", [1, 2])
 @pytest.mark.parametrize("m,k", [(1, 1), (1, 7), (2, 3), (31, 7), (32, 7), (33, 7), (4096, 30),
                                  (2**31 - 1, 7), (2**32 - 5, 7), (2**32 + 977, 7), (3 * 2**32 + 12345, 9)])
-def test_modulus_edge_cases(seb, torch_cuda, m, k):
-    """u32 and u64 residue paths, m near 2^32, runtime k != 7 (lsm/bloom.go:64 wraparound)."""
+def test_modulus_edge_cases(seb, torch_cuda, m, k, algo):
+    """u32 and u64 residue paths, m near 2^32, runtime k != 7 (lsm/bloom.go:64 wraparound).
+    algo 2 runs the radix-partitioned build where it applies (m <= 2^28), atomics elsewhere."""
     torch = torch_cuda
+    seb.set_option("build_algo", algo)
     rng = np.random.default_rng(m % 1000)
     n = 4096
     keys = rng.integers(0, 256, (n, 16), dtype=np.uint8)
@@ -281,9 +297,41 @@ def test_modulus_edge_cases(seb, torch_cuda, m, k):
     seb.dev_probe(kd, words, m, k, out)
     torch.cuda.synchronize()
     assert bool(out.all())
+    seb.set_option("build_algo", 0)
 
 
-def test_empty_batches(seb, ctx, torch_cuda):
+def test_probe_split_variants(seb, golden, torch_cuda, probe_split):
+    """The split-round probe (first-round gathers, the rest only where all bits so far are set)
+    returns exactly the single-round answers."""
+    torch = torch_cuda
+    row = next(r for r in golden["fixed16"] if r["n"] == 100000 and r["p"] == 0.01)
+    n, m, k = row["n"], row["m"], row["k"]
+    kd = seb.dev_keys(to_dev(torch, kg.key16(np.arange(n))), n=n, stride=16)
+    words, _ = dev_build_bits(seb, torch, kd, m, k)
+    out = torch.empty(n, dtype=torch.uint8, device="cuda")
+    seb.dev_probe(seb.dev_keys(to_dev(torch, kg.key16(kg.probe_indices(n))), n=n, stride=16), words, m, k, out)
+    torch.cuda.synchronize()
+    assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
+
+
+def test_dev_build_with_caller_workspace(seb, golden, torch_cuda):
+    torch = torch_cuda
+    row = next(r for r in golden["fixed16"] if r["n"] == 100000 and r["p"] == 0.01)
+    n, m, k = row["n"], row["m"], row["k"]
+    kd = seb.dev_keys(to_dev(torch, kg.key16(np.arange(n))), n=n, stride=16)
+    with seb.option("build_algo", 2):
+        need = seb.dev_build_workspace_size(n, m, k)
+        assert need > 0
+        ws = torch.empty(need, dtype=torch.uint8, device="cuda")
+        words = seb.new_words(m)
+        seb.dev_build_ws(kd, words, m, k, ws)
+        torch.cuda.synchronize()
+        assert sha(bn.encode(seb.words_to_bits(words, m), m, k)) == row["encode_sha256"]
+        with pytest.raises(seb.SebError):
+            seb.dev_build_ws(kd, words, m, k, ws[: need // 2])
+
+
+def test_empty_batches(seb, ctx, torch_cuda, build_algo):
     torch = torch_cuda
     m, k = oc.params(100, 0.01)
     words = seb.new_words(m)
@@ -297,7 +345,7 @@ def test_empty_batches(seb, ctx, torch_cuda):
     assert ctx.probe(np.zeros((0, 16), np.uint8), np.zeros(seb.num_bytes(m), np.uint8), m, k).size == 0
 
 
-def test_fuzz_against_oracle(seb, ctx):
+def test_fuzz_against_oracle(seb, ctx, build_algo):
     rng = np.random.default_rng(11)
     for trial in range(12):
         n = int(rng.integers(1, 3000))
