@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--build-algo", type=int, default=None, help="0 auto, 1 atomic, 2 bucketed")
     ap.add_argument("--probe-split", type=int, default=None)
+    ap.add_argument("--probe-kpt", type=int, default=None)
+    ap.add_argument("--probe-slice-shift", type=int, default=None)
+    ap.add_argument("--probe-slice-grid", type=int, default=None)
     return ap.parse_args()
 
 
@@ -77,6 +80,12 @@ def main():
         seb.set_option("build_algo", args.build_algo)
     if args.probe_split is not None:
         seb.set_option("probe_split", args.probe_split)
+    if args.probe_kpt is not None:
+        seb.set_option("probe_kpt", args.probe_kpt)
+    if args.probe_slice_shift is not None:
+        seb.set_option("probe_slice_shift", args.probe_slice_shift)
+    if args.probe_slice_grid is not None:
+        seb.set_option("probe_slice_grid", args.probe_slice_grid)
 
     n = args.keys
     p = 0.01
@@ -207,7 +216,8 @@ def main():
                          "other": {d: {"ms": round(v[0], 4), "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 2)}
                                    for d, v in kern.items()}},
             "parity": parity,
-            "options": {o: seb.get_option(o) for o in ("build_algo", "probe_split", "bucket_min_keys")},
+            "options": {o: seb.get_option(o) for o in ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift",
+                                                        "probe_slice_grid", "bucket_min_keys")},
         }
         if world == 1 and args.config == "c2c3" and not args.no_host_inclusive:
             result["host_inclusive"] = host_inclusive(seb, build_host, probe_host, m, k)

@@ -72,7 +72,8 @@ uint64_t seb_words_bytes(uint64_t num_bits);
 int seb_abi_version(void);
 /* Process-wide tuning knobs (results never change, only speed):
  *   "build_algo"      0 auto, 1 device-scope atomic OR, 2 radix-partitioned LDS build
- *   "probe_split"     k == 7 probes: words gathered before the first test (0 = all 7 at once)
+ *   "probe_split"     k == 7 probes: words gathered before the first test (0 = all 7, 2, 3)
+ *   "probe_kpt"       k == 7 probes: keys per thread (1, 2, 4) — gathers in flight per lane
  *   "bucket_min_keys" auto build_algo: radix-partitioned from this many keys on
  *   "grid_cap"        maximum workgroups of the grid-stride kernels
  * Environment variables SEB_BUILD_ALGO, SEB_PROBE_SPLIT, SEB_BUCKET_MIN_KEYS, SEB_GRID_CAP set the

@@ -98,6 +98,9 @@ static void load_env() {
     if (env_flag("SEB_GRID_CAP", &v) && v > 0) o.grid_cap = (unsigned)v;
     if (env_flag("SEB_BUILD_ALGO", &v)) o.build_algo = (int)v;
     if (env_flag("SEB_PROBE_SPLIT", &v)) o.probe_split = (int)v;
+    if (env_flag("SEB_PROBE_KPT", &v)) o.probe_kpt = (int)v;
+    if (env_flag("SEB_PROBE_SLICE_SHIFT", &v)) o.probe_slice_shift = (int)v;
+    if (env_flag("SEB_PROBE_SLICE_GRID", &v)) o.probe_slice_grid = (unsigned)v;
     if (env_flag("SEB_BUCKET_MIN_KEYS", &v) && v >= 0) o.bucket_min_keys = (uint64_t)v;
 }
 
@@ -106,7 +109,10 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     if (!name) return fail(SEB_ERR_INVALID, "seb_set_option: null name");
     Options &o = options();
     if (!strcmp(name, "build_algo") && value >= 0 && value <= 2) o.build_algo = (int)value;
-    else if (!strcmp(name, "probe_split") && value >= 0 && value <= 7) o.probe_split = (int)value;
+    else if (!strcmp(name, "probe_split") && (value == 0 || value == 2 || value == 3)) o.probe_split = (int)value;
+    else if (!strcmp(name, "probe_kpt") && (value == 1 || value == 2 || value == 4)) o.probe_kpt = (int)value;
+    else if (!strcmp(name, "probe_slice_shift") && value >= 0 && value <= 26) o.probe_slice_shift = (int)value;
+    else if (!strcmp(name, "probe_slice_grid") && value >= 0) o.probe_slice_grid = (unsigned)value;
     else if (!strcmp(name, "grid_cap") && value > 0 && value <= (1 << 30)) o.grid_cap = (unsigned)value;
     else if (!strcmp(name, "bucket_min_keys") && value >= 0) o.bucket_min_keys = (uint64_t)value;
     else return fail(SEB_ERR_INVALID, "seb_set_option: bad option %s=%lld", name, (long long)value);
@@ -119,6 +125,9 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     const Options &o = options();
     if (!strcmp(name, "build_algo")) *value = o.build_algo;
     else if (!strcmp(name, "probe_split")) *value = o.probe_split;
+    else if (!strcmp(name, "probe_kpt")) *value = o.probe_kpt;
+    else if (!strcmp(name, "probe_slice_shift")) *value = o.probe_slice_shift;
+    else if (!strcmp(name, "probe_slice_grid")) *value = o.probe_slice_grid;
     else if (!strcmp(name, "grid_cap")) *value = o.grid_cap;
     else if (!strcmp(name, "bucket_min_keys")) *value = (int64_t)o.bucket_min_keys;
     else return fail(SEB_ERR_INVALID, "seb_get_option: unknown option %s", name);

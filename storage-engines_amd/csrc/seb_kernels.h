@@ -48,7 +48,10 @@ struct ManyArg {
 // Process-wide tuning knobs (seb_set_option).
 struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed)
-    int probe_split = 3;          // k == 7 probes: gathers in the first round (0 or >= 7: all at once)
+    int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)
+    int probe_kpt = 2;            // k == 7 probes: keys per thread (1, 2, 4)
+    int probe_slice_shift = 19;   // k == 7, m < 2^32: sliced probe with 2^shift-word (2 MiB) slices (0 = off)
+    unsigned probe_slice_grid = 0;  // workgroups of the sliced probe (0 = one thread per KPT keys)
     uint64_t bucket_min_keys = 1u << 18;  // auto: bucketed build from this many keys on
     unsigned grid_cap = 1u << 20;
 };

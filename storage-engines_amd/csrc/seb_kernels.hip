@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "seb_device.h"
 #include "seb_kernels.h"
 
@@ -36,32 +38,97 @@ __global__ __launch_bounds__(256) void k_build(Src src, uint64_t n, uint32_t *__
     }
 }
 
-// Probe: one thread per key, 0/1 byte out; the answer is the AND of the k bits, as the
-// reference's early-exit loop returns.  KFIX == 7 computes all 7 positions first, gathers the
-// first SPLIT words, and gathers the rest only where those bits are all set (a key whose first
-// bits are clear is already "absent": fewer fabric reads, same answer).  SPLIT == 0: all at once.
-template <typename Src, int KFIX, bool M32, int SPLIT>
+// Probe: the answer is the AND of the k bits, as the reference's early-exit loop returns
+// (lsm/bloom.go:82-92); 0/1 byte out.  The k == 7 kernel is built for memory-level parallelism:
+// each thread owns KPT keys, computes all 7 positions of each, gathers the first SPLIT words of
+// every key, and gathers the remaining ones only for keys whose bits so far are all set (a key
+// with a clear bit is already "absent": fewer fabric reads, the same answer).
+template <typename Src, int KFIX, bool M32, int SPLIT, int KPT>
 __global__ __launch_bounds__(256) void k_probe(Src src, uint64_t n, const uint32_t *__restrict__ words, ModArg md,
                                                uint8_t *__restrict__ out) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        uint64_t h1, h2;
-        src.hash(i, h1, h2);
-        uint32_t acc = 1u;
-        if constexpr (KFIX > 0 && SPLIT > 0 && SPLIT < KFIX) {
-            uint64_t pos[KFIX];
-            for_positions<KFIX, M32>(h1, h2, md, KFIX, [&](uint32_t q, uint64_t p) { pos[q] = p; });
+    if constexpr (KFIX > 0) {
+        using P = typename std::conditional<M32, uint32_t, uint64_t>::type;
+        constexpr int S = (SPLIT > 0 && SPLIT < KFIX) ? SPLIT : KFIX;
+        const uint64_t span = (uint64_t)blockDim.x * KPT;
+        for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
+            P pos[KPT][KFIX];
+            uint32_t acc[KPT];
 #pragma unroll
-            for (int q = 0; q < SPLIT; ++q) acc &= words[pos[q] >> 5] >> (uint32_t)(pos[q] & 31);
-            if (acc & 1u) {
-#pragma unroll
-                for (int q = SPLIT; q < KFIX; ++q) acc &= words[pos[q] >> 5] >> (uint32_t)(pos[q] & 31);
+            for (int r = 0; r < KPT; ++r) {
+                const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+                uint64_t h1 = 0, h2 = 0;
+                if (i < n) src.hash(i, h1, h2);
+                for_positions<KFIX, M32>(h1, h2, md, KFIX, [&](uint32_t q, uint64_t p) { pos[r][q] = (P)p; });
+                acc[r] = i < n ? 1u : 0u;
             }
-        } else {
-            for_positions<KFIX, M32>(h1, h2, md, md.k,
-                                     [&](uint32_t, uint64_t p) { acc &= words[p >> 5] >> (uint32_t)(p & 31); });
+#pragma unroll
+            for (int r = 0; r < KPT; ++r)
+#pragma unroll
+                for (int q = 0; q < S; ++q)
+                    if (acc[r]) acc[r] &= words[pos[r][q] >> 5] >> (uint32_t)(pos[r][q] & 31);
+            if constexpr (S < KFIX) {
+#pragma unroll
+                for (int r = 0; r < KPT; ++r)
+                    if (acc[r] & 1u) {
+#pragma unroll
+                        for (int q = S; q < KFIX; ++q) acc[r] &= words[pos[r][q] >> 5] >> (uint32_t)(pos[r][q] & 31);
+                    }
+            }
+#pragma unroll
+            for (int r = 0; r < KPT; ++r) {
+                const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+                if (i < n) out[i] = (uint8_t)(acc[r] & 1u);
+            }
         }
-        out[i] = (uint8_t)(acc & 1u);
+    } else {
+        const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+            uint64_t h1, h2;
+            src.hash(i, h1, h2);
+            uint32_t acc = 1u;
+            for_positions<0, M32>(h1, h2, md, md.k,
+                                  [&](uint32_t, uint64_t p) { acc &= words[p >> 5] >> (uint32_t)(p & 31); });
+            out[i] = (uint8_t)(acc & 1u);
+        }
+    }
+}
+
+// Sliced probe (k == 7, m < 2^32): a filter larger than one XCD's 4 MiB L2 is probed in
+// phases.  Each thread keeps the 7 positions of its KPT keys in registers and, in phase s, gathers
+// only the words of slice s (2^slice_shift words).  Workgroups that progress at the same pace on
+// one XCD then share a single slice in that XCD's L2 instead of thrashing the whole filter; a
+// key whose bits so far include a clear one skips its remaining gathers.  Which slice a gather
+// belongs to changes only when it is issued, never the answer.
+template <typename Src, int KPT>
+__global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, const uint32_t *__restrict__ words,
+                                                      ModArg md, uint8_t *__restrict__ out, uint32_t slice_shift,
+                                                      uint32_t nslices) {
+    const uint64_t span = (uint64_t)blockDim.x * KPT;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
+        uint32_t pos[KPT][7];
+        uint32_t acc[KPT];
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            uint64_t h1 = 0, h2 = 0;
+            if (i < n) src.hash(i, h1, h2);
+            for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
+            acc[r] = i < n ? 1u : 0u;
+        }
+        for (uint32_t sl = 0; sl < nslices; ++sl) {
+#pragma unroll
+            for (int r = 0; r < KPT; ++r)
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    const uint32_t w = pos[r][q] >> 5;
+                    if ((acc[r] & 1u) && (w >> slice_shift) == sl) acc[r] &= words[w] >> (pos[r][q] & 31);
+                }
+        }
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            if (i < n) out[i] = (uint8_t)(acc[r] & 1u);
+        }
     }
 }
 
@@ -151,31 +218,53 @@ static hipError_t launch_build_t(const Src &src, uint64_t n, uint32_t *words, co
     return hipGetLastError();
 }
 
-template <typename Src, int KFIX, bool M32, int SPLIT>
+template <typename Src, int KFIX, bool M32, int SPLIT, int KPT>
 static hipError_t launch_probe_t(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
                                  hipStream_t s) {
-    unsigned g = grid_for(n, 256, options().grid_cap);
-    hipLaunchKernelGGL((k_probe<Src, KFIX, M32, SPLIT>), dim3(g), dim3(256), 0, s, src, n, words, md, out);
+    unsigned g = grid_for((n + KPT - 1) / KPT, 256, options().grid_cap);
+    hipLaunchKernelGGL((k_probe<Src, KFIX, M32, SPLIT, KPT>), dim3(g), dim3(256), 0, s, src, n, words, md, out);
+    return hipGetLastError();
+}
+
+template <typename Src, bool M32, int SPLIT>
+static hipError_t launch_probe7k(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
+                                 hipStream_t s) {
+    switch (options().probe_kpt) {
+        case 1: return launch_probe_t<Src, 7, M32, SPLIT, 1>(src, n, words, md, out, s);
+        case 4: return launch_probe_t<Src, 7, M32, SPLIT, 4>(src, n, words, md, out, s);
+        default: return launch_probe_t<Src, 7, M32, SPLIT, 2>(src, n, words, md, out, s);
+    }
+}
+
+template <typename Src, int KPT>
+static hipError_t launch_sliced_t(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
+                                  uint32_t shift, uint32_t nslices, hipStream_t s) {
+    const Options &o = options();
+    unsigned g = grid_for((n + KPT - 1) / KPT, 256, o.probe_slice_grid ? o.probe_slice_grid : o.grid_cap);
+    hipLaunchKernelGGL((k_probe_sliced<Src, KPT>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift, nslices);
     return hipGetLastError();
 }
 
 template <typename Src, bool M32>
 static hipError_t launch_probe7(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
                                 hipStream_t s) {
-    switch (options().probe_split) {
-        case 2: return launch_probe_t<Src, 7, M32, 2>(src, n, words, md, out, s);
-        case 3: return launch_probe_t<Src, 7, M32, 3>(src, n, words, md, out, s);
-        case 4: return launch_probe_t<Src, 7, M32, 4>(src, n, words, md, out, s);
-        default: return launch_probe_t<Src, 7, M32, 0>(src, n, words, md, out, s);
+    const Options &o = options();
+    const uint64_t nwords = (md.m + 31) / 32;
+    if constexpr (M32) {
+        if (o.probe_slice_shift > 0 && (nwords >> o.probe_slice_shift) > 0) {  // filter spans > 1 slice
+            const uint32_t nsl = (uint32_t)((nwords + (1ull << o.probe_slice_shift) - 1) >> o.probe_slice_shift);
+            switch (o.probe_kpt) {
+                case 1: return launch_sliced_t<Src, 1>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
+                case 4: return launch_sliced_t<Src, 4>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
+                default: return launch_sliced_t<Src, 2>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
+            }
+        }
     }
-}
-
-template <typename Src, typename MaskT, bool SAME, int KFIX, bool M32>
-static hipError_t launch_multi_t(const Src &src, uint64_t n, const MultiArg &ma, void *mask, hipStream_t s) {
-    unsigned g = grid_for(n, 256, options().grid_cap);
-    hipLaunchKernelGGL((k_probe_multi<Src, MaskT, SAME, KFIX, M32>), dim3(g), dim3(256), 0, s, src, n, ma,
-                       (MaskT *)mask);
-    return hipGetLastError();
+    switch (o.probe_split) {
+        case 0: return launch_probe7k<Src, M32, 0>(src, n, words, md, out, s);
+        case 2: return launch_probe7k<Src, M32, 2>(src, n, words, md, out, s);
+        default: return launch_probe7k<Src, M32, 3>(src, n, words, md, out, s);
+    }
 }
 
 hipError_t launch_build(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s) {
@@ -196,9 +285,17 @@ hipError_t launch_probe(const KeyBatch &kb, const uint32_t *words, const ModArg 
     const bool k7 = md.k == 7;
     return with_src(kb, [&](auto src) {
         using S = decltype(src);
-        if (m32) return k7 ? launch_probe7<S, true>(src, kb.n, words, md, out, s) : launch_probe_t<S, 0, true, 0>(src, kb.n, words, md, out, s);
-        return k7 ? launch_probe7<S, false>(src, kb.n, words, md, out, s) : launch_probe_t<S, 0, false, 0>(src, kb.n, words, md, out, s);
+        if (m32) return k7 ? launch_probe7<S, true>(src, kb.n, words, md, out, s) : launch_probe_t<S, 0, true, 0, 1>(src, kb.n, words, md, out, s);
+        return k7 ? launch_probe7<S, false>(src, kb.n, words, md, out, s) : launch_probe_t<S, 0, false, 0, 1>(src, kb.n, words, md, out, s);
     });
+}
+
+template <typename Src, typename MaskT, bool SAME, int KFIX, bool M32>
+static hipError_t launch_multi_t(const Src &src, uint64_t n, const MultiArg &ma, void *mask, hipStream_t s) {
+    unsigned g = grid_for(n, 256, options().grid_cap);
+    hipLaunchKernelGGL((k_probe_multi<Src, MaskT, SAME, KFIX, M32>), dim3(g), dim3(256), 0, s, src, n, ma,
+                       (MaskT *)mask);
+    return hipGetLastError();
 }
 
 template <typename MaskT>

@@ -171,9 +171,11 @@ def build_algo(request, seb):
         yield request.param
 
 
-@pytest.fixture(params=[0, 2, 3, 4], ids=lambda v: f"split{v}")
+@pytest.fixture(params=[(0, 1, 0), (2, 2, 0), (3, 1, 0), (3, 2, 0), (3, 4, 0), (0, 4, 0), (3, 1, 12), (3, 2, 10),
+                        (3, 4, 13)], ids=lambda v: f"split{v[0]}-kpt{v[1]}-slice{v[2]}")
 def probe_split(request, seb):
-    with seb.option("probe_split", request.param):
+    with seb.option("probe_split", request.param[0]), seb.option("probe_kpt", request.param[1]), \
+            seb.option("probe_slice_shift", request.param[2]):
         yield request.param
 
 
@@ -307,11 +309,19 @@ def test_probe_split_variants(seb, golden, torch_cuda, probe_split):
     row = next(r for r in golden["fixed16"] if r["n"] == 100000 and r["p"] == 0.01)
     n, m, k = row["n"], row["m"], row["k"]
     kd = seb.dev_keys(to_dev(torch, kg.key16(np.arange(n))), n=n, stride=16)
-    words, _ = dev_build_bits(seb, torch, kd, m, k)
+    words, bits = dev_build_bits(seb, torch, kd, m, k)
     out = torch.empty(n, dtype=torch.uint8, device="cuda")
     seb.dev_probe(seb.dev_keys(to_dev(torch, kg.key16(kg.probe_indices(n))), n=n, stride=16), words, m, k, out)
     torch.cuda.synchronize()
     assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
+    for nn in (1, 255, 513, 1001):  # ragged tails of the multi-key threads
+        pk = kg.key16(kg.probe_indices(nn))
+        o = torch.full((nn + 8,), 7, dtype=torch.uint8, device="cuda")
+        seb.dev_probe(seb.dev_keys(to_dev(torch, pk), n=nn, stride=16), words, m, k, o)
+        torch.cuda.synchronize()
+        got = o.cpu().numpy()
+        assert np.array_equal(got[:nn], oc.probe(bits, m, k, pk, nn, stride=16))
+        assert (got[nn:] == 7).all()  # nothing written past n
 
 
 def test_dev_build_with_caller_workspace(seb, golden, torch_cuda):

@@ -12,9 +12,9 @@ ARGS=${@:-"--steps 10 --warmup 3 --no-cpu-baseline --no-host-inclusive"}
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o bench --output-format csv -- \
     python3 "$ROOT/bench.py" $ARGS > "$OUT/trace.log" 2>&1
 i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_ATOMIC_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_ATOMIC_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES"; do
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --pmc $grp -d "$OUT/pmc$i" -o bench --output-format csv -- \
-        python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive > "$OUT/pmc$i.log" 2>&1 || \
+        python3 "$ROOT/bench.py" $ARGS --steps 3 --warmup 1 > "$OUT/pmc$i.log" 2>&1 || \
         { echo "pmc group '$grp' failed" >> "$OUT/pmc_fail.txt"; tail -5 "$OUT/pmc$i.log" >> "$OUT/pmc_fail.txt"; }
 done
