@@ -1,0 +1,103 @@
+"""CPU: the multi-GPU orchestration (filter sharding, key-batch broadcast, plane gather, mask
+assembly) in world-size-2 and 3 process groups on the gloo backend, with the oracle as the probe
+function.  The GPU run uses the same code with nccl (RCCL) and libseb_bloom's kernel."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import dist_probe as dp
+import keygen as kg
+from oracle import oracle_c as oc
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _filters(nf, per, p=0.01):
+    m, k = oc.params(per, p)
+    return [(oc.build(m, k, kg.key16(f * per + np.arange(per)), per, stride=16), m, k) for f in range(nf)]
+
+
+def _oracle_probe_fn(keys: torch.Tensor, local_filters, plane: torch.Tensor) -> None:
+    arr = keys.numpy()
+    mask = oc.probe_multi(list(local_filters), arr, arr.shape[0], stride=arr.shape[1])
+    plane.copy_(torch.from_numpy(mask.astype(np.int64)).to(plane.dtype))
+
+
+def _worker(rank, world, port, nf, per, nprobe, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shard = dp.FilterShard(nf, rank, world)
+        all_f = _filters(nf, per)
+        local = all_f[shard.lo: shard.hi]
+        if rank == 0:
+            qq = np.arange(nprobe)
+            half = qq // 2
+            keys = torch.from_numpy(kg.key16(np.where(qq % 2 == 0, (half % nf) * per + half // nf, nf * per + qq)))
+        else:
+            keys = torch.zeros((nprobe, 16), dtype=torch.uint8)  # filled by the broadcast
+        mask = dp.sharded_probe(keys, local, shard, _oracle_probe_fn)
+        q.put((rank, mask))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,nf", [(2, 5), (2, 2), (3, 8), (2, 1)])
+def test_sharded_probe_matches_single_process(world, nf):
+    per, nprobe = 3000, 4000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, nf, per, nprobe, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    qq = np.arange(nprobe)
+    half = qq // 2
+    keys = kg.key16(np.where(qq % 2 == 0, (half % nf) * per + half // nf, nf * per + qq))
+    ref = oc.probe_multi(_filters(nf, per), keys, nprobe, stride=16)
+    for r in range(world):
+        assert np.array_equal(results[r], ref), r
+    owner = half % nf
+    assert np.all(((ref[0::2] >> owner[0::2].astype(np.uint64)) & np.uint64(1)) == 1)  # no false negatives
+
+
+def test_filter_shard_partition():
+    for nf in (1, 7, 64):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for r in range(world):
+                s = dp.FilterShard(nf, r, world)
+                seen += list(range(s.lo, s.hi))
+                for f in range(s.lo, s.hi):
+                    assert s.owner(f) == r
+            assert seen == list(range(nf))
+    assert dp.FilterShard(64, 0, 8).plane_dtype() == torch.uint8
+    assert dp.FilterShard(64, 0, 1).plane_dtype() == torch.int64
+    assert dp.FilterShard(64, 0, 4).plane_dtype() == torch.int16
+
+
+def test_assemble_mask_high_bits():
+    # 64 filters on one rank: bit 63 must survive the int64 plane
+    plane = torch.tensor([-1, 1 << 62, 0], dtype=torch.int64)
+    m = dp.assemble_mask([plane], 64)
+    assert m[0] == np.uint64(0xFFFFFFFFFFFFFFFF) and m[1] == np.uint64(1 << 62) and m[2] == 0
+    # two ranks of 16-bit planes with the sign bit set
+    p0 = torch.tensor([-32768], dtype=torch.int16)
+    p1 = torch.tensor([1], dtype=torch.int16)
+    assert dp.assemble_mask([p0, p1], 32)[0] == np.uint64((1 << 15) | (1 << 16))

@@ -1,0 +1,83 @@
+"""Summarise a tools/gpu_profile.sh run (gpurun_out/prof_TAG) into profiles/ (committed).
+
+    python tools/summarize_profile.py TAG [--config c2c3]
+
+Writes profiles/TAG_kernel_stats.csv (the rocprofv3 --kernel-trace --stats summary, verbatim),
+profiles/TAG_pmc.csv (per-kernel mean of every PMC counter over its dispatches) and merges the
+per-launch HBM traffic of the build and probe steps into profiles/pmc_r01.json, which bench.py
+reports as roofline.traffic.
+
+HBM bytes per launch, per MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB and
+come from the L2's memory-side (EA) request counters (Infinity-Cache hits included).  gfx950's
+FETCH_SIZE counts exactly half the bytes of a wide (16 B/lane) coalesced streaming read; the only
+such stream in these kernels is the key batch (16 B per key, dwordx4 per lane), so
+    read  = FETCH_SIZE*1024 + key_bytes/2      (the streamed half FETCH_SIZE misses)
+    write = WRITE_SIZE*1024
+The random 4-byte gathers of the probe are one 64-B EA request each (TCC_EA0_RDREQ), which
+FETCH_SIZE counts at 64 B; they need no correction.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STEP_KERNELS = {
+    "build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned"),
+    "probe": ("k_probe",),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--config", default="c2c3")
+    ap.add_argument("--key-bytes", type=float, default=16.0 * 10_000_000)
+    ap.add_argument("--out-tag", default=None)
+    a = ap.parse_args()
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
+    tag = a.out_tag or a.tag
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "bench_kernel_stats.csv"),
+                os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
+    agg = collections.defaultdict(list)
+    for fn in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv"))):
+        for r in csv.DictReader(open(fn)):
+            agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    rows = sorted((k, c, sum(v) / len(v), len(v)) for (k, c), v in agg.items())
+    with open(os.path.join(ROOT, "profiles", f"{tag}_pmc.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "counter", "mean_per_dispatch", "dispatches"])
+        for k, c, v, cnt in rows:
+            w.writerow([k, c, f"{v:.6g}", cnt])
+    mean = {(k, c): v for k, c, v, _ in rows}
+    steps = {}
+    for step, pats in STEP_KERNELS.items():
+        fetch = write = 0.0
+        kernels = []
+        for (k, c), v in mean.items():
+            if any(p in k for p in pats) and "seb::" in k or (step == "build" and "fillBufferAligned" in k):
+                if c == "FETCH_SIZE":
+                    fetch += v
+                    kernels.append(k)
+                elif c == "WRITE_SIZE":
+                    write += v
+        read = fetch * 1024 + a.key_bytes / 2
+        steps[step] = {"hbm_bytes_per_launch": int(read + write * 1024), "read_bytes": int(read),
+                       "write_bytes": int(write * 1024), "fetch_size_kib": fetch, "write_size_kib": write,
+                       "kernels": sorted(set(kernels)), "source": f"profiles/{tag}_pmc.csv"}
+    out = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    doc = json.load(open(out)) if os.path.exists(out) else {}
+    doc[a.config] = steps
+    doc["_correction"] = __doc__.split("HBM bytes per launch")[1].strip()
+    json.dump(doc, open(out, "w"), indent=1)
+    print(json.dumps(steps, indent=1))
+
+
+if __name__ == "__main__":
+    main()
