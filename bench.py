@@ -1,14 +1,18 @@
 """Bloom build + probe benchmark (BASELINE.json metric), one process per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2c3|c4]
-    torchrun --nproc-per-node N bench.py --gpus N ...        (RCCL over xGMI)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2c3|c4|c5]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...   (RCCL over xGMI)
 
-One step on every GPU = clear + build one SSTable filter from 10M x 16-B keys @1% FPR
-(BASELINE C2; m = 95,850,584, k = 7) and probe a 10M-key batch against it (C3, 50% present).
-Rank g builds the filter of its own SSTable (keys key16(g*n + i)); the probe batch arrives on
-rank 0 and is RCCL-broadcast to every GPU, double-buffered so the broadcast of batch j+1 overlaps
-step j.  Per-GPU work is fixed as N grows (weak scaling); value = (build + probe keys over all
-ranks) / max-over-ranks wall time, inputs already resident in HBM.
+c2c3 (default, the metric's config): one step on every GPU = clear + build one SSTable filter
+from 10M x 16-B keys @1% FPR (BASELINE C2; m = 95,850,584, k = 7) and probe a 10M-key batch
+against it (C3, 50% present).  Rank g builds the filter of its own SSTable (keys key16(g*n + i));
+the probe batch arrives on rank 0 and is RCCL-broadcast to every GPU, double-buffered so the
+broadcast of batch j+1 overlaps step j.  Per-GPU work is fixed as N grows (weak scaling); value =
+(build + probe keys over all ranks) / max-over-ranks wall time, inputs already resident in HBM.
+c4: the same with variable-length keys (8-256 B, zipf); no broadcast.
+c5: 64 compaction-sized filters (100K keys each) sharded over the ranks, a 10M-key batch
+broadcast from rank 0, multi-filter probe, masks all-gathered (strong scaling; value = batch
+keys / s).
 
 Printed (rank 0): one JSON line with the metric, a `roofline` object for the dominant kernel
 (algorithmic bytes / hipEvent-measured launch time on the launch stream) and a `cpu_baseline`
@@ -33,6 +37,9 @@ METRIC = "bloom build+probe Mkeys/s device-resident, 10M×16B keys @1% FPR, 1/2/
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
 GOLDEN_C2 = "a86f3c69041ea0caac1dc559cfb36b06d5d5513d4ee203d22878715f612a0c3a"  # sha256(Encode()) n=10M
 GOLDEN_C3 = "aba77536fae51d566de525f519cd4c573799880d63000d88a2ce3052d0b90f95"  # sha256(answers)
+GOLDEN_C5 = "0668715db8804f529bc6795461a1cbd9905bbaab44b18b88a3b29881cd29f375"  # sha256(u64 masks)
+OPTIONS = ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "bucket_min_keys",
+           "multi_interleave")
 
 
 def sha(b) -> str:
@@ -44,17 +51,158 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4"])
+    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5"])
     ap.add_argument("--keys", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=1)
-    ap.add_argument("--build-algo", type=int, default=None, help="0 auto, 1 atomic, 2 bucketed")
-    ap.add_argument("--probe-split", type=int, default=None)
-    ap.add_argument("--probe-kpt", type=int, default=None)
-    ap.add_argument("--probe-slice-shift", type=int, default=None)
-    ap.add_argument("--probe-slice-grid", type=int, default=None)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N>1 on one GPU")
+    for o in OPTIONS:
+        ap.add_argument("--" + o.replace("_", "-"), type=int, default=None)
     return ap.parse_args()
+
+
+class Setup:
+    """Inputs resident in HBM plus the per-step work of one config."""
+
+    workload = ""
+    parallelism = ""
+    scaling = "weak"
+    units_per_step = 0.0
+    kernel_bytes: dict = {}
+    build = None
+    build_host = probe_host = None
+    broadcast_bufs = None
+
+
+def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
+    st = Setup()
+    n = args.keys
+    m, k = seb.params(n, 0.01)
+    st.m, st.k, st.n = m, k, n
+    st.build_host = kg.key16(rank * n + np.arange(n))
+    build_keys = torch.from_numpy(st.build_host).to(dev)
+    st.kb = seb.dev_keys(build_keys, n=n, stride=16)
+    st.probe_host = kg.key16(kg.probe_indices(n)) if rank == 0 else None
+    st.pbufs = [torch.zeros((n, 16), dtype=torch.uint8, device=dev) for _ in range(2)]
+    if rank == 0:
+        st.pbufs[0].copy_(torch.from_numpy(st.probe_host))
+        st.pbufs[1].copy_(st.pbufs[0])
+    st.pk = [seb.dev_keys(b, n=n, stride=16) for b in st.pbufs]
+    st.words = seb.new_words(m, device=dev)
+    st.out = torch.empty(n, dtype=torch.uint8, device=dev)
+    nb = (m + 7) // 8
+    st.kernel_bytes = {"build": 16.0 * n + 2 * nb, "probe": 16.0 * n + nb + n}
+    st.units_per_step = 2.0 * n * world
+    st.broadcast_bufs = st.pbufs if world > 1 else None
+    st.workload = ("C2+C3: per GPU build one filter from 10M x 16B keys @1% FPR (m=95,850,584, k=7) "
+                   "+ probe a 10M-key batch (50% present) RCCL-broadcast from rank 0")
+    st.parallelism = f"filter-per-gpu x{world}, probe batch broadcast (RCCL)"
+
+    def build():
+        seb.dev_clear(st.words, m)
+        seb.dev_build(st.kb, st.words, m, k)
+
+    def probe(j):
+        seb.dev_probe(st.pk[j % 2], st.words, m, k, st.out)
+
+    def parity():
+        if n != 10_000_000 or rank != 0:
+            return None
+        bits = seb.words_to_bits(st.words, m)
+        ok_b = sha(m.to_bytes(8, "little") + k.to_bytes(4, "little") + bits.tobytes()) == GOLDEN_C2
+        ok_p = sha(st.out.cpu().numpy().tobytes()) == GOLDEN_C3
+        return ("bit-exact (sha256 of Encode() and of the 10M answers match tests/golden)" if ok_b and ok_p
+                else f"MISMATCH build={ok_b} probe={ok_p}")
+
+    st.build, st.probe, st.parity = build, probe, parity
+    return st
+
+
+def setup_c4(args, seb, kg, torch, dev, rank, world, dist):
+    st = Setup()
+    n = args.keys
+    m, k = seb.params(n, 0.01)
+    st.m, st.k, st.n = m, k, n
+    bd, bo = kg.varlen_keys(rank * n + np.arange(n))
+    st.kb = seb.dev_keys(torch.from_numpy(bd).to(dev), torch.from_numpy(bo.view(np.int64)).to(dev))
+    pd, po = kg.varlen_keys(kg.probe_indices(n))
+    pk = seb.dev_keys(torch.from_numpy(pd).to(dev), torch.from_numpy(po.view(np.int64)).to(dev))
+    st.pk = [pk, pk]
+    st.words = seb.new_words(m, device=dev)
+    st.out = torch.empty(n, dtype=torch.uint8, device=dev)
+    nb = (m + 7) // 8
+    st.kernel_bytes = {"build": float(bo[-1]) + 8.0 * (n + 1) + 2 * nb,
+                       "probe": float(po[-1]) + 8.0 * (n + 1) + nb + n}
+    st.units_per_step = 2.0 * n * world
+    st.workload = ("C4: per GPU build + probe 10M variable-length keys 8-256 B (zipf s=1.1, mean 39.95 B) @1% FPR "
+                   f"({bo[-1] / 1e6:.1f} MB of build keys)")
+    st.parallelism = f"filter-per-gpu x{world}"
+
+    def build():
+        seb.dev_clear(st.words, m)
+        seb.dev_build(st.kb, st.words, m, k)
+
+    def parity():
+        if rank != 0:
+            return None
+        ok = bool(st.out.cpu().numpy()[0::2].all())  # every even probe is a built key
+        return "no false negatives on the 5M present probes (bit-exactness: tests/test_gpu_parity.py C4)" if ok \
+            else "MISMATCH: false negative"
+
+    st.build = build
+    st.probe = lambda j: seb.dev_probe(st.pk[j % 2], st.words, m, k, st.out)
+    st.parity = parity
+    return st
+
+
+def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
+    import dist_probe as dp
+
+    st = Setup()
+    nf, per, n = 64, 100_000, args.keys
+    m, k = seb.params(per, 0.01)
+    st.m, st.k, st.n = m, k, n
+    shard = dp.FilterShard(nf, rank, world)
+    fkeys = torch.from_numpy(kg.key16(shard.lo * per + np.arange(shard.count * per))).to(dev)
+    st.local = [(seb.new_words(m, device=dev), m, k) for _ in range(shard.count)]
+    if shard.count:
+        seb.dev_build_many(seb.dev_keys(fkeys, n=shard.count * per, stride=16),
+                           [j * per for j in range(shard.count + 1)], st.local)
+    torch.cuda.synchronize()
+    q = np.arange(n, dtype=np.int64)
+    half = q // 2
+    probe_host = kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q)) if rank == 0 else None
+    st.pbufs = [torch.zeros((n, 16), dtype=torch.uint8, device=dev) for _ in range(2)]
+    if rank == 0:
+        st.pbufs[0].copy_(torch.from_numpy(probe_host))
+        st.pbufs[1].copy_(st.pbufs[0])
+    st.pk = [seb.dev_keys(b, n=n, stride=16) for b in st.pbufs]
+    st.plane = torch.zeros(n, dtype=shard.plane_dtype(), device=dev)
+    st.planes = [torch.empty_like(st.plane) for _ in range(world)]
+    st.kernel_bytes = {"probe": 16.0 * n + shard.count * ((m + 7) // 8) + st.plane.element_size() * n}
+    st.units_per_step = float(n)
+    st.scaling = "strong"
+    st.broadcast_bufs = st.pbufs if world > 1 else None
+    st.workload = ("C5: 64 SSTable filters (100K keys each, m=958,506, k=7) sharded over the GPUs; a 10M-key "
+                   "batch RCCL-broadcast from rank 0, multi-filter probe, u64 masks all-gathered")
+    st.parallelism = f"filters sharded {nf}/{world} per gpu, batch broadcast + mask all-gather (RCCL)"
+
+    def probe(j):
+        if shard.count:
+            seb.dev_probe_multi(st.pk[j % 2], st.local, st.plane)
+        if world > 1:
+            dist.all_gather(st.planes, st.plane)
+
+    def parity():
+        if n != 10_000_000 or rank != 0:
+            return None
+        mask = dp.assemble_mask(st.planes if world > 1 else [st.plane], nf)
+        ok = sha(mask.astype("<u8").tobytes()) == GOLDEN_C5
+        return "bit-exact (sha256 of the 10M u64 masks matches tests/golden c5)" if ok else "MISMATCH masks"
+
+    st.probe, st.parity = probe, parity
+    return st
 
 
 def main():
@@ -70,97 +218,58 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = torch.device("cuda", local % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
     seb.device_check(dev.index)
-    if args.build_algo is not None:
-        seb.set_option("build_algo", args.build_algo)
-    if args.probe_split is not None:
-        seb.set_option("probe_split", args.probe_split)
-    if args.probe_kpt is not None:
-        seb.set_option("probe_kpt", args.probe_kpt)
-    if args.probe_slice_shift is not None:
-        seb.set_option("probe_slice_shift", args.probe_slice_shift)
-    if args.probe_slice_grid is not None:
-        seb.set_option("probe_slice_grid", args.probe_slice_grid)
+    for o in OPTIONS:
+        v = getattr(args, o)
+        if v is not None:
+            seb.set_option(o, v)
 
-    n = args.keys
-    p = 0.01
-    m, k = seb.params(n, p)
-    # ---- inputs, resident in HBM before timing
-    if args.config == "c2c3":
-        build_host = kg.key16(rank * n + np.arange(n))
-        build_keys = torch.from_numpy(build_host).to(dev)
-        kb = seb.dev_keys(build_keys, n=n, stride=16)
-        probe_host = kg.key16(kg.probe_indices(n)) if rank == 0 else None
-        pbufs = [torch.empty((n, 16), dtype=torch.uint8, device=dev) for _ in range(2)]
-        if rank == 0:
-            pbufs[0].copy_(torch.from_numpy(probe_host))
-            pbufs[1].copy_(pbufs[0])
-        pk = [seb.dev_keys(b, n=n, stride=16) for b in pbufs]
-        key_bytes_build = 16.0 * n
-        key_bytes_probe = 16.0 * n
-        workload = ("C2+C3: per GPU build one filter from 10M x 16B keys @1% FPR (m=95,850,584, k=7) "
-                    "+ probe a 10M-key batch (50% present) RCCL-broadcast from rank 0")
-    else:  # c4: variable-length keys 8-256 B (zipf)
-        bd, bo = kg.varlen_keys(rank * n + np.arange(n))
-        bdev, bodev = torch.from_numpy(bd).to(dev), torch.from_numpy(bo.view(np.int64)).to(dev)
-        kb = seb.dev_keys(bdev, bodev)
-        pd, po = kg.varlen_keys(kg.probe_indices(n))
-        pbufs = [(torch.from_numpy(pd).to(dev), torch.from_numpy(po.view(np.int64)).to(dev)) for _ in range(2)]
-        pk = [seb.dev_keys(d, o) for d, o in pbufs]
-        key_bytes_build = float(bo[-1]) + 8.0 * (n + 1)
-        key_bytes_probe = float(po[-1]) + 8.0 * (n + 1)
-        workload = "C4: per GPU build + probe 10M variable-length keys 8-256 B (zipf s=1.1) @1% FPR"
-    words = seb.new_words(m)
-    out = torch.empty(n, dtype=torch.uint8, device=dev)
+    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5}[args.config]
+    st = setup(args, seb, kg, torch, dev, rank, world, dist)
     torch.cuda.synchronize()
-
     stream = torch.cuda.current_stream()
-    ev = {name: [] for name in ("clear0", "build0", "build1", "probe0", "probe1")}
+    times = {"build": [], "probe": []}
 
     def broadcast(j):
-        if world == 1 or args.config != "c2c3":
+        if st.broadcast_bufs is None:
             return None
-        return dist.broadcast(pbufs[j % 2], src=0, async_op=True)
+        return dist.broadcast(st.broadcast_bufs[j % 2], src=0, async_op=True)
 
     def step(j, pending, record):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
-        nxt = broadcast(j + 1)  # next batch rides xGMI while this step computes
-        if record:
-            e[0].record(stream)
-        seb.dev_clear(words, m)
-        seb.dev_build(kb, words, m, k)
-        if record:
-            e[1].record(stream)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        nxt = broadcast(j + 1)  # the next batch rides xGMI while this step computes
+        if st.build is not None:
+            if record:
+                ev[0].record(stream)
+            st.build()
+            if record:
+                ev[1].record(stream)
         if pending is not None:
             pending.wait()
         if record:
-            e[2].record(stream)
-        seb.dev_probe(pk[j % 2], words, m, k, out)
+            ev[2].record(stream)
+        st.probe(j)
         if record:
-            e[3].record(stream)
-            ev["build0"].append(e[0]); ev["build1"].append(e[1])
-            ev["probe0"].append(e[2]); ev["probe1"].append(e[3])
+            ev[3].record(stream)
+            if st.build is not None:
+                times["build"].append((ev[0], ev[1]))
+            times["probe"].append((ev[2], ev[3]))
         return nxt
 
     pending = broadcast(0)
     for j in range(args.warmup):
         pending = step(j, pending, False)
     torch.cuda.synchronize()
-
-    # ---- parity on the same run (rank 0 builds the golden filter; batch from rank 0)
-    parity = None
-    if args.config == "c2c3" and n == 10_000_000 and rank == 0:
-        bits = seb.words_to_bits(words, m)
-        enc = m.to_bytes(8, "little") + k.to_bytes(4, "little") + bits.tobytes()
-        ok_b = sha(enc) == GOLDEN_C2
-        ok_p = sha(out.cpu().numpy().tobytes()) == GOLDEN_C3
-        parity = "bit-exact (sha256 of Encode() and of the 10M answers match tests/golden)" if ok_b and ok_p \
-            else f"MISMATCH build={ok_b} probe={ok_p}"
+    parity = st.parity()  # on the same run, after the warm-up steps
 
     if world > 1:
         dist.barrier()
@@ -180,19 +289,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    build_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(ev["build0"], ev["build1"])]))
-    probe_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(ev["probe0"], ev["probe1"])]))
-    ms_per_step = elapsed * 1000.0 / args.steps
-    total_keys = 2.0 * n * world * args.steps
-    value = total_keys / elapsed / 1e6
-
+    kern_ms = {name: float(np.mean([a.elapsed_time(b) for a, b in pairs])) for name, pairs in times.items() if pairs}
+    value = st.units_per_step * args.steps / elapsed / 1e6
     result = None
     if rank == 0:
-        nb = (m + 7) // 8
-        # algorithmic bytes per launch (DESIGN.md "Roofline accounting")
-        build_bytes = key_bytes_build + nb + nb        # keys + filter write + the clear it ORs into
-        probe_bytes = key_bytes_probe + nb + n         # keys + filter read once + 1 answer byte per key
-        kern = {"build": (build_ms, build_bytes), "probe": (probe_ms, probe_bytes)}
+        kern = {name: (ms, st.kernel_bytes[name]) for name, ms in kern_ms.items()}
         dom = max(kern, key=lambda x: kern[x][0])
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
@@ -202,27 +303,25 @@ def main():
         ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mkeys/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),
+            "higher_is_better": True, "scaling": st.scaling, "vs_baseline": None, "dtype": "u64",
             "data": "synthetic (reference key format user%010d+2B, common/benchmark/keygen.go:89-109)",
-            "config": {"workload": workload, "keys_per_gpu": n, "fpr": p, "num_bits": m, "num_hashes": k,
-                       "parallelism": f"filter-per-gpu x{world}, probe batch broadcast (RCCL)"},
-            "build_gkeys_s": round(n / (build_ms * 1e-3) / 1e9, 3),
-            "probe_gkeys_s": round(n / (probe_ms * 1e-3) / 1e9, 3),
-            "build_ms": round(build_ms, 4), "probe_ms": round(probe_ms, 4),
+            "config": {"workload": st.workload, "keys_per_gpu": st.n, "fpr": 0.01, "num_bits": st.m,
+                       "num_hashes": st.k, "parallelism": st.parallelism},
+            **{f"{name}_gkeys_s": round(st.n / (ms * 1e-3) / 1e9, 3) for name, ms in kern_ms.items()},
+            **{f"{name}_ms": round(ms, 4) for name, ms in kern_ms.items()},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(kern[dom][1]),
                          "other": {d: {"ms": round(v[0], 4), "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 2)}
                                    for d, v in kern.items()}},
             "parity": parity,
-            "options": {o: seb.get_option(o) for o in ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift",
-                                                        "probe_slice_grid", "bucket_min_keys")},
+            "options": {o: seb.get_option(o) for o in OPTIONS},
         }
         if world == 1 and args.config == "c2c3" and not args.no_host_inclusive:
-            result["host_inclusive"] = host_inclusive(seb, build_host, probe_host, m, k)
-        if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(args, n, m, k)
+            result["host_inclusive"] = host_inclusive(seb, st.build_host, st.probe_host, st.m, st.k)
+        if world == 1 and not args.no_cpu_baseline and args.config != "c5":
+            result["cpu_baseline"] = cpu_baseline(args, st.n, st.m, st.k)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

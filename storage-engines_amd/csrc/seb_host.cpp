@@ -99,6 +99,7 @@ static void load_env() {
     if (env_flag("SEB_BUILD_ALGO", &v)) o.build_algo = (int)v;
     if (env_flag("SEB_PROBE_SPLIT", &v)) o.probe_split = (int)v;
     if (env_flag("SEB_PROBE_KPT", &v)) o.probe_kpt = (int)v;
+    if (env_flag("SEB_MULTI_INTERLEAVE", &v)) o.multi_interleave = (int)v;
     if (env_flag("SEB_PROBE_SLICE_SHIFT", &v)) o.probe_slice_shift = (int)v;
     if (env_flag("SEB_PROBE_SLICE_GRID", &v)) o.probe_slice_grid = (unsigned)v;
     if (env_flag("SEB_BUCKET_MIN_KEYS", &v) && v >= 0) o.bucket_min_keys = (uint64_t)v;
@@ -113,6 +114,7 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     else if (!strcmp(name, "probe_kpt") && (value == 1 || value == 2 || value == 4)) o.probe_kpt = (int)value;
     else if (!strcmp(name, "probe_slice_shift") && value >= 0 && value <= 26) o.probe_slice_shift = (int)value;
     else if (!strcmp(name, "probe_slice_grid") && value >= 0) o.probe_slice_grid = (unsigned)value;
+    else if (!strcmp(name, "multi_interleave") && (value == 0 || value == 1)) o.multi_interleave = (int)value;
     else if (!strcmp(name, "grid_cap") && value > 0 && value <= (1 << 30)) o.grid_cap = (unsigned)value;
     else if (!strcmp(name, "bucket_min_keys") && value >= 0) o.bucket_min_keys = (uint64_t)value;
     else return fail(SEB_ERR_INVALID, "seb_set_option: bad option %s=%lld", name, (long long)value);
@@ -128,6 +130,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "probe_kpt")) *value = o.probe_kpt;
     else if (!strcmp(name, "probe_slice_shift")) *value = o.probe_slice_shift;
     else if (!strcmp(name, "probe_slice_grid")) *value = o.probe_slice_grid;
+    else if (!strcmp(name, "multi_interleave")) *value = o.multi_interleave;
     else if (!strcmp(name, "grid_cap")) *value = o.grid_cap;
     else if (!strcmp(name, "bucket_min_keys")) *value = (int64_t)o.bucket_min_keys;
     else return fail(SEB_ERR_INVALID, "seb_get_option: unknown option %s", name);
@@ -285,7 +288,15 @@ extern "C" int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *f
         (rc = fill_multi(filters, nf, mask_bytes, &ma, "seb_dev_probe_multi")))
         return rc;
     if (!mask && keys->n) return fail(SEB_ERR_INVALID, "seb_dev_probe_multi: null mask");
-    HIP_OR_FAIL(launch_probe_multi(key_batch(keys), ma, mask, mask_bytes, (hipStream_t)stream));
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t tb = options().multi_interleave ? interleaved_bytes(ma, mask_bytes) : 0;
+    if (tb && keys->n >= 65536) {
+        void *ws = nullptr;
+        if ((rc = cached_workspace(s, tb, &ws))) return rc;
+        HIP_OR_FAIL(launch_probe_interleaved(key_batch(keys), ma, mask, mask_bytes, ws, s));
+        return SEB_OK;
+    }
+    HIP_OR_FAIL(launch_probe_multi(key_batch(keys), ma, mask, mask_bytes, s));
     return SEB_OK;
 }
 

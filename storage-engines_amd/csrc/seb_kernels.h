@@ -48,6 +48,7 @@ struct ManyArg {
 // Process-wide tuning knobs (seb_set_option).
 struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed)
+    int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
     int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)
     int probe_kpt = 2;            // k == 7 probes: keys per thread (1, 2, 4)
     int probe_slice_shift = 19;   // k == 7, m < 2^32: sliced probe with 2^shift-word (2 MiB) slices (0 = off)
@@ -67,6 +68,11 @@ int choose_build_algo(uint64_t n, uint64_t m, uint32_t k);
 hipError_t launch_probe(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s);
 hipError_t launch_probe_multi(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes,
                               hipStream_t s);
+// Interleaved multi-filter probe (all filters share (m, k), k == 7, m < 2^32): scratch bytes
+// needed for the per-call table (0 = not applicable), and the launch (table in `ws`).
+uint64_t interleaved_bytes(const MultiArg &ma, uint32_t mask_bytes);
+hipError_t launch_probe_interleaved(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes, void *ws,
+                                    hipStream_t s);
 hipError_t launch_build_many_lds(const KeyBatch &kb, const ManyArg &ma, uint32_t lds_bytes, hipStream_t s);
 
 }  // namespace seb

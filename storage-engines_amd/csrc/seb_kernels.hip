@@ -166,6 +166,63 @@ __global__ __launch_bounds__(256) void k_probe_multi(Src src, uint64_t n, MultiA
     }
 }
 
+// Interleaved multi-filter table: entry p (one MaskT per bit position p < m) holds bit p of every
+// filter, bit f = filter f.  Built per call from the filters' own word arrays (which stay the
+// canonical, Encode-able layout); valid when all filters share (m, k), as compaction outputs do.
+// One thread per 32 positions: nf coalesced word loads, 32 entries out.
+template <typename MaskT>
+__global__ __launch_bounds__(256) void k_interleave(MultiArg ma, uint64_t nwords, uint64_t m, MaskT *__restrict__ table) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwords) return;
+    MaskT e[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) e[j] = 0;
+    for (uint32_t f = 0; f < ma.nf; ++f) {
+        const uint32_t v = ma.f[f].words[w];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) e[j] |= (MaskT)((v >> j) & 1u) << f;
+    }
+    const uint64_t p0 = w * 32;
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+        if (p0 + j < m) table[p0 + j] = e[j];
+}
+
+// Probe against the interleaved table: 7 gathers of one MaskT per key, AND -> the mask of every
+// filter at once (bit f = MayContain of filter f).  Phase-sliced like k_probe_sliced so a table
+// larger than one XCD's L2 is walked one slice (2^slice_shift entries) at a time; a key whose
+// mask is already 0 stops gathering.
+template <typename Src, typename MaskT, int KPT>
+__global__ __launch_bounds__(256) void k_probe_interleaved(Src src, uint64_t n, const MaskT *__restrict__ table, ModArg md,
+                                                           MaskT *__restrict__ mask, uint32_t slice_shift,
+                                                           uint32_t nslices) {
+    const uint64_t span = (uint64_t)blockDim.x * KPT;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
+        uint32_t pos[KPT][7];
+        MaskT acc[KPT];
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            uint64_t h1 = 0, h2 = 0;
+            if (i < n) src.hash(i, h1, h2);
+            for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
+            acc[r] = i < n ? (MaskT)~(MaskT)0 : (MaskT)0;
+        }
+        for (uint32_t sl = 0; sl < nslices; ++sl) {
+#pragma unroll
+            for (int r = 0; r < KPT; ++r)
+#pragma unroll
+                for (int q = 0; q < 7; ++q)
+                    if (acc[r] && (pos[r][q] >> slice_shift) == sl) acc[r] &= table[pos[r][q]];
+        }
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            if (i < n) mask[i] = acc[r];
+        }
+    }
+}
+
 // Batched build of independent small filters: one workgroup per filter, the whole filter held
 // in LDS (ds_or_b32 atomics, no global atomics), then OR-merged into HBM with coalesced
 // accesses.  Filters too large for LDS go through k_build.
@@ -296,6 +353,45 @@ static hipError_t launch_multi_t(const Src &src, uint64_t n, const MultiArg &ma,
     hipLaunchKernelGGL((k_probe_multi<Src, MaskT, SAME, KFIX, M32>), dim3(g), dim3(256), 0, s, src, n, ma,
                        (MaskT *)mask);
     return hipGetLastError();
+}
+
+template <typename MaskT>
+static hipError_t interleaved_mask(const KeyBatch &kb, const MultiArg &ma, void *mask, void *ws, hipStream_t s) {
+    const ModArg &md = ma.f[0].md;
+    const uint64_t nwords = (md.m + 31) / 32;
+    MaskT *table = (MaskT *)ws;
+    // valid-bit mask: filters beyond nf must read 0, which the zero-initialised entries give
+    hipLaunchKernelGGL((k_interleave<MaskT>), dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, ma, nwords, md.m,
+                       table);
+    const uint64_t entries_per_slice_shift = 21 - (sizeof(MaskT) == 1 ? 0 : sizeof(MaskT) == 2 ? 1 : sizeof(MaskT) == 4 ? 2 : 3);
+    const uint32_t shift = (uint32_t)entries_per_slice_shift;  // 2 MiB of table per slice
+    const uint32_t nsl = (uint32_t)((md.m + (1ull << shift) - 1) >> shift);
+    return with_src(kb, [&](auto src) {
+        using S = decltype(src);
+        unsigned g = grid_for((kb.n + 1) / 2, 256, options().grid_cap);
+        hipLaunchKernelGGL((k_probe_interleaved<S, MaskT, 2>), dim3(g), dim3(256), 0, s, src, kb.n, (const MaskT *)table,
+                           md, (MaskT *)mask, shift, nsl);
+        return hipGetLastError();
+    });
+}
+
+uint64_t interleaved_bytes(const MultiArg &ma, uint32_t mask_bytes) {
+    if (ma.nf < 2) return 0;
+    for (uint32_t f = 1; f < ma.nf; ++f)
+        if (ma.f[f].md.m != ma.f[0].md.m || ma.f[f].md.k != ma.f[0].md.k) return 0;
+    if (ma.f[0].md.k != 7 || ma.f[0].md.m > 0xffffffffull) return 0;
+    return ((ma.f[0].md.m + 31) / 32) * 32 * mask_bytes;
+}
+
+hipError_t launch_probe_interleaved(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes, void *ws,
+                                    hipStream_t s) {
+    if (kb.n == 0) return hipSuccess;
+    switch (mask_bytes) {
+        case 1: return interleaved_mask<uint8_t>(kb, ma, mask, ws, s);
+        case 2: return interleaved_mask<uint16_t>(kb, ma, mask, ws, s);
+        case 4: return interleaved_mask<uint32_t>(kb, ma, mask, ws, s);
+        default: return interleaved_mask<uint64_t>(kb, ma, mask, ws, s);
+    }
 }
 
 template <typename MaskT>

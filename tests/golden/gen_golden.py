@@ -116,6 +116,31 @@ def multi_case(nf: int, per: int, nprobe: int, p: float) -> dict:
                 np.unpackbits(mask.astype("<u8").view(np.uint8)).sum())}
 
 
+def c5_case(nf: int = 64, per: int = 100_000, n: int = 10_000_000, p: float = 0.01) -> dict:
+    """BASELINE C5: 64 compaction-sized filters (filter f = key16(f*per + j)), one 10M-key batch;
+    q even -> key16((q/2 % nf)*per + (q/2)/nf) (in exactly filter q/2 % nf), q odd -> absent."""
+    m, k = oc.params(per, p)
+    q = np.arange(n, dtype=np.int64)
+    half = q // 2
+    pk = kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q))
+    mask = np.zeros(n, dtype=np.uint64)
+    fsha = []
+    for f in range(nf):
+        bits = oc.build(m, k, kg.key16(f * per + np.arange(per)), per, stride=16, threads=8)
+        fsha.append(sha(bn.encode(bits, m, k)))
+        mask |= oc.probe(bits, m, k, pk, n, stride=16, threads=8).astype(np.uint64) << np.uint64(f)
+    owner = half % nf
+    assert np.all(((mask[0::2] >> owner[0::2].astype(np.uint64)) & np.uint64(1)) == 1)
+    return {"filters": nf, "keys_per_filter": per, "probes": n, "p": p, "m": m, "k": k,
+            "rule": "filter f = key16(f*100000 + j); probe q even -> key16((q/2 % 64)*100000 + (q/2)/64), "
+                    "q odd -> key16(6400000 + q)",
+            "filter0_sha256": fsha[0], "filter_sha256_sha256": sha("".join(fsha).encode()),
+            "mask_sha256": sha(mask.astype("<u8").tobytes()),
+            "mask_popcount": int(np.unpackbits(mask.astype("<u8").view(np.uint8)).sum()),
+            "plane8_sha256": [sha(((mask >> np.uint64(8 * g)) & np.uint64(0xFF)).astype(np.uint8).tobytes())
+                              for g in range(8)]}
+
+
 def main():
     out: dict = {"generator": "tests/golden/gen_golden.py", "key_format": "key16(i) = b'user%010d' % i + "
                  "bytes([i & 0xff, (i + 1) & 0xff]) (common/benchmark/keygen.go:89-109)",
@@ -164,6 +189,7 @@ def main():
     out["varlen"] = [varlen_case(n, 0.01, check_np=n <= 100000) for n in [1000, 100000, 1000000]]
     print("varlen done", flush=True)
     out["multi"] = [multi_case(8, 10000, 160000, 0.01), multi_case(64, 2000, 256000, 0.01)]
+    out["c5"] = c5_case()
     with open(OUT, "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", OUT)

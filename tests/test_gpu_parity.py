@@ -414,6 +414,36 @@ def test_multi_filter_probe(seb, golden, torch_cuda, which):
     assert np.array_equal(mm.cpu().numpy(), ref.astype(np.uint8))
 
 
+@pytest.mark.parametrize("interleave", [0, 1])
+def test_multi_filter_interleaved_vs_direct(seb, golden, torch_cuda, interleave):
+    """The interleaved (bit-transposed) table path and the per-filter path give identical masks."""
+    torch = torch_cuda
+    row = golden["multi"][1]  # 64 filters x 2000 keys
+    nf, per, npr, m, k = row["filters"], row["keys_per_filter"], row["probes"], row["m"], row["k"]
+    keys = to_dev(torch, kg.key16(np.arange(nf * per)))
+    filters = [(seb.new_words(m), m, k) for _ in range(nf)]
+    seb.dev_build_many(seb.dev_keys(keys, n=nf * per, stride=16), [f * per for f in range(nf + 1)], filters)
+    q = np.arange(npr, dtype=np.int64)
+    half = q // 2
+    kd = seb.dev_keys(to_dev(torch, kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q))),
+                      n=npr, stride=16)
+    with seb.option("multi_interleave", interleave):
+        for dt, nsub in ((torch.int64, 64), (torch.int32, 32), (torch.int16, 16), (torch.uint8, 8)):
+            mask = torch.zeros(npr, dtype=dt, device="cuda")
+            seb.dev_probe_multi(kd, filters[:nsub], mask)
+            torch.cuda.synchronize()
+            got = mask.cpu().numpy().astype(np.int64).view(np.uint64) & np.uint64((1 << nsub) - 1 if nsub < 64 else
+                                                                                   0xFFFFFFFFFFFFFFFF)
+            if nsub == 64:
+                assert sha(got.astype("<u8").tobytes()) == row["mask_sha256"]
+            else:
+                bits = [seb.words_to_bits(w, m) for w, _, _ in filters[:nsub]]
+                ref = oc.probe_multi([(b, m, k) for b in bits], kg.key16(np.where(q % 2 == 0, (half % nf) * per +
+                                                                                   half // nf, nf * per + q)), npr,
+                                     stride=16)
+                assert np.array_equal(got, ref), nsub
+
+
 def test_multi_filter_host_api(seb, golden, ctx):
     row = golden["multi"][0]
     nf, per, npr, m, k = row["filters"], row["keys_per_filter"], row["probes"], row["m"], row["k"]
