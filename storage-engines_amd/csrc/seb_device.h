@@ -43,6 +43,7 @@ __device__ __forceinline__ void fnv_word_part(uint32_t w, uint32_t lo, uint32_t 
 // Key sources.  Each provides hash(i, h1, h2) for key i.
 struct Keys16 {  // fixed 16-B keys, 16-B aligned: one dwordx4 per lane, 1 KiB per wave, coalesced
     const uint4 *p;
+    __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
     __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
         uint4 v = p[i];
         h1 = kFnvOffset;
@@ -57,6 +58,7 @@ struct Keys16 {  // fixed 16-B keys, 16-B aligned: one dwordx4 per lane, 1 KiB p
 struct KeysStrideW {  // fixed stride, multiple of 4 bytes, 4-B aligned
     const uint32_t *p;
     uint32_t words;
+    __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
     __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
         const uint32_t *k = p + i * words;
         h1 = kFnvOffset;
@@ -68,6 +70,7 @@ struct KeysStrideW {  // fixed stride, multiple of 4 bytes, 4-B aligned
 struct KeysStrideB {  // any fixed stride (including 0)
     const uint8_t *p;
     uint32_t stride;
+    __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
     __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
         const uint8_t *k = p + i * stride;
         h1 = kFnvOffset;
@@ -76,27 +79,52 @@ struct KeysStrideB {  // any fixed stride (including 0)
     }
 };
 
+// Hash bytes [s, e) of a packed buffer: walk the aligned dwords that cover them.  A dword holding
+// at least one byte of the buffer never crosses a page, so the over-read at either end cannot fault.
+__device__ __forceinline__ void fnv_range(const uint8_t *p, uint64_t s, uint64_t e, uint64_t &h1, uint64_t &h2) {
+    h1 = kFnvOffset;
+    h2 = kFnvOffset;
+    uintptr_t a = ((uintptr_t)(p + s)) & ~(uintptr_t)3;
+    const uintptr_t end = (uintptr_t)(p + e);
+    const uintptr_t beg = (uintptr_t)(p + s);
+    for (; a < end; a += 4) {
+        const uint32_t w = *(const uint32_t *)a;
+        const uint32_t lo = beg > a ? (uint32_t)(beg - a) : 0u;
+        const uint32_t hi = end - a < 4 ? (uint32_t)(end - a) : 4u;
+        if (lo == 0 && hi == 4)
+            fnv_word(w, h1, h2);
+        else
+            fnv_word_part(w, lo, hi, h1, h2);
+    }
+}
+
 struct KeysVar {  // variable length: key i = p[off[i], off[i+1])
     const uint8_t *p;
     const uint64_t *off;
+    __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
     __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
-        uint64_t s = off[i], e = off[i + 1];
-        h1 = kFnvOffset;
-        h2 = kFnvOffset;
-        // Walk the aligned dwords that cover [s, e).  A dword holding at least one byte of
-        // the buffer never crosses a page, so the over-read at either end cannot fault.
-        uintptr_t a = ((uintptr_t)(p + s)) & ~(uintptr_t)3;
-        uintptr_t end = (uintptr_t)(p + e);
-        uintptr_t beg = (uintptr_t)(p + s);
-        for (; a < end; a += 4) {
-            uint32_t w = *(const uint32_t *)a;
-            uint32_t lo = beg > a ? (uint32_t)(beg - a) : 0u;
-            uint32_t hi = end - a < 4 ? (uint32_t)(end - a) : 4u;
-            if (lo == 0 && hi == 4)
-                fnv_word(w, h1, h2);
-            else
-                fnv_word_part(w, lo, hi, h1, h2);
-        }
+        fnv_range(p, off[i], off[i + 1], h1, h2);
+    }
+};
+
+struct KeysVarPerm {  // variable length, processed in length-bucketed order: i-th = key perm[i]
+    const uint8_t *p;
+    const uint64_t *off;
+    const uint32_t *perm;
+    __device__ __forceinline__ uint64_t index(uint64_t i) const { return perm[i]; }
+    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
+        const uint64_t j = perm[i];
+        fnv_range(p, off[j], off[j + 1], h1, h2);
+    }
+};
+
+struct KeysHashed {  // pre-hashed batch (k_hash_varlen): one coalesced 16-B load per key
+    const uint4 *h;
+    __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
+    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
+        const uint4 v = h[i];
+        h1 = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        h2 = (uint64_t)v.z | ((uint64_t)v.w << 32);
     }
 };
 
@@ -157,6 +185,8 @@ __device__ __forceinline__ void for_positions(uint64_t h1, uint64_t h2, const Mo
 // Dispatch on the key source.  Fixed 16-B aligned keys take the vector path.
 template <typename Fn>
 static inline hipError_t with_src(const KeyBatch &kb, Fn &&fn) {
+    if (kb.hashes) return fn(KeysHashed{kb.hashes});
+    if (kb.offsets && kb.perm) return fn(KeysVarPerm{kb.data, kb.offsets, kb.perm});
     if (kb.offsets) return fn(KeysVar{kb.data, kb.offsets});
     if (kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0) return fn(Keys16{(const uint4 *)kb.data});
     if (kb.stride % 4 == 0 && ((uintptr_t)kb.data & 3) == 0)

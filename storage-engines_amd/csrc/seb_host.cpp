@@ -100,6 +100,8 @@ static void load_env() {
     if (env_flag("SEB_PROBE_SPLIT", &v)) o.probe_split = (int)v;
     if (env_flag("SEB_PROBE_KPT", &v)) o.probe_kpt = (int)v;
     if (env_flag("SEB_MULTI_INTERLEAVE", &v)) o.multi_interleave = (int)v;
+    if (env_flag("SEB_VARLEN_SORT_MIN_KEYS", &v) && v >= 0) o.varlen_sort_min_keys = (uint64_t)v;
+    if (env_flag("SEB_VARLEN_PREHASH_MIN_KEYS", &v) && v >= 0) o.varlen_prehash_min_keys = (uint64_t)v;
     if (env_flag("SEB_PROBE_SLICE_SHIFT", &v)) o.probe_slice_shift = (int)v;
     if (env_flag("SEB_PROBE_SLICE_GRID", &v)) o.probe_slice_grid = (unsigned)v;
     if (env_flag("SEB_BUCKET_MIN_KEYS", &v) && v >= 0) o.bucket_min_keys = (uint64_t)v;
@@ -115,6 +117,8 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     else if (!strcmp(name, "probe_slice_shift") && value >= 0 && value <= 26) o.probe_slice_shift = (int)value;
     else if (!strcmp(name, "probe_slice_grid") && value >= 0) o.probe_slice_grid = (unsigned)value;
     else if (!strcmp(name, "multi_interleave") && (value == 0 || value == 1)) o.multi_interleave = (int)value;
+    else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
+    else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
     else if (!strcmp(name, "grid_cap") && value > 0 && value <= (1 << 30)) o.grid_cap = (unsigned)value;
     else if (!strcmp(name, "bucket_min_keys") && value >= 0) o.bucket_min_keys = (uint64_t)value;
     else return fail(SEB_ERR_INVALID, "seb_set_option: bad option %s=%lld", name, (long long)value);
@@ -131,6 +135,8 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "probe_slice_shift")) *value = o.probe_slice_shift;
     else if (!strcmp(name, "probe_slice_grid")) *value = o.probe_slice_grid;
     else if (!strcmp(name, "multi_interleave")) *value = o.multi_interleave;
+    else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
+    else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;
     else if (!strcmp(name, "grid_cap")) *value = o.grid_cap;
     else if (!strcmp(name, "bucket_min_keys")) *value = (int64_t)o.bucket_min_keys;
     else return fail(SEB_ERR_INVALID, "seb_get_option: unknown option %s", name);
@@ -202,30 +208,80 @@ static int cached_workspace(hipStream_t s, uint64_t bytes, void **out) {
     return SEB_OK;
 }
 
-// Build dispatcher: bucketed (LDS, no global atomics) or device-scope atomics.  `ws`/`ws_bytes`
-// may be null/0, in which case `grow` supplies scratch (or the atomic path runs).
+static bool want_prehash(const KeyBatch &kb) {
+    return kb.offsets && !kb.hashes && kb.n >= options().varlen_prehash_min_keys;
+}
+static bool want_len_perm(const KeyBatch &kb) {
+    return kb.offsets && !kb.perm && !want_prehash(kb) && kb.n >= options().varlen_sort_min_keys &&
+           kb.n <= 0xffffffffull;
+}
+static uint64_t prehash_bytes(const KeyBatch &kb) { return want_prehash(kb) ? ((kb.n * 16 + 255) & ~255ull) : 0; }
+
+// Build dispatcher: bucketed (LDS, no global atomics) or device-scope atomics; variable-length
+// batches are first put in length-bucketed order.  Scratch layout: [perm | bucketed].  `ws` /
+// `ws_bytes` may be null/0, in which case `grow` supplies scratch.
 template <typename Grow>
-static int build_dispatch(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s, void *ws,
-                          uint64_t ws_bytes, Grow &&grow) {
+static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStream_t s, void *ws, uint64_t ws_bytes,
+                          Grow &&grow) {
     if (kb.n == 0 || md.k == 0) return SEB_OK;
-    if (choose_build_algo(kb.n, md.m, md.k) == 2) {
-        const uint64_t need = bucketed_workspace_bytes(kb.n, md.m, md.k);
-        if (ws_bytes < need) {
-            int rc = grow(need, &ws);
-            if (rc) return rc;
-            ws_bytes = need;
-        }
-        HIP_OR_FAIL(launch_build_bucketed(kb, words, md, ws, ws_bytes, s));
+    const bool bucketed = choose_build_algo(kb.n, md.m, md.k) == 2;
+    const uint64_t pre_b = prehash_bytes(kb);
+    const uint64_t perm_b = want_len_perm(kb) ? len_perm_workspace_bytes(kb.n) : 0;
+    const uint64_t head = pre_b + perm_b;
+    const uint64_t need = head + (bucketed ? bucketed_workspace_bytes(kb.n, md.m, md.k) : 0);
+    if (need > ws_bytes) {
+        int rc = grow(need, &ws);
+        if (rc) return rc;
+        ws_bytes = need;
+    }
+    if (pre_b) {
+        HIP_OR_FAIL(launch_hash_varlen(kb, (uint4 *)ws, s));
+        kb.hashes = (const uint4 *)ws;
+    }
+    if (perm_b) HIP_OR_FAIL(launch_len_perm(kb, (uint8_t *)ws + pre_b, perm_b, s, &kb.perm));
+    if (bucketed) {
+        HIP_OR_FAIL(launch_build_bucketed(kb, words, md, (uint8_t *)ws + head, ws_bytes - head, s));
         return SEB_OK;
     }
     HIP_OR_FAIL(launch_build(kb, words, md, s));
     return SEB_OK;
 }
 
+// Variable-length probe batches: pre-hash (or length-bucketed order) into the per-(device,
+// stream) scratch cache first.  `extra` bytes at the front of the scratch are the caller's.
+static int prepare_probe_keys(KeyBatch &kb, hipStream_t s, uint64_t extra, void **ws_out) {
+    const uint64_t pre_b = prehash_bytes(kb);
+    const uint64_t perm_b = want_len_perm(kb) ? len_perm_workspace_bytes(kb.n) : 0;
+    *ws_out = nullptr;
+    if (extra + pre_b + perm_b == 0) return SEB_OK;
+    void *ws = nullptr;
+    int rc = cached_workspace(s, extra + pre_b + perm_b, &ws);
+    if (rc) return rc;
+    *ws_out = ws;
+    if (pre_b) {
+        HIP_OR_FAIL(launch_hash_varlen(kb, (uint4 *)((uint8_t *)ws + extra), s));
+        kb.hashes = (const uint4 *)((uint8_t *)ws + extra);
+    }
+    if (perm_b) HIP_OR_FAIL(launch_len_perm(kb, (uint8_t *)ws + extra + pre_b, perm_b, s, &kb.perm));
+    return SEB_OK;
+}
+
+static int probe_dispatch(KeyBatch kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s) {
+    void *ws;
+    int rc = prepare_probe_keys(kb, s, 0, &ws);
+    if (rc) return rc;
+    HIP_OR_FAIL(launch_probe(kb, words, md, out, s));
+    return SEB_OK;
+}
+
 extern "C" uint64_t seb_dev_build_workspace_size(uint64_t n, uint64_t m, uint32_t k) {
     std::call_once(g_env_once, load_env);
-    if (m == 0 || choose_build_algo(n, m, k) != 2) return 0;
-    return bucketed_workspace_bytes(n, m, k);
+    if (m == 0 || n == 0) return 0;
+    // conservative: assumes a variable-length batch (length-bucketed order) as well
+    const Options &o = options();
+    const uint64_t pre_b = n >= o.varlen_prehash_min_keys ? ((n * 16 + 255) & ~255ull) : 0;
+    const uint64_t perm_b = !pre_b && n >= o.varlen_sort_min_keys && n <= 0xffffffffull ? len_perm_workspace_bytes(n) : 0;
+    return pre_b + perm_b + (choose_build_algo(n, m, k) == 2 ? bucketed_workspace_bytes(n, m, k) : 0);
 }
 
 extern "C" int seb_dev_build_ws(const seb_keys *keys, uint32_t *words, uint64_t m, uint32_t k, void *ws,
@@ -257,8 +313,7 @@ extern "C" int seb_dev_probe(const seb_keys *keys, const uint32_t *words, uint64
     int rc;
     if ((rc = check_keys(keys, "seb_dev_probe")) || (rc = check_filter_args(m, k, "seb_dev_probe"))) return rc;
     if (!words || (!out && keys->n)) return fail(SEB_ERR_INVALID, "seb_dev_probe: null words/out");
-    HIP_OR_FAIL(launch_probe(key_batch(keys), words, mod_arg(m, k), out, (hipStream_t)stream));
-    return SEB_OK;
+    return probe_dispatch(key_batch(keys), words, mod_arg(m, k), out, (hipStream_t)stream);
 }
 
 static int fill_multi(const seb_filter_ref *filters, uint32_t nf, uint32_t mask_bytes, MultiArg *ma,
@@ -289,14 +344,15 @@ extern "C" int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *f
         return rc;
     if (!mask && keys->n) return fail(SEB_ERR_INVALID, "seb_dev_probe_multi: null mask");
     hipStream_t s = (hipStream_t)stream;
-    const uint64_t tb = options().multi_interleave ? interleaved_bytes(ma, mask_bytes) : 0;
-    if (tb && keys->n >= 65536) {
-        void *ws = nullptr;
-        if ((rc = cached_workspace(s, tb, &ws))) return rc;
-        HIP_OR_FAIL(launch_probe_interleaved(key_batch(keys), ma, mask, mask_bytes, ws, s));
+    KeyBatch kb = key_batch(keys);
+    const uint64_t tb = options().multi_interleave && keys->n >= 65536 ? interleaved_bytes(ma, mask_bytes) : 0;
+    void *ws = nullptr;
+    if ((rc = prepare_probe_keys(kb, s, (tb + 255) & ~255ull, &ws))) return rc;
+    if (tb) {
+        HIP_OR_FAIL(launch_probe_interleaved(kb, ma, mask, mask_bytes, ws, s));
         return SEB_OK;
     }
-    HIP_OR_FAIL(launch_probe_multi(key_batch(keys), ma, mask, mask_bytes, s));
+    HIP_OR_FAIL(launch_probe_multi(kb, ma, mask, mask_bytes, s));
     return SEB_OK;
 }
 
@@ -557,7 +613,7 @@ static int probe_device_to_host(seb_ctx *c, const seb_keys *kb, const uint32_t *
         const uint64_t cnt = dk.n;
         if ((rc = c->out[b].reserve(cnt))) return rc;
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));  // out[b] drained
-        HIP_OR_FAIL(launch_probe(dk, dwords, md, (uint8_t *)c->out[b].p, c->s_comp));
+        if ((rc = probe_dispatch(dk, dwords, md, (uint8_t *)c->out[b].p, c->s_comp))) return rc;
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
         HIP_OR_FAIL(hipMemcpyAsync(out + chunks[j].i0, c->out[b].p, cnt, hipMemcpyDeviceToHost, c->s_d2h));

@@ -19,6 +19,8 @@ struct KeyBatch {  // device pointers
     const uint64_t *offsets;  // n+1 or nullptr
     uint64_t n;
     uint32_t stride;
+    const uint32_t *perm = nullptr;  // variable-length only: processing order (length-bucketed)
+    const uint4 *hashes = nullptr;   // pre-hashed batch: (h1 lo, h1 hi, h2 lo, h2 hi) per key
 };
 
 constexpr int kMaxMulti = 64;
@@ -48,7 +50,9 @@ struct ManyArg {
 // Process-wide tuning knobs (seb_set_option).
 struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed)
-    int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
+    int multi_interleave = 1;
+    uint64_t varlen_sort_min_keys = INT64_MAX;  // length-bucketed order (measured slower; off by default)
+    uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys     // multi-filter probe: interleaved table when filters share (m, k)
     int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)
     int probe_kpt = 2;            // k == 7 probes: keys per thread (1, 2, 4)
     int probe_slice_shift = 19;   // k == 7, m < 2^32: sliced probe with 2^shift-word (2 MiB) slices (0 = off)
@@ -68,6 +72,14 @@ int choose_build_algo(uint64_t n, uint64_t m, uint32_t k);
 hipError_t launch_probe(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s);
 hipError_t launch_probe_multi(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes,
                               hipStream_t s);
+// Length-bucketed order for variable-length keys: perm[i] = the i-th key in order of
+// ceil(len/4) (capped at 64 dwords), so one wave hashes keys of one length.  Scratch bytes / launch.
+uint64_t len_perm_workspace_bytes(uint64_t n);
+hipError_t launch_len_perm(const KeyBatch &kb, void *ws, uint64_t ws_bytes, hipStream_t s, const uint32_t **perm_out);
+
+// Pre-hash a variable-length batch into one uint4 (h1, h2) per key (LDS-staged byte walk).
+hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s);
+
 // Interleaved multi-filter probe (all filters share (m, k), k == 7, m < 2^32): scratch bytes
 // needed for the per-call table (0 = not applicable), and the launch (table in `ws`).
 uint64_t interleaved_bytes(const MultiArg &ma, uint32_t mask_bytes);

@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_probe(Src src, uint64_t n, const uint32
 #pragma unroll
             for (int r = 0; r < KPT; ++r) {
                 const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
-                if (i < n) out[i] = (uint8_t)(acc[r] & 1u);
+                if (i < n) out[src.index(i)] = (uint8_t)(acc[r] & 1u);
             }
         }
     } else {
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void k_probe(Src src, uint64_t n, const uint32
             uint32_t acc = 1u;
             for_positions<0, M32>(h1, h2, md, md.k,
                                   [&](uint32_t, uint64_t p) { acc &= words[p >> 5] >> (uint32_t)(p & 31); });
-            out[i] = (uint8_t)(acc & 1u);
+            out[src.index(i)] = (uint8_t)(acc & 1u);
         }
     }
 }
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, const
 #pragma unroll
         for (int r = 0; r < KPT; ++r) {
             const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
-            if (i < n) out[i] = (uint8_t)(acc[r] & 1u);
+            if (i < n) out[src.index(i)] = (uint8_t)(acc[r] & 1u);
         }
     }
 }
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void k_probe_multi(Src src, uint64_t n, MultiA
                 w |= (MaskT)(acc & 1u) << f;
             }
         }
-        mask[i] = w;
+        mask[src.index(i)] = w;
     }
 }
 
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256) void k_probe_interleaved(Src src, uint64_t n, 
 #pragma unroll
         for (int r = 0; r < KPT; ++r) {
             const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
-            if (i < n) mask[i] = acc[r];
+            if (i < n) mask[src.index(i)] = acc[r];
         }
     }
 }

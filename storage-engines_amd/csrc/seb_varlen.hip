@@ -1,0 +1,191 @@
+// seb_varlen.hip — length-bucketed processing order for variable-length keys (BASELINE C4).
+//
+// The reference hashes each key with a byte-serial FNV chain (lsm/bloom.go:44-54), so a lane's
+// work is its key's length.  In a wave of 64 keys drawn from the C4 zipf lengths (8-256 B, mean
+// 40 B) almost every wave holds one long key, and the whole wave waits for it.  These kernels
+// build perm[] = the keys ordered by ceil(len/4) (a device counting sort over 65 length buckets),
+// so the build / probe kernels (KeysVarPerm) give each wave keys of one length.  Order never
+// changes a result: bits are OR-ed, and probe answers are written back to perm[i].
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "seb_device.h"
+#include "seb_kernels.h"
+
+namespace seb {
+
+constexpr uint32_t kLenBuckets = 65;  // ceil(len/4) in [0, 64]; longer keys share bucket 64
+constexpr uint32_t kPermThreads = 1024;
+constexpr uint32_t kPermTile = 8192;  // keys per workgroup
+
+__device__ __forceinline__ uint32_t len_bucket(const uint64_t *off, uint64_t i) {
+    const uint64_t d = (off[i + 1] - off[i] + 3) >> 2;
+    return d > 64 ? 64u : (uint32_t)d;
+}
+
+// per-(bucket, tile) counts, bucket-major: counts[b * ntiles + t]
+__global__ __launch_bounds__(kPermThreads) void k_len_hist(const uint64_t *__restrict__ off, uint64_t n,
+                                                           uint32_t ntiles, uint32_t *__restrict__ counts) {
+    __shared__ uint32_t hist[kLenBuckets];
+    if (threadIdx.x < kLenBuckets) hist[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint64_t k0 = (uint64_t)blockIdx.x * kPermTile;
+    const uint64_t k1 = k0 + kPermTile < n ? k0 + kPermTile : n;
+    for (uint64_t i = k0 + threadIdx.x; i < k1; i += blockDim.x) atomicAdd(&hist[len_bucket(off, i)], 1u);
+    __syncthreads();
+    if (threadIdx.x < kLenBuckets) counts[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = hist[threadIdx.x];
+}
+
+// exclusive scan of counts[0, len) in place, one workgroup: each thread owns a contiguous run
+__global__ __launch_bounds__(kPermThreads) void k_len_scan(uint32_t *__restrict__ counts, uint32_t len) {
+    __shared__ uint32_t wsum[kPermThreads / 64];
+    const uint32_t per = (len + blockDim.x - 1) / blockDim.x;
+    const uint32_t b0 = threadIdx.x * per;
+    uint32_t s = 0;
+    for (uint32_t j = 0; j < per; ++j)
+        if (b0 + j < len) s += counts[b0 + j];
+    // block exclusive scan of s
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t v = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v += y;
+    }
+    if (lane == 63) wsum[wid] = v;
+    __syncthreads();
+    if (wid == 0) {
+        uint32_t t = lane < nw ? wsum[lane] : 0u;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            uint32_t y = __shfl_up(t, d, 64);
+            if (lane >= (uint32_t)d) t += y;
+        }
+        if (lane < nw) wsum[lane] = t;
+    }
+    __syncthreads();
+    uint32_t run = (wid ? wsum[wid - 1] : 0u) + v - s;
+    for (uint32_t j = 0; j < per; ++j)
+        if (b0 + j < len) {
+            const uint32_t c = counts[b0 + j];
+            counts[b0 + j] = run;
+            run += c;
+        }
+}
+
+__global__ __launch_bounds__(kPermThreads) void k_len_scatter(const uint64_t *__restrict__ off, uint64_t n,
+                                                              uint32_t ntiles, const uint32_t *__restrict__ counts,
+                                                              uint32_t *__restrict__ perm) {
+    __shared__ uint32_t cur[kLenBuckets];
+    if (threadIdx.x < kLenBuckets) cur[threadIdx.x] = counts[(uint64_t)threadIdx.x * ntiles + blockIdx.x];
+    __syncthreads();
+    const uint64_t k0 = (uint64_t)blockIdx.x * kPermTile;
+    const uint64_t k1 = k0 + kPermTile < n ? k0 + kPermTile : n;
+    for (uint64_t i = k0 + threadIdx.x; i < k1; i += blockDim.x) perm[atomicAdd(&cur[len_bucket(off, i)], 1u)] = (uint32_t)i;
+}
+
+// ---- pre-hash: (h1, h2) of every variable-length key, written as one uint4 per key.
+// A workgroup owns kHashKeys consecutive keys.  It copies their byte span (16-B aligned chunks,
+// coalesced dwordx4 loads) into LDS, counting-sorts its keys by dword length in LDS, and lane t
+// then hashes the t-th shortest key from LDS: a wave's lanes walk keys of about one length
+// (divergence would otherwise make every wave as slow as its longest key), and each dependent
+// read is an LDS access instead of an L2/fabric round trip.  A span larger than the LDS window
+// is hashed straight from HBM in input order.  Build and probe then read 16 B per key
+// (KeysHashed), exactly like the fixed 16-B path.
+constexpr uint32_t kHashKeys = 512;
+constexpr uint32_t kHashLds = 40 * 1024;
+
+__global__ __launch_bounds__(kHashKeys) void k_hash_varlen(const uint8_t *__restrict__ data,
+                                                           const uint64_t *__restrict__ off, uint64_t n,
+                                                           uint4 *__restrict__ hashes) {
+    __shared__ uint4 stage[kHashLds / 16 + 1];  // +16 B: the funnel walk reads one dword past a key
+    __shared__ uint32_t cur[kLenBuckets];
+    __shared__ uint16_t order[kHashKeys];
+    const uint64_t k0 = (uint64_t)blockIdx.x * kHashKeys;
+    const uint64_t k1 = k0 + kHashKeys < n ? k0 + kHashKeys : n;
+    const uint32_t cnt = (uint32_t)(k1 - k0);
+    const uintptr_t s0 = (uintptr_t)(data + off[k0]);
+    const uintptr_t s1 = (uintptr_t)(data + off[k1]);
+    const uintptr_t base = s0 & ~(uintptr_t)15;
+    const uint64_t chunks = (s1 - base + 15) >> 4;
+    const bool staged = chunks * 16 <= kHashLds;  // block-uniform
+    uint64_t i = k0 + threadIdx.x;
+    if (staged) {
+        if (threadIdx.x < kLenBuckets) cur[threadIdx.x] = 0u;
+        for (uint64_t c = threadIdx.x; c < chunks; c += blockDim.x) stage[c] = ((const uint4 *)base)[c];
+        __syncthreads();
+        const uint32_t bk = threadIdx.x < cnt ? len_bucket(off, k0 + threadIdx.x) : 0u;
+        if (threadIdx.x < cnt) atomicAdd(&cur[bk], 1u);
+        __syncthreads();
+        if (threadIdx.x < 64) {  // exclusive scan of the 65 bucket counts by one wave
+            const uint32_t lane = threadIdx.x;
+            uint32_t c = cur[lane] + (lane == 63 ? cur[64] : 0u);
+            uint32_t v = c;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                uint32_t y = __shfl_up(v, d, 64);
+                if (lane >= (uint32_t)d) v += y;
+            }
+            const uint32_t last63 = cur[63];
+            cur[lane] = v - c;
+            if (lane == 63) cur[64] = v - c + last63;
+        }
+        __syncthreads();
+        if (threadIdx.x < cnt) order[atomicAdd(&cur[bk], 1u)] = (uint16_t)threadIdx.x;
+        __syncthreads();
+        if (threadIdx.x < cnt) i = k0 + order[threadIdx.x];
+    }
+    if (i >= k1) return;
+    uint64_t h1, h2;
+    const uint64_t s = off[i], e = off[i + 1];
+    if (staged) {
+        // Funnel walk: every 4 key bytes come from two aligned LDS dwords (v_alignbyte), so all
+        // full words take the same path whatever the key's alignment; the < 4-byte tail last.
+        const uint32_t *lds = (const uint32_t *)stage;
+        const uint32_t b = (uint32_t)((uintptr_t)(data + s) - base);
+        const uint32_t len = (uint32_t)(e - s);
+        const uint32_t sh = (b & 3u) * 8u;
+        uint32_t wi = b >> 2;
+        uint32_t cur = lds[wi];
+        h1 = kFnvOffset;
+        h2 = kFnvOffset;
+        for (uint32_t j = 0; j + 4 <= len; j += 4) {
+            const uint32_t nxt = lds[++wi];
+            fnv_word(__builtin_amdgcn_alignbyte(nxt, cur, sh >> 3), h1, h2);
+            cur = nxt;
+        }
+        const uint32_t r = len & 3u;
+        if (r) fnv_word_part(__builtin_amdgcn_alignbyte(lds[wi + 1], cur, sh >> 3), 0u, r, h1, h2);
+    } else {
+        fnv_range(data, s, e, h1, h2);
+    }
+    hashes[i] = make_uint4((uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32));
+}
+
+hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s) {
+    if (!kb.offsets || kb.n == 0) return hipSuccess;
+    const uint64_t blocks = (kb.n + kHashKeys - 1) / kHashKeys;
+    hipLaunchKernelGGL(k_hash_varlen, dim3((unsigned)blocks), dim3(kHashKeys), 0, s, kb.data, kb.offsets, kb.n, hashes);
+    return hipGetLastError();
+}
+
+uint64_t len_perm_workspace_bytes(uint64_t n) {
+    const uint64_t ntiles = (n + kPermTile - 1) / kPermTile;
+    return ((n * 4 + 255) & ~255ull) + ((kLenBuckets * ntiles * 4 + 255) & ~255ull);
+}
+
+hipError_t launch_len_perm(const KeyBatch &kb, void *ws, uint64_t ws_bytes, hipStream_t s, const uint32_t **perm_out) {
+    *perm_out = nullptr;
+    if (!kb.offsets || kb.n == 0) return hipSuccess;
+    if (kb.n > 0xffffffffull || ws_bytes < len_perm_workspace_bytes(kb.n)) return hipErrorInvalidValue;
+    const uint32_t ntiles = (uint32_t)((kb.n + kPermTile - 1) / kPermTile);
+    uint32_t *perm = (uint32_t *)ws;
+    uint32_t *counts = (uint32_t *)((uint8_t *)ws + ((kb.n * 4 + 255) & ~255ull));
+    hipLaunchKernelGGL(k_len_hist, dim3(ntiles), dim3(kPermThreads), 0, s, kb.offsets, kb.n, ntiles, counts);
+    hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(kPermThreads), 0, s, counts, kLenBuckets * ntiles);
+    hipLaunchKernelGGL(k_len_scatter, dim3(ntiles), dim3(kPermThreads), 0, s, kb.offsets, kb.n, ntiles, counts, perm);
+    *perm_out = perm;
+    return hipGetLastError();
+}
+
+}  // namespace seb

@@ -235,6 +235,35 @@ def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
     assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
+@pytest.mark.parametrize("mode", [(0, 1 << 40), (1 << 40, 0), (1 << 40, 1 << 40)],
+                         ids=["prehash", "length-bucketed", "direct"])
+def test_varlen_processing_order_invisible(seb, torch_cuda, mode, build_algo):
+    """The LDS-staged pre-hash, the length-bucketed processing order (perm) and the direct byte
+    walk give the same bit array and answers, including for empty keys and keys longer than
+    256 B (the last length bucket, and LDS spans that overflow the staging window)."""
+    prehash_min, sort_min = mode
+    torch = torch_cuda
+    rng = np.random.default_rng(5)
+    n = 70000
+    lens = rng.choice([0, 1, 3, 8, 15, 16, 17, 40, 64, 255, 256, 300, 1000], size=n)
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    data = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    m, k = oc.params(n, 0.01)
+    ref = oc.build(m, k, data, n, offsets=off)
+    with seb.option("varlen_sort_min_keys", sort_min), seb.option("varlen_prehash_min_keys", prehash_min):
+        kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
+        words, bits = dev_build_bits(seb, torch, kd, m, k)
+        assert np.array_equal(bits, ref)
+        pd = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+        pd[: int(off[n // 2])] = data[: int(off[n // 2])]  # first half present
+        pkd = seb.dev_keys(to_dev(torch, pd), to_dev(torch, off))
+        out = torch.empty(n, dtype=torch.uint8, device="cuda")
+        seb.dev_probe(pkd, words, m, k, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), oc.probe(ref, m, k, pd, n, offsets=off))
+
+
 def test_c4_varlen_10m_properties(seb, torch_cuda):
     """Full C4 size: no false negatives, and the bit array equals the oracle's."""
     torch = torch_cuda
