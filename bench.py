@@ -39,7 +39,7 @@ GOLDEN_C2 = "a86f3c69041ea0caac1dc559cfb36b06d5d5513d4ee203d22878715f612a0c3a"  
 GOLDEN_C3 = "aba77536fae51d566de525f519cd4c573799880d63000d88a2ce3052d0b90f95"  # sha256(answers)
 GOLDEN_C5 = "0668715db8804f529bc6795461a1cbd9905bbaab44b18b88a3b29881cd29f375"  # sha256(u64 masks)
 OPTIONS = ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "bucket_min_keys",
-           "multi_interleave", "varlen_prehash_min_keys", "varlen_sort_min_keys")
+           "multi_interleave", "varlen_prehash_min_keys", "varlen_sort_min_keys", "scatter_threads")
 
 
 def sha(b) -> str:

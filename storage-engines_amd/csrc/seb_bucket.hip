@@ -30,7 +30,7 @@ constexpr uint32_t kTileThreads = 1024;
 constexpr uint32_t kTilePos = 28672;                     // positions per tile sorted in LDS (112 KiB)
 constexpr uint32_t kKpt7 = 4;                            // keys per thread per round when k == 7
 constexpr uint32_t kMaxTiles = 1024;                     // super-tiles (workgroups) per launch
-constexpr uint32_t kTargetTiles = 256;                   // one 1024-thread workgroup per CU
+constexpr uint32_t kTargetTiles = 256;                   // workgroups per CU x 256 CUs
 
 // Exclusive scan of one value per thread over a block of kScanThreads / kTileThreads threads.
 // wsum: LDS scratch of (threads / 64) words.  Returns the prefix; *total = block sum.
@@ -66,15 +66,16 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *w
 // for hash-distributed keys: cap = mean + 8 sigma + 32) is OR-ed straight into the filter with
 // device-scope atomics instead, which k_bkt_apply's read-modify-write OR preserves.
 // LDS: sorted[kTilePos] u32 | cursor[nb] | fill[nb] | wsum[16]
-template <typename Src, int KFIX>
-__global__ __launch_bounds__(kTileThreads) void k_bkt_scatter(Src src, uint64_t n, ModArg md, uint32_t nb,
+template <typename Src, int KFIX, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, ModArg md, uint32_t nb,
                                                               uint32_t tile_keys, uint32_t ntiles, uint32_t cap,
                                                               uint16_t *__restrict__ regions,
                                                               uint32_t *__restrict__ counts,
                                                               uint32_t *__restrict__ words) {
     extern __shared__ uint32_t smem[];
+    constexpr uint32_t kPos = (uint32_t)THREADS * kKpt7 * 7;  // positions sorted per round
     uint32_t *sorted = smem;
-    uint32_t *cursor = smem + kTilePos;
+    uint32_t *cursor = smem + kPos;
     uint32_t *fill = cursor + nb;
     uint32_t *wsum = fill + nb;
     const uint32_t t = blockIdx.x;
@@ -83,10 +84,10 @@ __global__ __launch_bounds__(kTileThreads) void k_bkt_scatter(Src src, uint64_t 
         fill[b] = 0u;
     }
     __syncthreads();
-    const uint32_t round_keys = KFIX > 0 ? kKpt7 * kTileThreads : kTilePos / md.k;
+    const uint32_t round_keys = KFIX > 0 ? kKpt7 * THREADS : kPos / md.k;
     const uint64_t t0 = (uint64_t)t * tile_keys;
     const uint64_t t1 = t0 + tile_keys < n ? t0 + tile_keys : n;
-    const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;  // <= 4 buckets per thread in the scan
+    const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;  // <= 8 buckets per thread in the scan
 
     for (uint64_t k0 = t0; k0 < t1; k0 += round_keys) {
         const uint64_t k1 = k0 + round_keys < t1 ? k0 + round_keys : t1;
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(kTileThreads) void k_bkt_scatter(Src src, uint64_t 
         __syncthreads();
         {  // exclusive scan of this round's bucket counts
             const uint32_t b0 = threadIdx.x * per;
-            uint32_t c[4] = {0u, 0u, 0u, 0u}, s = 0;
+            uint32_t c[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, s = 0;
             for (uint32_t j = 0; j < per; ++j)
                 if (b0 + j < nb) {
                     c[j] = cursor[b0 + j];
@@ -150,13 +151,15 @@ __global__ __launch_bounds__(kTileThreads) void k_bkt_scatter(Src src, uint64_t 
             }
         }
         __syncthreads();
-        // cursor[b] is now the END of bucket b's run in `sorted`; its start is cursor[b-1].
+        // cursor[b] is now the END of bucket b's run in `sorted`, its start is cursor[b-1]: turn
+        // fill[b] into (fill - start) so an element's region slot is fill[b] + its sorted index.
+        for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) fill[b] -= b ? cursor[b - 1] : 0u;
+        __syncthreads();
         const uint32_t cnt = (uint32_t)(k1 - k0) * md.k;
         for (uint32_t idx = threadIdx.x; idx < cnt; idx += blockDim.x) {
             const uint32_t p = sorted[idx];
             const uint32_t b = p >> kBktShift;
-            const uint32_t start = b ? cursor[b - 1] : 0u;
-            const uint32_t slot = fill[b] + (idx - start);
+            const uint32_t slot = fill[b] + idx;
             if (slot < cap)
                 regions[((uint64_t)b * ntiles + t) * cap + slot] = (uint16_t)p;
             else
@@ -164,11 +167,9 @@ __global__ __launch_bounds__(kTileThreads) void k_bkt_scatter(Src src, uint64_t 
         }
         __syncthreads();
         for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
-            const uint32_t start = b ? cursor[b - 1] : 0u;
-            fill[b] += cursor[b] - start;
+            fill[b] += cursor[b];  // (fill - start) + end = fill + this round's count
+            cursor[b] = 0u;
         }
-        __syncthreads();
-        for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) cursor[b] = 0u;
         __syncthreads();
     }
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) counts[(uint64_t)b * ntiles + t] = min(fill[b], cap);
@@ -218,13 +219,18 @@ struct BktPlan {
     uint64_t off_regions, off_counts, bytes;
 };
 
+static uint32_t scatter_threads() { return options().scatter_threads == 512 ? 512u : 1024u; }
+
 static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k) {
     BktPlan p{};
     const uint64_t nwords = (m + 31) / 32;
     p.nb = (uint32_t)((nwords + kBktWords - 1) / kBktWords);
-    const uint32_t round_keys = k == 7 ? kKpt7 * kTileThreads : kTilePos / k;
+    const uint32_t thr = scatter_threads();
+    const uint32_t pos = thr * kKpt7 * 7;
+    const uint32_t round_keys = k == 7 ? kKpt7 * thr : pos / k;
+    const uint32_t target = kTargetTiles * (1024 / thr);
     uint64_t rounds_total = (n + round_keys - 1) / round_keys;
-    uint64_t rounds_per_tile = (rounds_total + kTargetTiles - 1) / kTargetTiles;
+    uint64_t rounds_per_tile = (rounds_total + target - 1) / target;
     if (rounds_per_tile < 1) rounds_per_tile = 1;
     p.tile_keys = (uint32_t)(rounds_per_tile * round_keys);
     p.ntiles = (uint32_t)((n + p.tile_keys - 1) / p.tile_keys);
@@ -273,13 +279,15 @@ hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModA
         uint16_t *regions = (uint16_t *)(w + p.off_regions);
         uint32_t *counts = (uint32_t *)(w + p.off_counts);
         const uint64_t nwords = (md.m + 31) / 32;
-        const size_t lds = (kTilePos + 2 * p.nb + 16) * sizeof(uint32_t);
+        const uint32_t thr = scatter_threads();
+        const size_t lds = ((size_t)thr * kKpt7 * 7 + 2 * p.nb + 16) * sizeof(uint32_t);
         hipError_t e = with_src(sub, [&](auto src) -> hipError_t {
             using S = decltype(src);
-            auto scat = md.k == 7 ? k_bkt_scatter<S, 7> : k_bkt_scatter<S, 0>;
+            auto scat = thr == 512 ? (md.k == 7 ? k_bkt_scatter<S, 7, 512> : k_bkt_scatter<S, 0, 512>)
+                                   : (md.k == 7 ? k_bkt_scatter<S, 7, 1024> : k_bkt_scatter<S, 0, 1024>);
             hipError_t a = hipFuncSetAttribute((const void *)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (a != hipSuccess) return a;
-            hipLaunchKernelGGL(scat, dim3(p.ntiles), dim3(kTileThreads), lds, s, src, sub.n, md, p.nb, p.tile_keys,
+            hipLaunchKernelGGL(scat, dim3(p.ntiles), dim3(thr), lds, s, src, sub.n, md, p.nb, p.tile_keys,
                                p.ntiles, p.cap, regions, counts, words);
             hipLaunchKernelGGL(k_bkt_apply, dim3(p.nb), dim3(256), 0, s, regions, counts, p.ntiles, p.cap, words, nwords);
             return hipGetLastError();

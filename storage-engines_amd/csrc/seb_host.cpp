@@ -100,6 +100,7 @@ static void load_env() {
     if (env_flag("SEB_PROBE_SPLIT", &v)) o.probe_split = (int)v;
     if (env_flag("SEB_PROBE_KPT", &v)) o.probe_kpt = (int)v;
     if (env_flag("SEB_MULTI_INTERLEAVE", &v)) o.multi_interleave = (int)v;
+    if (env_flag("SEB_SCATTER_THREADS", &v)) o.scatter_threads = (int)v;
     if (env_flag("SEB_VARLEN_SORT_MIN_KEYS", &v) && v >= 0) o.varlen_sort_min_keys = (uint64_t)v;
     if (env_flag("SEB_VARLEN_PREHASH_MIN_KEYS", &v) && v >= 0) o.varlen_prehash_min_keys = (uint64_t)v;
     if (env_flag("SEB_PROBE_SLICE_SHIFT", &v)) o.probe_slice_shift = (int)v;
@@ -117,6 +118,7 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     else if (!strcmp(name, "probe_slice_shift") && value >= 0 && value <= 26) o.probe_slice_shift = (int)value;
     else if (!strcmp(name, "probe_slice_grid") && value >= 0) o.probe_slice_grid = (unsigned)value;
     else if (!strcmp(name, "multi_interleave") && (value == 0 || value == 1)) o.multi_interleave = (int)value;
+    else if (!strcmp(name, "scatter_threads") && (value == 512 || value == 1024)) o.scatter_threads = (int)value;
     else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
     else if (!strcmp(name, "grid_cap") && value > 0 && value <= (1 << 30)) o.grid_cap = (unsigned)value;
@@ -135,6 +137,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "probe_slice_shift")) *value = o.probe_slice_shift;
     else if (!strcmp(name, "probe_slice_grid")) *value = o.probe_slice_grid;
     else if (!strcmp(name, "multi_interleave")) *value = o.multi_interleave;
+    else if (!strcmp(name, "scatter_threads")) *value = o.scatter_threads;
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;
     else if (!strcmp(name, "grid_cap")) *value = o.grid_cap;

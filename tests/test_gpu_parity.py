@@ -165,10 +165,10 @@ def test_host_api_chunked_pipeline(seb, monkeypatch, torch_cuda):
 
 # --------------------------------------------------------- device-resident API --------------
 
-@pytest.fixture(params=[1, 2], ids=["atomic", "bucketed"])
+@pytest.fixture(params=[(1, 1024), (2, 1024), (2, 512)], ids=["atomic", "bucketed", "bucketed512"])
 def build_algo(request, seb):
-    with seb.option("build_algo", request.param):
-        yield request.param
+    with seb.option("build_algo", request.param[0]), seb.option("scatter_threads", request.param[1]):
+        yield request.param[0]
 
 
 @pytest.fixture(params=[(0, 1, 0), (2, 2, 0), (3, 1, 0), (3, 2, 0), (3, 4, 0), (0, 4, 0), (3, 1, 12), (3, 2, 10),

@@ -28,8 +28,8 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STEP_KERNELS = {
-    "build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned"),
-    "probe": ("k_probe",),
+    "build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned", "k_hash_varlen"),
+    "probe": ("k_probe", "k_hash_varlen"),
 }
 
 
