@@ -39,7 +39,8 @@ GOLDEN_C2 = "a86f3c69041ea0caac1dc559cfb36b06d5d5513d4ee203d22878715f612a0c3a"  
 GOLDEN_C3 = "aba77536fae51d566de525f519cd4c573799880d63000d88a2ce3052d0b90f95"  # sha256(answers)
 GOLDEN_C5 = "0668715db8804f529bc6795461a1cbd9905bbaab44b18b88a3b29881cd29f375"  # sha256(u64 masks)
 OPTIONS = ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "bucket_min_keys",
-           "multi_interleave", "varlen_prehash_min_keys", "varlen_sort_min_keys", "scatter_threads")
+           "multi_interleave", "varlen_prehash_min_keys", "varlen_sort_min_keys", "scatter_threads",
+           "stream_nt", "probe_persistent", "scatter_kpt")
 
 
 def sha(b) -> str:
@@ -57,6 +58,8 @@ def parse():
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="c2c3/c4: build step j+1 (second filter buffer, own stream) while step j probes")
     for o in OPTIONS:
         ap.add_argument("--" + o.replace("_", "-"), type=int, default=None)
     return ap.parse_args()
@@ -89,7 +92,7 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
         st.pbufs[0].copy_(torch.from_numpy(st.probe_host))
         st.pbufs[1].copy_(st.pbufs[0])
     st.pk = [seb.dev_keys(b, n=n, stride=16) for b in st.pbufs]
-    st.words = seb.new_words(m, device=dev)
+    st.wbufs = [seb.new_words(m, device=dev) for _ in range(2 if args.overlap else 1)]
     st.out = torch.empty(n, dtype=torch.uint8, device=dev)
     nb = (m + 7) // 8
     st.kernel_bytes = {"build": 16.0 * n + 2 * nb, "probe": 16.0 * n + nb + n}
@@ -99,17 +102,18 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
                    "+ probe a 10M-key batch (50% present) RCCL-broadcast from rank 0")
     st.parallelism = f"filter-per-gpu x{world}, probe batch broadcast (RCCL)"
 
-    def build():
-        seb.dev_clear(st.words, m)
-        seb.dev_build(st.kb, st.words, m, k)
+    def build(j):
+        w = st.wbufs[j % len(st.wbufs)]
+        seb.dev_clear(w, m)
+        seb.dev_build(st.kb, w, m, k)
 
     def probe(j):
-        seb.dev_probe(st.pk[j % 2], st.words, m, k, st.out)
+        seb.dev_probe(st.pk[j % 2], st.wbufs[j % len(st.wbufs)], m, k, st.out)
 
-    def parity():
+    def parity(j):
         if n != 10_000_000 or rank != 0:
             return None
-        bits = seb.words_to_bits(st.words, m)
+        bits = seb.words_to_bits(st.wbufs[j % len(st.wbufs)], m)
         ok_b = sha(m.to_bytes(8, "little") + k.to_bytes(4, "little") + bits.tobytes()) == GOLDEN_C2
         ok_p = sha(st.out.cpu().numpy().tobytes()) == GOLDEN_C3
         return ("bit-exact (sha256 of Encode() and of the 10M answers match tests/golden)" if ok_b and ok_p
@@ -129,7 +133,7 @@ def setup_c4(args, seb, kg, torch, dev, rank, world, dist):
     pd, po = kg.varlen_keys(kg.probe_indices(n))
     pk = seb.dev_keys(torch.from_numpy(pd).to(dev), torch.from_numpy(po.view(np.int64)).to(dev))
     st.pk = [pk, pk]
-    st.words = seb.new_words(m, device=dev)
+    st.wbufs = [seb.new_words(m, device=dev) for _ in range(2 if args.overlap else 1)]
     st.out = torch.empty(n, dtype=torch.uint8, device=dev)
     nb = (m + 7) // 8
     st.kernel_bytes = {"build": float(bo[-1]) + 8.0 * (n + 1) + 2 * nb,
@@ -139,11 +143,12 @@ def setup_c4(args, seb, kg, torch, dev, rank, world, dist):
                    f"({bo[-1] / 1e6:.1f} MB of build keys)")
     st.parallelism = f"filter-per-gpu x{world}"
 
-    def build():
-        seb.dev_clear(st.words, m)
-        seb.dev_build(st.kb, st.words, m, k)
+    def build(j):
+        w = st.wbufs[j % len(st.wbufs)]
+        seb.dev_clear(w, m)
+        seb.dev_build(st.kb, w, m, k)
 
-    def parity():
+    def parity(j):
         if rank != 0:
             return None
         ok = bool(st.out.cpu().numpy()[0::2].all())  # every even probe is a built key
@@ -151,7 +156,7 @@ def setup_c4(args, seb, kg, torch, dev, rank, world, dist):
             else "MISMATCH: false negative"
 
     st.build = build
-    st.probe = lambda j: seb.dev_probe(st.pk[j % 2], st.words, m, k, st.out)
+    st.probe = lambda j: seb.dev_probe(st.pk[j % 2], st.wbufs[j % len(st.wbufs)], m, k, st.out)
     st.parity = parity
     return st
 
@@ -194,7 +199,7 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
         if world > 1:
             dist.all_gather(st.planes, st.plane)
 
-    def parity():
+    def parity(j):
         if n != 10_000_000 or rank != 0:
             return None
         mask = dp.assemble_mask(st.planes if world > 1 else [st.plane], nf)
@@ -236,7 +241,11 @@ def main():
     setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5}[args.config]
     st = setup(args, seb, kg, torch, dev, rank, world, dist)
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
+    overlap = bool(args.overlap) and st.build is not None
+    sp = torch.cuda.current_stream()                          # probe (and broadcast) stream
+    sb = torch.cuda.Stream(device=dev) if overlap else sp     # build stream
+    built = [torch.cuda.Event() for _ in range(2)]
+    probed = [torch.cuda.Event() for _ in range(2)]
     times = {"build": [], "probe": []}
 
     def broadcast(j):
@@ -248,28 +257,35 @@ def main():
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
         nxt = broadcast(j + 1)  # the next batch rides xGMI while this step computes
         if st.build is not None:
-            if record:
-                ev[0].record(stream)
-            st.build()
-            if record:
-                ev[1].record(stream)
+            with torch.cuda.stream(sb):
+                if overlap:
+                    sb.wait_event(probed[j % 2])  # probe j-2 is done with this filter buffer
+                if record:
+                    ev[0].record(sb)
+                st.build(j)
+                if record:
+                    ev[1].record(sb)
+                built[j % 2].record(sb)
+            if overlap:
+                sp.wait_event(built[j % 2])
         if pending is not None:
             pending.wait()
         if record:
-            ev[2].record(stream)
+            ev[2].record(sp)
         st.probe(j)
         if record:
-            ev[3].record(stream)
+            ev[3].record(sp)
             if st.build is not None:
                 times["build"].append((ev[0], ev[1]))
             times["probe"].append((ev[2], ev[3]))
+        probed[j % 2].record(sp)
         return nxt
 
     pending = broadcast(0)
     for j in range(args.warmup):
         pending = step(j, pending, False)
     torch.cuda.synchronize()
-    parity = st.parity()  # on the same run, after the warm-up steps
+    parity = st.parity(args.warmup - 1)  # on the same run, after the warm-up steps
 
     if world > 1:
         dist.barrier()
@@ -316,7 +332,7 @@ def main():
                          "other": {d: {"ms": round(v[0], 4), "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 2)}
                                    for d, v in kern.items()}},
             "parity": parity,
-            "options": {o: seb.get_option(o) for o in OPTIONS},
+            "options": {**{o: seb.get_option(o) for o in OPTIONS}, "overlap": int(overlap)},
         }
         if world == 1 and args.config == "c2c3" and not args.no_host_inclusive:
             result["host_inclusive"] = host_inclusive(seb, st.build_host, st.probe_host, st.m, st.k)

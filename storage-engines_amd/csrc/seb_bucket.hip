@@ -26,7 +26,6 @@ namespace seb {
 constexpr int kBktShift = 16;                            // 64 Ki bits per bucket
 constexpr uint32_t kBktWords = 1u << (kBktShift - 5);   // 2048 u32 words = 8 KiB of LDS
 constexpr uint32_t kMaxBuckets = 4096;                   // m <= 2^28 bits
-constexpr uint32_t kTileThreads = 1024;
 constexpr uint32_t kTilePos = 28672;                     // positions per tile sorted in LDS (112 KiB)
 constexpr uint32_t kKpt7 = 4;                            // keys per thread per round when k == 7
 constexpr uint32_t kMaxTiles = 1024;                     // super-tiles (workgroups) per launch
@@ -66,14 +65,14 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *w
 // for hash-distributed keys: cap = mean + 8 sigma + 32) is OR-ed straight into the filter with
 // device-scope atomics instead, which k_bkt_apply's read-modify-write OR preserves.
 // LDS: sorted[kTilePos] u32 | cursor[nb] | fill[nb] | wsum[16]
-template <typename Src, int KFIX, int THREADS>
+template <typename Src, int KFIX, int THREADS, int KPT7>
 __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, ModArg md, uint32_t nb,
                                                               uint32_t tile_keys, uint32_t ntiles, uint32_t cap,
                                                               uint16_t *__restrict__ regions,
                                                               uint32_t *__restrict__ counts,
                                                               uint32_t *__restrict__ words) {
     extern __shared__ uint32_t smem[];
-    constexpr uint32_t kPos = (uint32_t)THREADS * kKpt7 * 7;  // positions sorted per round
+    constexpr uint32_t kPos = (uint32_t)THREADS * KPT7 * 7;  // positions sorted per round
     uint32_t *sorted = smem;
     uint32_t *cursor = smem + kPos;
     uint32_t *fill = cursor + nb;
@@ -84,14 +83,14 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, Mo
         fill[b] = 0u;
     }
     __syncthreads();
-    const uint32_t round_keys = KFIX > 0 ? kKpt7 * THREADS : kPos / md.k;
+    const uint32_t round_keys = KFIX > 0 ? KPT7 * THREADS : kPos / md.k;
     const uint64_t t0 = (uint64_t)t * tile_keys;
     const uint64_t t1 = t0 + tile_keys < n ? t0 + tile_keys : n;
     const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;  // <= 8 buckets per thread in the scan
 
     for (uint64_t k0 = t0; k0 < t1; k0 += round_keys) {
         const uint64_t k1 = k0 + round_keys < t1 ? k0 + round_keys : t1;
-        constexpr int KP = KFIX > 0 ? (int)kKpt7 : 1;
+        constexpr int KP = KFIX > 0 ? KPT7 : 1;
         constexpr int KQ = KFIX > 0 ? KFIX : 1;
         uint32_t pos[KP][KQ];
         if constexpr (KFIX > 0) {  // positions stay in registers between counting and placing
@@ -220,14 +219,15 @@ struct BktPlan {
 };
 
 static uint32_t scatter_threads() { return options().scatter_threads == 512 ? 512u : 1024u; }
+static uint32_t scatter_kpt() { return options().scatter_kpt == 5 ? 5u : 4u; }
 
 static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k) {
     BktPlan p{};
     const uint64_t nwords = (m + 31) / 32;
     p.nb = (uint32_t)((nwords + kBktWords - 1) / kBktWords);
     const uint32_t thr = scatter_threads();
-    const uint32_t pos = thr * kKpt7 * 7;
-    const uint32_t round_keys = k == 7 ? kKpt7 * thr : pos / k;
+    const uint32_t pos = thr * scatter_kpt() * 7;
+    const uint32_t round_keys = k == 7 ? scatter_kpt() * thr : pos / k;
     const uint32_t target = kTargetTiles * (1024 / thr);
     uint64_t rounds_total = (n + round_keys - 1) / round_keys;
     uint64_t rounds_per_tile = (rounds_total + target - 1) / target;
@@ -280,11 +280,13 @@ hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModA
         uint32_t *counts = (uint32_t *)(w + p.off_counts);
         const uint64_t nwords = (md.m + 31) / 32;
         const uint32_t thr = scatter_threads();
-        const size_t lds = ((size_t)thr * kKpt7 * 7 + 2 * p.nb + 16) * sizeof(uint32_t);
+        const uint32_t kpt = scatter_kpt();
+        const size_t lds = ((size_t)thr * kpt * 7 + 2 * p.nb + 16) * sizeof(uint32_t);
         hipError_t e = with_src(sub, [&](auto src) -> hipError_t {
             using S = decltype(src);
-            auto scat = thr == 512 ? (md.k == 7 ? k_bkt_scatter<S, 7, 512> : k_bkt_scatter<S, 0, 512>)
-                                   : (md.k == 7 ? k_bkt_scatter<S, 7, 1024> : k_bkt_scatter<S, 0, 1024>);
+            auto scat = thr == 512 ? (md.k == 7 ? k_bkt_scatter<S, 7, 512, 4> : k_bkt_scatter<S, 0, 512, 4>)
+                        : kpt == 5 ? (md.k == 7 ? k_bkt_scatter<S, 7, 1024, 5> : k_bkt_scatter<S, 0, 1024, 5>)
+                                   : (md.k == 7 ? k_bkt_scatter<S, 7, 1024, 4> : k_bkt_scatter<S, 0, 1024, 4>);
             hipError_t a = hipFuncSetAttribute((const void *)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (a != hipSuccess) return a;
             hipLaunchKernelGGL(scat, dim3(p.ntiles), dim3(thr), lds, s, src, sub.n, md, p.nb, p.tile_keys,

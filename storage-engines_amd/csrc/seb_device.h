@@ -55,6 +55,21 @@ struct Keys16 {  // fixed 16-B keys, 16-B aligned: one dwordx4 per lane, 1 KiB p
     }
 };
 
+struct Keys16NT {  // Keys16 with non-temporal loads: the streamed batch does not evict filter lines from L2
+    const uint4 *p;
+    __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
+    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(p + i));
+        h1 = kFnvOffset;
+        h2 = kFnvOffset;
+        fnv_word(v.x, h1, h2);
+        fnv_word(v.y, h1, h2);
+        fnv_word(v.z, h1, h2);
+        fnv_word(v.w, h1, h2);
+    }
+};
+
 struct KeysStrideW {  // fixed stride, multiple of 4 bytes, 4-B aligned
     const uint32_t *p;
     uint32_t words;
@@ -188,7 +203,10 @@ static inline hipError_t with_src(const KeyBatch &kb, Fn &&fn) {
     if (kb.hashes) return fn(KeysHashed{kb.hashes});
     if (kb.offsets && kb.perm) return fn(KeysVarPerm{kb.data, kb.offsets, kb.perm});
     if (kb.offsets) return fn(KeysVar{kb.data, kb.offsets});
-    if (kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0) return fn(Keys16{(const uint4 *)kb.data});
+    if (kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0) {
+        if (options().stream_nt) return fn(Keys16NT{(const uint4 *)kb.data});
+        return fn(Keys16{(const uint4 *)kb.data});
+    }
     if (kb.stride % 4 == 0 && ((uintptr_t)kb.data & 3) == 0)
         return fn(KeysStrideW{(const uint32_t *)kb.data, kb.stride / 4});
     return fn(KeysStrideB{kb.data, kb.stride});

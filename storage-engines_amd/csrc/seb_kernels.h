@@ -58,7 +58,10 @@ struct Options {
     int probe_slice_shift = 19;   // k == 7, m < 2^32: sliced probe with 2^shift-word (2 MiB) slices (0 = off)
     unsigned probe_slice_grid = 0;  // workgroups of the sliced probe (0 = one thread per KPT keys)
     uint64_t bucket_min_keys = 1u << 18;  // auto: bucketed build from this many keys on
-    int scatter_threads = 1024;   // bucketed build: threads per scatter workgroup (512: two per CU)
+    int scatter_threads = 1024;
+    int scatter_kpt = 5;          // bucketed build, k == 7: keys per thread per round (4: 112 KiB LDS, 5: 140 KiB)
+    int stream_nt = 1;            // non-temporal loads for 16-B key batches (keeps filter lines in L2)
+    int probe_persistent = 0;     // sliced probe: persistent 1024-thread workgroups, barrier per slice (0 = off)   // bucketed build: threads per scatter workgroup (512: two per CU)
     unsigned grid_cap = 1u << 20;
 };
 Options &options();

@@ -132,6 +132,44 @@ __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, const
     }
 }
 
+// Persistent variant of the sliced probe: `gridDim.x` 1024-thread workgroups loop over batches of
+// 1024*KPT keys and finish each slice phase with a workgroup barrier, so all 16 waves of a CU's
+// workgroup gather from one slice at a time (workgroups on one XCD start together and do equal
+// work, which keeps them close to one slice).  Same answers as k_probe_sliced.
+template <typename Src, int KPT>
+__global__ __launch_bounds__(1024) void k_probe_sliced_pers(Src src, uint64_t n, const uint32_t *__restrict__ words,
+                                                            ModArg md, uint8_t *__restrict__ out, uint32_t slice_shift,
+                                                            uint32_t nslices) {
+    const uint64_t span = (uint64_t)blockDim.x * KPT;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
+        uint32_t pos[KPT][7];
+        uint32_t acc[KPT];
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            uint64_t h1 = 0, h2 = 0;
+            if (i < n) src.hash(i, h1, h2);
+            for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
+            acc[r] = i < n ? 1u : 0u;
+        }
+        for (uint32_t sl = 0; sl < nslices; ++sl) {
+#pragma unroll
+            for (int r = 0; r < KPT; ++r)
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    const uint32_t w = pos[r][q] >> 5;
+                    if ((acc[r] & 1u) && (w >> slice_shift) == sl) acc[r] &= words[w] >> (pos[r][q] & 31);
+                }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            if (i < n) out[src.index(i)] = (uint8_t)(acc[r] & 1u);
+        }
+    }
+}
+
 // Multi-filter probe: hash once, test every filter; bit f of the mask = filter f's answer.
 // SAME: all filters share (m, k) -> positions computed once per key.
 template <typename Src, typename MaskT, bool SAME, int KFIX, bool M32>
@@ -297,6 +335,12 @@ template <typename Src, int KPT>
 static hipError_t launch_sliced_t(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
                                   uint32_t shift, uint32_t nslices, hipStream_t s) {
     const Options &o = options();
+    if (o.probe_persistent > 0) {
+        unsigned g = grid_for((n + KPT - 1) / KPT, 1024, (unsigned)o.probe_persistent);
+        hipLaunchKernelGGL((k_probe_sliced_pers<Src, KPT>), dim3(g), dim3(1024), 0, s, src, n, words, md, out, shift,
+                           nslices);
+        return hipGetLastError();
+    }
     unsigned g = grid_for((n + KPT - 1) / KPT, 256, o.probe_slice_grid ? o.probe_slice_grid : o.grid_cap);
     hipLaunchKernelGGL((k_probe_sliced<Src, KPT>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift, nslices);
     return hipGetLastError();

@@ -165,17 +165,22 @@ def test_host_api_chunked_pipeline(seb, monkeypatch, torch_cuda):
 
 # --------------------------------------------------------- device-resident API --------------
 
-@pytest.fixture(params=[(1, 1024), (2, 1024), (2, 512)], ids=["atomic", "bucketed", "bucketed512"])
+@pytest.fixture(params=[(1, 1024, 4), (2, 1024, 4), (2, 512, 4), (2, 1024, 5)],
+                ids=["atomic", "bucketed", "bucketed512", "bucketed-kpt5"])
 def build_algo(request, seb):
-    with seb.option("build_algo", request.param[0]), seb.option("scatter_threads", request.param[1]):
+    with seb.option("build_algo", request.param[0]), seb.option("scatter_threads", request.param[1]), \
+            seb.option("scatter_kpt", request.param[2]):
         yield request.param[0]
 
 
-@pytest.fixture(params=[(0, 1, 0), (2, 2, 0), (3, 1, 0), (3, 2, 0), (3, 4, 0), (0, 4, 0), (3, 1, 12), (3, 2, 10),
-                        (3, 4, 13)], ids=lambda v: f"split{v[0]}-kpt{v[1]}-slice{v[2]}")
+@pytest.fixture(params=[(0, 1, 0, 0, 0), (2, 2, 0, 0, 0), (3, 1, 0, 0, 1), (3, 2, 0, 0, 0), (3, 4, 0, 0, 0),
+                        (0, 4, 0, 0, 0), (3, 1, 12, 0, 0), (3, 2, 10, 0, 1), (3, 4, 13, 0, 0), (3, 2, 12, 64, 0),
+                        (3, 1, 10, 7, 1)],
+                ids=lambda v: f"split{v[0]}-kpt{v[1]}-slice{v[2]}-pers{v[3]}-nt{v[4]}")
 def probe_split(request, seb):
-    with seb.option("probe_split", request.param[0]), seb.option("probe_kpt", request.param[1]), \
-            seb.option("probe_slice_shift", request.param[2]):
+    sp, kpt, sl, pers, nt = request.param
+    with seb.option("probe_split", sp), seb.option("probe_kpt", kpt), seb.option("probe_slice_shift", sl), \
+            seb.option("probe_persistent", pers), seb.option("stream_nt", nt):
         yield request.param
 
 
