@@ -165,6 +165,26 @@ uint32_t seb_filter_num_hashes(const seb_filter *f);
 uint64_t seb_filter_pending(seb_filter *f);
 int seb_filter_flush(seb_filter *f);
 
+/* ------------------ device-resident filter registry + batched LSM lookup ---- */
+/* One registry per LSM instance.  seb_registry_put decodes an SSTable's bloom block (the bytes
+ * OpenSSTable reads, lsm/sstable.go:121-129) straight into HBM, with the file's level and
+ * [MinKey, MaxKey]; level 0 keeps insertion order, levels 1..4 are ordered by MinKey, as
+ * lsm/levels.go:45-63 keeps them.  seb_registry_remove frees it (compaction, lsm/compaction.go).
+ * seb_registry_multiget: for each key, bit s of maybe[i] is set when registry slot s is a file
+ * LSM.Get would consult for the key (every L0 file; per level 1..4 the first file whose range
+ * covers it, lsm/lsm.go:168-198) AND its filter may contain the key.  At most 64 files. */
+typedef struct seb_registry seb_registry;
+seb_registry *seb_registry_new(int device);
+void seb_registry_free(seb_registry *reg);
+/* returns the slot (>= 0) or < 0 */
+int seb_registry_put(seb_registry *reg, uint64_t file_num, int level, const uint8_t *bloom, uint64_t bloom_len,
+                     const uint8_t *min_key, uint64_t min_len, const uint8_t *max_key, uint64_t max_len);
+int seb_registry_remove(seb_registry *reg, uint64_t file_num);
+/* file number and level of every slot (UINT64_MAX / -1 for free slots); returns the file count */
+int seb_registry_slots(seb_registry *reg, uint64_t *file_nums, int32_t *levels, uint32_t cap);
+int seb_registry_multiget(seb_registry *reg, const seb_keys *keys, uint64_t *maybe);          /* host keys */
+int seb_registry_multiget_dev(seb_registry *reg, const seb_keys *keys, uint64_t *maybe, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

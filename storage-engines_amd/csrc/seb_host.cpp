@@ -941,3 +941,208 @@ extern "C" int seb_filter_flush(seb_filter *f) {
     std::lock_guard<std::mutex> g(f->mu);
     return flush_locked(f);
 }
+
+// --------------------------------- device-resident filter registry + batched MultiGet --------
+// SURVEY.md §8(f) rows 1-2.  Each SSTable's bloom block (its Encode() bytes, read at
+// lsm/sstable.go:121-129) is decoded straight into HBM once; the level layout mirrors
+// lsm/levels.go: level 0 in insertion order (AddSSTable appends, :53), levels 1..4 sorted by
+// MinKey (:56-60; ties keep insertion order).  seb_registry_multiget answers, for a whole key
+// batch, which registered files LSM.Get would consult and which of their filters may contain the
+// key (lsm/lsm.go:168-198).
+
+struct RegEntry {
+    uint64_t file_num = 0, seq = 0;
+    int level = 0;
+    uint32_t slot = 0;
+    uint64_t m = 0;
+    uint32_t k = 0;
+    uint32_t *dwords = nullptr;
+    std::string min_key, max_key;
+};
+
+struct seb_registry {
+    std::mutex mu;
+    int device = 0;
+    std::vector<RegEntry> entries;
+    uint64_t seq = 0;
+    bool dirty = true;
+    DevBuf dslots, dranges;
+    uint32_t nslots = 0;
+    seb_ctx *ctx = nullptr;
+};
+
+extern "C" seb_registry *seb_registry_new(int device) {
+    seb_registry *r = new (std::nothrow) seb_registry();
+    if (!r) return nullptr;
+    r->device = device;
+    return r;
+}
+
+extern "C" void seb_registry_free(seb_registry *r) {
+    if (!r) return;
+    (void)hipSetDevice(r->device);
+    for (auto &e : r->entries) (void)hipFree(e.dwords);
+    r->dslots.release();
+    r->dranges.release();
+    if (r->ctx) seb_ctx_destroy(r->ctx);
+    delete r;
+}
+
+extern "C" int seb_registry_put(seb_registry *r, uint64_t file_num, int level, const uint8_t *bloom, uint64_t bloom_len,
+                                const uint8_t *min_key, uint64_t min_len, const uint8_t *max_key, uint64_t max_len) {
+    if (!r || !bloom || (!min_key && min_len) || (!max_key && max_len))
+        return fail(SEB_ERR_INVALID, "seb_registry_put: null argument");
+    if (level < 0 || level > 4) return fail(SEB_ERR_INVALID, "seb_registry_put: level %d outside 0..4", level);
+    if (bloom_len < 12) return fail(SEB_ERR_INVALID, "seb_registry_put: bloom block < 12 bytes (DecodeBloomFilter: nil)");
+    uint64_t m = 0;
+    uint32_t k = 0;
+    for (int b = 0; b < 8; ++b) m |= (uint64_t)bloom[b] << (8 * b);
+    for (int b = 0; b < 4; ++b) k |= (uint32_t)bloom[8 + b] << (8 * b);
+    int rc = check_filter_args(m, k, "seb_registry_put");
+    if (rc) return rc;
+    if (bloom_len - 12 < seb_num_bytes(m)) return fail(SEB_ERR_SHORT, "seb_registry_put: bits shorter than ceil(m/8)");
+    std::lock_guard<std::mutex> g(r->mu);
+    for (auto &e : r->entries)
+        if (e.file_num == file_num) return fail(SEB_ERR_INVALID, "seb_registry_put: file %llu already registered",
+                                                (unsigned long long)file_num);
+    if (r->entries.size() >= 64) return fail(SEB_ERR_INVALID, "seb_registry_put: registry holds at most 64 files");
+    uint64_t used = 0;
+    for (auto &e : r->entries) used |= 1ull << e.slot;
+    uint32_t slot = 0;
+    while (used >> slot & 1) ++slot;
+    HIP_OR_FAIL(hipSetDevice(r->device));
+    RegEntry e;
+    e.file_num = file_num;
+    e.seq = r->seq++;
+    e.level = level;
+    e.slot = slot;
+    e.m = m;
+    e.k = k;
+    e.min_key.assign((const char *)min_key, min_len);
+    e.max_key.assign((const char *)max_key, max_len);
+    const uint64_t wb = seb_words_bytes(m);
+    hipError_t a = hipMalloc((void **)&e.dwords, wb);
+    if (a != hipSuccess) return fail(SEB_ERR_NOMEM, "seb_registry_put: hipMalloc: %s", hipGetErrorString(a));
+    HIP_OR_FAIL(hipMemset(e.dwords, 0, wb));
+    HIP_OR_FAIL(hipMemcpy(e.dwords, bloom + 12, seb_num_bytes(m), hipMemcpyHostToDevice));
+    r->entries.push_back(std::move(e));
+    r->dirty = true;
+    return (int)slot;
+}
+
+extern "C" int seb_registry_remove(seb_registry *r, uint64_t file_num) {
+    if (!r) return fail(SEB_ERR_INVALID, "seb_registry_remove: null registry");
+    std::lock_guard<std::mutex> g(r->mu);
+    for (size_t i = 0; i < r->entries.size(); ++i)
+        if (r->entries[i].file_num == file_num) {
+            HIP_OR_FAIL(hipSetDevice(r->device));
+            HIP_OR_FAIL(hipDeviceSynchronize());  // no multiget may still read it
+            HIP_OR_FAIL(hipFree(r->entries[i].dwords));
+            r->entries.erase(r->entries.begin() + i);
+            r->dirty = true;
+            return SEB_OK;
+        }
+    return fail(SEB_ERR_INVALID, "seb_registry_remove: file %llu not registered", (unsigned long long)file_num);
+}
+
+// Lookup order: level 0 by insertion, then each level 1..4 by (MinKey, insertion).
+static std::vector<const RegEntry *> lookup_order(const seb_registry *r) {
+    std::vector<const RegEntry *> v;
+    for (auto &e : r->entries) v.push_back(&e);
+    std::stable_sort(v.begin(), v.end(), [](const RegEntry *a, const RegEntry *b) {
+        if (a->level != b->level) return a->level < b->level;
+        if (a->level > 0 && a->min_key != b->min_key) return a->min_key < b->min_key;
+        return a->seq < b->seq;
+    });
+    return v;
+}
+
+static int sync_registry_locked(seb_registry *r) {
+    if (!r->dirty) return SEB_OK;
+    HIP_OR_FAIL(hipSetDevice(r->device));
+    auto order = lookup_order(r);
+    std::vector<RegSlot> slots;
+    std::string ranges;
+    for (const RegEntry *e : order) {
+        RegSlot s{};
+        s.words = e->dwords;
+        s.md = mod_arg(e->m, e->k);
+        s.min_off = (uint32_t)ranges.size();
+        s.min_len = (uint32_t)e->min_key.size();
+        ranges += e->min_key;
+        s.max_off = (uint32_t)ranges.size();
+        s.max_len = (uint32_t)e->max_key.size();
+        ranges += e->max_key;
+        s.level = e->level;
+        s.slot = e->slot;
+        slots.push_back(s);
+    }
+    int rc;
+    if ((rc = r->dslots.reserve(sizeof(RegSlot) * (slots.size() + 1))) ||
+        (rc = r->dranges.reserve(ranges.size() + 16)))
+        return rc;
+    HIP_OR_FAIL(hipDeviceSynchronize());  // previous multigets may still read the tables
+    if (!slots.empty()) HIP_OR_FAIL(hipMemcpy(r->dslots.p, slots.data(), sizeof(RegSlot) * slots.size(), hipMemcpyHostToDevice));
+    if (!ranges.empty()) HIP_OR_FAIL(hipMemcpy(r->dranges.p, ranges.data(), ranges.size(), hipMemcpyHostToDevice));
+    r->nslots = (uint32_t)slots.size();
+    r->dirty = false;
+    return SEB_OK;
+}
+
+extern "C" int seb_registry_slots(seb_registry *r, uint64_t *file_nums, int32_t *levels, uint32_t cap) {
+    if (!r) return fail(SEB_ERR_INVALID, "seb_registry_slots: null registry");
+    std::lock_guard<std::mutex> g(r->mu);
+    for (uint32_t s = 0; s < cap; ++s) {
+        if (file_nums) file_nums[s] = UINT64_MAX;
+        if (levels) levels[s] = -1;
+    }
+    for (auto &e : r->entries)
+        if (e.slot < cap) {
+            if (file_nums) file_nums[e.slot] = e.file_num;
+            if (levels) levels[e.slot] = e.level;
+        }
+    return (int)r->entries.size();
+}
+
+extern "C" int seb_registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t *maybe, void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc;
+    if (!r) return fail(SEB_ERR_INVALID, "seb_registry_multiget: null registry");
+    if ((rc = check_keys(keys, "seb_registry_multiget"))) return rc;
+    if (!maybe && keys->n) return fail(SEB_ERR_INVALID, "seb_registry_multiget: null output");
+    std::lock_guard<std::mutex> g(r->mu);
+    if ((rc = sync_registry_locked(r))) return rc;
+    HIP_OR_FAIL(launch_multiget(key_batch(keys), (const RegSlot *)r->dslots.p, r->nslots, (const uint8_t *)r->dranges.p,
+                                maybe, (hipStream_t)stream));
+    return SEB_OK;
+}
+
+extern "C" int seb_registry_multiget(seb_registry *r, const seb_keys *kb, uint64_t *maybe) {
+    int rc;
+    if (!r) return fail(SEB_ERR_INVALID, "seb_registry_multiget: null registry");
+    if ((rc = check_keys(kb, "seb_registry_multiget")) || (rc = validate_offsets(kb, "seb_registry_multiget"))) return rc;
+    if (!maybe && kb->n) return fail(SEB_ERR_INVALID, "seb_registry_multiget: null output");
+    std::lock_guard<std::mutex> g(r->mu);
+    if ((rc = sync_registry_locked(r))) return rc;
+    if (!r->ctx && (rc = seb_ctx_create(r->device, &r->ctx))) return rc;
+    seb_ctx *c = r->ctx;
+    std::lock_guard<std::mutex> g2(c->mu);
+    HIP_OR_FAIL(hipSetDevice(c->device));
+    std::vector<Chunk> chunks;
+    plan_chunks(kb, c->chunk_bytes, chunks);
+    for (size_t j = 0; j < chunks.size(); ++j) {
+        const int b = (int)(j & 1);
+        KeyBatch dk{};
+        if ((rc = stage_chunk(c, kb, chunks[j], b, &dk))) return rc;
+        if ((rc = c->out[b].reserve(dk.n * 8))) return rc;
+        HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));
+        HIP_OR_FAIL(launch_multiget(dk, (const RegSlot *)r->dslots.p, r->nslots, (const uint8_t *)r->dranges.p,
+                                    (uint64_t *)c->out[b].p, c->s_comp));
+        HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
+        HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
+        HIP_OR_FAIL(hipMemcpyAsync(maybe + chunks[j].i0, c->out[b].p, dk.n * 8, hipMemcpyDeviceToHost, c->s_d2h));
+        HIP_OR_FAIL(hipEventRecord(c->ev_d2h[b], c->s_d2h));
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(c->s_d2h));
+    return SEB_OK;
+}

@@ -47,6 +47,17 @@ struct ManyArg {
     uint32_t pad;
 };
 
+// One registered SSTable filter, in LSM lookup order (k_multiget).
+struct RegSlot {
+    const uint32_t *words;
+    ModArg md;
+    uint32_t min_off, min_len, max_off, max_len;  // key range bytes in the registry's range buffer
+    int32_t level;
+    uint32_t slot;  // bit of the output mask
+};
+hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const uint8_t *ranges,
+                           uint64_t *maybe, hipStream_t s);
+
 // Process-wide tuning knobs (seb_set_option).
 struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed)

@@ -92,6 +92,13 @@ _SIGS = {
     "seb_filter_num_hashes": (_u32, [_vp]),
     "seb_filter_pending": (_u64, [_vp]),
     "seb_filter_flush": (_i, [_vp]),
+    "seb_registry_new": (_vp, [_i]),
+    "seb_registry_free": (None, [_vp]),
+    "seb_registry_put": (_i, [_vp, _u64, _i, _vp, _u64, _vp, _u64, _vp, _u64]),
+    "seb_registry_remove": (_i, [_vp, _u64]),
+    "seb_registry_slots": (_i, [_vp, C.POINTER(_u64), C.POINTER(C.c_int32), _u32]),
+    "seb_registry_multiget": (_i, [_vp, C.POINTER(seb_keys), _vp]),
+    "seb_registry_multiget_dev": (_i, [_vp, C.POINTER(seb_keys), _vp, _vp]),
 }
 
 
@@ -316,6 +323,48 @@ class BloomFilter:
         out = np.zeros(size, dtype=np.uint8)
         check(lib().seb_filter_encode(self._h, out.ctypes.data, size))
         return out.tobytes()
+
+
+# ------------------------------------------- filter registry + batched LSM lookup (§8f) ----
+
+class Registry:
+    """Device-resident SSTable filter registry (seb_registry): put the bloom block of each open
+    SSTable with its level and key range; multiget() returns, per key, a u64 mask of the slots
+    LSM.Get would consult whose filter may contain the key (lsm/lsm.go:168-198)."""
+
+    def __init__(self, device: int = 0):
+        self._h = lib().seb_registry_new(device)
+        if not self._h:
+            raise SebError(-3, "seb_registry_new failed")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().seb_registry_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def put(self, file_num: int, level: int, bloom_block: bytes, min_key: bytes, max_key: bytes) -> int:
+        return check(lib().seb_registry_put(self._h, file_num, level, bloom_block, len(bloom_block), min_key,
+                                            len(min_key), max_key, len(max_key)))
+
+    def remove(self, file_num: int) -> None:
+        check(lib().seb_registry_remove(self._h, file_num))
+
+    def slots(self) -> dict[int, tuple[int, int]]:
+        fn = (_u64 * 64)()
+        lv = (C.c_int32 * 64)()
+        check(lib().seb_registry_slots(self._h, fn, lv, 64))
+        return {s: (fn[s], lv[s]) for s in range(64) if lv[s] >= 0}
+
+    def multiget(self, keys) -> np.ndarray:
+        kb = as_keys(keys)
+        out = np.zeros(max(kb.n, 1), dtype=np.uint64)
+        check(lib().seb_registry_multiget(self._h, kb.ref, out.ctypes.data))
+        return out[: kb.n]
+
+    def multiget_dev(self, keys: "seb_keys", out, stream=None) -> None:
+        check(lib().seb_registry_multiget_dev(self._h, C.byref(keys), out.data_ptr(), _stream(stream)))
 
 
 # ------------------------------------------------- device-resident API (torch tensors) ----

@@ -38,7 +38,7 @@ def ctx(seb, torch_cuda):
 
 
 def to_dev(torch, arr):
-    return torch.from_numpy(np.ascontiguousarray(arr)).cuda()
+    return torch.from_numpy(np.array(arr, copy=True)).cuda()
 
 
 def dev_build_bits(seb, torch, keys_dev, m, k):
@@ -544,3 +544,82 @@ def test_c_harness_replays_sstable_sequence(seb, golden, n, expected):
     if row is not None and expected == n:
         assert res["encode_sha256"] == row["encode_sha256"]
         assert res["probe_sha256"] == row["probe_sha256"]
+
+
+# ------------------------------------------- registry + batched LSM lookup ----
+
+def _lsm_get_model(files, key: bytes):
+    """lsm/lsm.go:168-198 candidate walk over (slot, level, min, max, bits, m, k, seq) records:
+    every L0 file in insertion order, then per level 1..4 the first file (by MinKey) whose range
+    covers the key.  Returns the slots visited whose filter may contain the key."""
+    visited = []
+    l0 = sorted((f for f in files if f["level"] == 0), key=lambda f: f["seq"])
+    visited += l0
+    for lvl in range(1, 5):
+        for f in sorted((f for f in files if f["level"] == lvl), key=lambda f: (f["min"], f["seq"])):
+            if f["min"] <= key <= f["max"]:
+                visited.append(f)
+                break
+    mask = 0
+    for f in visited:
+        kb = np.frombuffer(key, np.uint8).reshape(1, -1) if key else np.zeros((1, 0), np.uint8)
+        if oc.probe(f["bits"], f["m"], f["k"], kb, 1, stride=len(key))[0]:
+            mask |= 1 << f["slot"]
+    return mask
+
+
+def test_registry_multiget_matches_lsm_get_walk(seb, torch_cuda):
+    torch = torch_cuda
+    rng = np.random.default_rng(17)
+    reg = seb.Registry(0)
+    files = []
+    seq = 0
+
+    def add(file_num, level, keys):
+        nonlocal seq
+        m, k = oc.params(max(len(keys), 1), 0.01)
+        arr = np.frombuffer(b"".join(keys), np.uint8)
+        lens = np.array([len(x) for x in keys], np.uint64)
+        off = np.zeros(len(keys) + 1, np.uint64)
+        np.cumsum(lens, out=off[1:])
+        bits = oc.build(m, k, arr, len(keys), offsets=off)
+        mn, mx = min(keys), max(keys)
+        slot = reg.put(file_num, level, bn.encode(bits, m, k), mn, mx)
+        files.append(dict(file=file_num, level=level, min=mn, max=mx, bits=bits, m=m, k=k, seq=seq, slot=slot))
+        seq += 1
+
+    universe = sorted({kg.key16_bytes(int(i)) for i in rng.integers(0, 200000, 30000)})
+    # L0: 3 overlapping flushes of random subsets
+    for f in range(3):
+        add(100 + f, 0, sorted(rng.choice(universe, 2000, replace=False).tolist()))
+    # L1..L3: non-overlapping contiguous ranges, added out of MinKey order
+    for lvl, parts in ((1, 4), (2, 6), (3, 3)):
+        chunks = np.array_split(np.array(universe, dtype=object), parts)
+        for j in rng.permutation(parts):
+            add(1000 * lvl + int(j), lvl, list(chunks[j]))
+    # probes: present keys, absent keys inside ranges, keys outside every range, varied lengths
+    probes = list(rng.choice(universe, 3000).tolist()) + [kg.key16_bytes(int(i)) for i in rng.integers(200000, 400000, 2000)]
+    probes += [b"", b"a", b"user", b"zzzz" * 10, universe[0], universe[-1], universe[0][:-1]]
+    got = reg.multiget(probes)
+    want = np.array([_lsm_get_model(files, p) for p in probes], dtype=np.uint64)
+    assert np.array_equal(got, want)
+    # device-resident form on fixed 16-B keys
+    fixed = [p for p in probes if len(p) == 16]
+    dk = seb.dev_keys(to_dev(torch, np.frombuffer(b"".join(fixed), np.uint8)), n=len(fixed), stride=16)
+    out = torch.zeros(len(fixed), dtype=torch.int64, device="cuda")
+    reg.multiget_dev(dk, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), np.array([_lsm_get_model(files, p) for p in fixed],
+                                                                      dtype=np.uint64))
+    # compaction removes L0 files; slots are reused
+    for f in [f for f in files if f["level"] == 0]:
+        reg.remove(f["file"])
+    files = [f for f in files if f["level"] != 0]
+    add(4000, 4, sorted(rng.choice(universe, 5000, replace=False).tolist()))
+    got = reg.multiget(probes)
+    assert np.array_equal(got, np.array([_lsm_get_model(files, p) for p in probes], dtype=np.uint64))
+    slots = reg.slots()
+    assert len(slots) == len(files) and {v[0] for v in slots.values()} == {f["file"] for f in files}
+    with pytest.raises(seb.SebError):
+        reg.remove(123456)
+    reg.close()
