@@ -38,6 +38,7 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s meas
 GOLDEN_C2 = "a86f3c69041ea0caac1dc559cfb36b06d5d5513d4ee203d22878715f612a0c3a"  # sha256(Encode()) n=10M
 GOLDEN_C3 = "aba77536fae51d566de525f519cd4c573799880d63000d88a2ce3052d0b90f95"  # sha256(answers)
 GOLDEN_C5 = "0668715db8804f529bc6795461a1cbd9905bbaab44b18b88a3b29881cd29f375"  # sha256(u64 masks)
+GOLDEN_LSM = "caf8282a71e15e15141639089e86e2ae5adabdfc91f69ea47e28fe5d71a941f9"  # sha256(MultiGet masks)
 OPTIONS = ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "bucket_min_keys",
            "multi_interleave", "varlen_prehash_min_keys", "varlen_sort_min_keys", "scatter_threads",
            "stream_nt", "probe_persistent", "scatter_kpt")
@@ -52,7 +53,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "lsm"])
     ap.add_argument("--keys", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
@@ -210,6 +211,45 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
     return st
 
 
+def setup_lsm(args, seb, kg, torch, dev, rank, world, dist):
+    """a device-resident filter registry for a 3-level LSM (4 overlapping
+    L0 files of 250K keys, 8 L1 files of 1M, 16 L2 files of 500K; keygen.lsm_files) and one batched
+    MultiGet of 10M keys (half present) that resolves LSM.Get's file walk + bloom checks on the GPU."""
+    st = Setup()
+    lay = kg.LSM_LAYOUT
+    files = kg.lsm_files(lay)
+    st.reg = seb.Registry(dev.index)
+    for level, file_num, idx in files:
+        m, k = seb.params(len(idx), 0.01)
+        keys = torch.from_numpy(kg.key16(2 * idx)).to(dev)
+        w = seb.new_words(m, device=dev)
+        seb.dev_build(seb.dev_keys(keys, n=len(idx), stride=16), w, m, k)
+        bits = seb.words_to_bits(w, m)
+        block = m.to_bytes(8, "little") + k.to_bytes(4, "little") + bits.tobytes()
+        st.reg.put(file_num, level, block, kg.key16_bytes(int(2 * idx[0])), kg.key16_bytes(int(2 * idx[-1])))
+    n = lay["probes"]
+    st.m, st.k, st.n = 0, 7, n
+    pk = torch.from_numpy(kg.key16(kg.lsm_probe_indices(lay))).to(dev)
+    st.pk = seb.dev_keys(pk, n=n, stride=16)
+    st.mask = torch.zeros(n, dtype=torch.int64, device=dev)
+    filt_bytes = sum((seb.params(len(i), 0.01)[0] + 7) // 8 for _, _, i in files)
+    st.kernel_bytes = {"probe": 16.0 * n + filt_bytes + 8.0 * n}
+    st.units_per_step = float(n) * world
+    st.workload = ("LSM MultiGet (SURVEY 8(f)): registry of 28 SSTable filters (L0 4x250K overlapping, L1 8x1M, "
+                   "L2 16x500K keys); one 10M-key batch resolved per LSM.Get's file walk + bloom checks")
+    st.parallelism = f"registry-per-gpu x{world}"
+    st.probe = lambda j: st.reg.multiget_dev(st.pk, st.mask)
+
+    def parity(j):
+        if rank != 0:
+            return None
+        ok = sha(st.mask.cpu().numpy().view(np.uint64).astype("<u8").tobytes()) == GOLDEN_LSM
+        return "bit-exact (sha256 of the 10M MultiGet masks matches tests/golden lsm)" if ok else "MISMATCH masks"
+
+    st.parity = parity
+    return st
+
+
 def main():
     args = parse()
     import torch
@@ -238,7 +278,7 @@ def main():
         if v is not None:
             seb.set_option(o, v)
 
-    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5}[args.config]
+    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "lsm": setup_lsm}[args.config]
     st = setup(args, seb, kg, torch, dev, rank, world, dist)
     torch.cuda.synchronize()
     overlap = bool(args.overlap) and st.build is not None
@@ -336,7 +376,7 @@ def main():
         }
         if world == 1 and args.config == "c2c3" and not args.no_host_inclusive:
             result["host_inclusive"] = host_inclusive(seb, st.build_host, st.probe_host, st.m, st.k)
-        if world == 1 and not args.no_cpu_baseline and args.config != "c5":
+        if world == 1 and not args.no_cpu_baseline and args.config in ("c2c3", "c4"):
             result["cpu_baseline"] = cpu_baseline(args, st.n, st.m, st.k)
     if world > 1:
         dist.barrier()

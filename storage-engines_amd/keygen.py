@@ -104,3 +104,34 @@ def varlen_keys(idx: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
             ok = nb > b
             data[base[ok] + b] = wb[ok, b]
     return data, offsets
+
+
+# ---- synthetic LSM layout for the registry / MultiGet config (bench.py --config lsm)
+LSM_LAYOUT = {"l0_files": 4, "l0_keys": 250_000, "l1_files": 8, "l1_keys": 1_000_000, "l2_files": 16,
+              "l2_keys": 500_000, "probes": 10_000_000, "seed": 12345}
+
+
+def lsm_files(lay=LSM_LAYOUT):
+    """Synthetic LSM for the registry/MultiGet config: keys key16(2i).  L1 file j holds
+    i in [j*1M, (j+1)*1M), L2 file j holds i in [j*500K, (j+1)*500K) (non-overlapping, ranges in
+    key order), L0 file f holds 250K random i (overlapping).  Returns [(level, file_num, i_array)]
+    in registration order (L2 files registered in reverse to exercise the MinKey sort)."""
+    rng = np.random.default_rng(lay["seed"])
+    span = lay["l1_files"] * lay["l1_keys"]
+    files = []
+    for j in reversed(range(lay["l2_files"])):
+        files.append((2, 2000 + j, np.arange(j * lay["l2_keys"], (j + 1) * lay["l2_keys"])))
+    for j in range(lay["l1_files"]):
+        files.append((1, 1000 + j, np.arange(j * lay["l1_keys"], (j + 1) * lay["l1_keys"])))
+    for f in range(lay["l0_files"]):
+        files.append((0, 100 + f, np.sort(rng.choice(span, lay["l0_keys"], replace=False))))
+    return files
+
+
+def lsm_probe_indices(lay=LSM_LAYOUT):
+    """q even -> key16(2r) (present in L1, L2 and maybe L0), q odd -> key16(2r+1) (absent, inside
+    the level ranges), r uniform in the key span."""
+    rng = np.random.default_rng(lay["seed"] + 1)
+    n = lay["probes"]
+    r = rng.integers(0, lay["l1_files"] * lay["l1_keys"], n)
+    return np.where(np.arange(n) % 2 == 0, 2 * r, 2 * r + 1)

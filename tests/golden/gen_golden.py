@@ -141,6 +141,29 @@ def c5_case(nf: int = 64, per: int = 100_000, n: int = 10_000_000, p: float = 0.
                               for g in range(8)]}
 
 
+def lsm_case(lay=kg.LSM_LAYOUT) -> dict:
+    files = kg.lsm_files(lay)
+    pidx = kg.lsm_probe_indices(lay)
+    pk = kg.key16(pidx)
+    n = pk.shape[0]
+    mask = np.zeros(n, dtype=np.uint64)
+    slot = 0
+    for level, _fn, idx in files:  # registration order = slot order (slots 0..27)
+        m, k = oc.params(len(idx), 0.01)
+        bits = oc.build(m, k, kg.key16(2 * idx), len(idx), stride=16, threads=8)
+        if level == 0:
+            cand = np.ones(n, dtype=bool)
+        else:  # the one file per level whose [min, max] covers the key (lsm/lsm.go:184-196)
+            lo, hi = 2 * idx[0], 2 * idx[-1]
+            cand = (pidx >= lo) & (pidx <= hi)
+        sel = np.nonzero(cand)[0]
+        ans = oc.probe(bits, m, k, pk[sel], len(sel), stride=16, threads=8)
+        mask[sel] |= ans.astype(np.uint64) << np.uint64(slot)
+        slot += 1
+    return {"layout": lay, "files": len(files), "mask_sha256": sha(mask.astype("<u8").tobytes()),
+            "mask_popcount": int(np.unpackbits(mask.astype("<u8").view(np.uint8)).sum())}
+
+
 def main():
     out: dict = {"generator": "tests/golden/gen_golden.py", "key_format": "key16(i) = b'user%010d' % i + "
                  "bytes([i & 0xff, (i + 1) & 0xff]) (common/benchmark/keygen.go:89-109)",
@@ -190,6 +213,7 @@ def main():
     print("varlen done", flush=True)
     out["multi"] = [multi_case(8, 10000, 160000, 0.01), multi_case(64, 2000, 256000, 0.01)]
     out["c5"] = c5_case()
+    out["lsm"] = lsm_case()
     with open(OUT, "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", OUT)
