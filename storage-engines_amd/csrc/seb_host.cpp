@@ -968,8 +968,20 @@ struct seb_registry {
     bool dirty = true;
     DevBuf dslots, dranges;
     uint32_t nslots = 0;
+    RegLayout layout{};
     seb_ctx *ctx = nullptr;
 };
+
+static void be_prefix(const std::string &s, uint64_t out[2]) {  // first 16 bytes, big-endian, zero padded
+    for (int w = 0; w < 2; ++w) {
+        uint64_t v = 0;
+        for (int i = 0; i < 8; ++i) {
+            const size_t at = (size_t)w * 8 + i;
+            v = (v << 8) | (at < s.size() ? (uint8_t)s[at] : 0u);
+        }
+        out[w] = v;
+    }
+}
 
 extern "C" seb_registry *seb_registry_new(int device) {
     seb_registry *r = new (std::nothrow) seb_registry();
@@ -1063,6 +1075,24 @@ static int sync_registry_locked(seb_registry *r) {
     auto order = lookup_order(r);
     std::vector<RegSlot> slots;
     std::string ranges;
+    RegLayout lay{};
+    lay.all_k7_m32 = 1;
+    for (int L = 0; L < 5; ++L) lay.lo[L] = lay.hi[L] = 0;
+    for (size_t i = 0; i < order.size(); ++i) {
+        const int L = order[i]->level;
+        if (i == 0 || order[i - 1]->level != L) lay.lo[L] = (uint32_t)i;
+        lay.hi[L] = (uint32_t)i + 1;
+        if (order[i]->k != 7 || order[i]->m > 0xffffffffull) lay.all_k7_m32 = 0;
+    }
+    for (int L = 0; L < 5; ++L)
+        if (lay.hi[L] == 0) lay.lo[L] = lay.hi[L] = (uint32_t)order.size();  // empty level
+    for (int L = 1; L < 5; ++L) {  // disjoint, MinKey-ordered level: bisection finds the first cover
+        bool ok = true;
+        for (uint32_t i = lay.lo[L]; i + 1 < lay.hi[L]; ++i)
+            ok &= order[i]->min_key <= order[i]->max_key && order[i]->max_key < order[i + 1]->min_key;
+        if (lay.hi[L] > lay.lo[L]) ok &= order[lay.hi[L] - 1]->min_key <= order[lay.hi[L] - 1]->max_key;
+        if (ok) lay.nonoverlap |= 1u << L;
+    }
     for (const RegEntry *e : order) {
         RegSlot s{};
         s.words = e->dwords;
@@ -1075,6 +1105,8 @@ static int sync_registry_locked(seb_registry *r) {
         ranges += e->max_key;
         s.level = e->level;
         s.slot = e->slot;
+        be_prefix(e->min_key, s.min_be);
+        be_prefix(e->max_key, s.max_be);
         slots.push_back(s);
     }
     int rc;
@@ -1085,6 +1117,7 @@ static int sync_registry_locked(seb_registry *r) {
     if (!slots.empty()) HIP_OR_FAIL(hipMemcpy(r->dslots.p, slots.data(), sizeof(RegSlot) * slots.size(), hipMemcpyHostToDevice));
     if (!ranges.empty()) HIP_OR_FAIL(hipMemcpy(r->dranges.p, ranges.data(), ranges.size(), hipMemcpyHostToDevice));
     r->nslots = (uint32_t)slots.size();
+    r->layout = lay;
     r->dirty = false;
     return SEB_OK;
 }
@@ -1112,8 +1145,8 @@ extern "C" int seb_registry_multiget_dev(seb_registry *r, const seb_keys *keys, 
     if (!maybe && keys->n) return fail(SEB_ERR_INVALID, "seb_registry_multiget: null output");
     std::lock_guard<std::mutex> g(r->mu);
     if ((rc = sync_registry_locked(r))) return rc;
-    HIP_OR_FAIL(launch_multiget(key_batch(keys), (const RegSlot *)r->dslots.p, r->nslots, (const uint8_t *)r->dranges.p,
-                                maybe, (hipStream_t)stream));
+    HIP_OR_FAIL(launch_multiget(key_batch(keys), (const RegSlot *)r->dslots.p, r->nslots, r->layout,
+                                (const uint8_t *)r->dranges.p, maybe, (hipStream_t)stream));
     return SEB_OK;
 }
 
@@ -1136,8 +1169,8 @@ extern "C" int seb_registry_multiget(seb_registry *r, const seb_keys *kb, uint64
         if ((rc = stage_chunk(c, kb, chunks[j], b, &dk))) return rc;
         if ((rc = c->out[b].reserve(dk.n * 8))) return rc;
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));
-        HIP_OR_FAIL(launch_multiget(dk, (const RegSlot *)r->dslots.p, r->nslots, (const uint8_t *)r->dranges.p,
-                                    (uint64_t *)c->out[b].p, c->s_comp));
+        HIP_OR_FAIL(launch_multiget(dk, (const RegSlot *)r->dslots.p, r->nslots, r->layout,
+                                    (const uint8_t *)r->dranges.p, (uint64_t *)c->out[b].p, c->s_comp));
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
         HIP_OR_FAIL(hipMemcpyAsync(maybe + chunks[j].i0, c->out[b].p, dk.n * 8, hipMemcpyDeviceToHost, c->s_d2h));

@@ -53,10 +53,17 @@ struct RegSlot {
     ModArg md;
     uint32_t min_off, min_len, max_off, max_len;  // key range bytes in the registry's range buffer
     int32_t level;
-    uint32_t slot;  // bit of the output mask
+    uint32_t slot;          // bit of the output mask
+    uint64_t min_be[2];     // first 16 bytes of MinKey / MaxKey as big-endian words (zero padded)
+    uint64_t max_be[2];
 };
-hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const uint8_t *ranges,
-                           uint64_t *maybe, hipStream_t s);
+struct RegLayout {          // slot index ranges per level (lookup order) + shape flags
+    uint32_t lo[5], hi[5];
+    uint32_t nonoverlap;    // bit L: level L's files are disjoint and in MinKey order (bisection exact)
+    uint32_t all_k7_m32;    // every filter has k == 7 and m < 2^32
+};
+hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
+                           const uint8_t *ranges, uint64_t *maybe, hipStream_t s);
 
 // Process-wide tuning knobs (seb_set_option).
 struct Options {

@@ -5,10 +5,12 @@
 //   level 0:    every file, in the level's order (they may overlap)           lsm/lsm.go:173-182
 //   level 1..4: the FIRST file whose [MinKey, MaxKey] covers the key, then stop lsm/lsm.go:184-196
 // and each visited file first asks its bloom filter (lsm/sstable.go:206).  k_multiget does that
-// for a whole key batch in one launch: per key it hashes once, walks the registry's slots in the
-// same order, compares the key bytewise against each L1+ file's range (Go string order), tests the
-// filter of every file Get would visit and sets bit s of the key's mask when slot s is visited AND
-// its filter may contain the key.  The caller reads SSTable blocks only for set bits, in slot order.
+// for a whole key batch in one launch: per key it hashes once, tests every L0 filter, and per
+// level 1..4 finds the covering file (bisection over the MinKey-ordered files when the registry
+// verified the level is disjoint, else the reference's linear scan), then tests that one filter.
+// Bit s of the key's mask = slot s is visited AND its filter may contain the key.  Key ranges are
+// compared in Go string order: bytewise, a proper prefix first; the first 16 bytes come from LDS
+// as big-endian words, longer ties fall back to the bytes in HBM.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -17,18 +19,43 @@
 
 namespace seb {
 
-// Go's string comparison: bytewise, a proper prefix sorts first.  Returns <0, 0, >0.
-__device__ __forceinline__ int key_cmp(const uint8_t *a, uint32_t alen, const uint8_t *b, uint32_t blen) {
-    const uint32_t n = alen < blen ? alen : blen;
-    for (uint32_t i = 0; i < n; ++i) {
-        const int d = (int)a[i] - (int)b[i];
-        if (d) return d;
-    }
-    return (int)alen - (int)blen;
+constexpr uint32_t kMaxSlots = 64;
+
+__device__ __forceinline__ uint64_t be64(const uint8_t *p, uint32_t len) {  // first min(len,8) bytes, big-endian
+    uint64_t v = 0;
+    for (uint32_t i = 0; i < 8; ++i) v = (v << 8) | (i < len ? p[i] : 0u);
+    return v;
 }
 
-__global__ __launch_bounds__(256) void k_multiget(KeyBatch kb, const RegSlot *__restrict__ slots, uint32_t nslots,
-                                                  const uint8_t *__restrict__ ranges, uint64_t *__restrict__ maybe) {
+// Go bytewise compare of key (k0,k1 = its first 16 bytes big-endian) vs a stored range key.
+__device__ __forceinline__ int cmp_key(const uint8_t *key, uint32_t klen, uint64_t k0, uint64_t k1,
+                                       const uint64_t be[2], const uint8_t *bytes, uint32_t blen) {
+    if (k0 != be[0]) return k0 < be[0] ? -1 : 1;
+    if (k1 != be[1]) return k1 < be[1] ? -1 : 1;
+    // equal zero-padded 16-byte prefixes: the shorter key is a prefix of the other unless both
+    // run past 16 bytes, where the tail bytes (in HBM) decide
+    const uint32_t n = klen < blen ? klen : blen;
+    for (uint32_t i = 16; i < n; ++i)
+        if (key[i] != bytes[i]) return key[i] < bytes[i] ? -1 : 1;
+    return (int)klen - (int)blen;
+}
+
+template <int KFIX, bool M32>
+__device__ __forceinline__ uint32_t test_filter(const RegSlot &sl, uint64_t h1, uint64_t h2) {
+    uint32_t acc = 1u;
+    for_positions<KFIX, M32>(h1, h2, sl.md, sl.md.k, [&](uint32_t, uint64_t p) {
+        acc &= sl.words[p >> 5] >> (uint32_t)(p & 31);
+    });
+    return acc & 1u;
+}
+
+template <typename Src, int KFIX, bool M32>
+__global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const RegSlot *__restrict__ gslots,
+                                                  uint32_t nslots, RegLayout lay, const uint8_t *__restrict__ ranges,
+                                                  uint64_t *__restrict__ maybe) {
+    __shared__ RegSlot slots[kMaxSlots];
+    for (uint32_t s = threadIdx.x; s < nslots; s += blockDim.x) slots[s] = gslots[s];
+    __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kb.n; i += stride) {
         const uint8_t *key;
@@ -41,35 +68,60 @@ __global__ __launch_bounds__(256) void k_multiget(KeyBatch kb, const RegSlot *__
             klen = kb.stride;
         }
         uint64_t h1, h2;
-        fnv_range(key, 0, klen, h1, h2);
+        src.hash(i, h1, h2);
+        const uint64_t k0 = be64(key, klen), k1 = klen > 8 ? be64(key + 8, klen - 8) : 0ull;
         uint64_t mask = 0;
-        uint32_t done = 0;  // bit L: level L's covering file already found
-        for (uint32_t s = 0; s < nslots; ++s) {
-            const RegSlot sl = slots[s];
-            if (sl.level > 0) {
-                if (done & (1u << sl.level)) continue;
-                if (key_cmp(key, klen, ranges + sl.min_off, sl.min_len) < 0 ||
-                    key_cmp(key, klen, ranges + sl.max_off, sl.max_len) > 0)
-                    continue;
-                done |= 1u << sl.level;
+        for (uint32_t s = lay.lo[0]; s < lay.hi[0]; ++s)  // every L0 file
+            mask |= (uint64_t)test_filter<KFIX, M32>(slots[s], h1, h2) << slots[s].slot;
+        for (uint32_t L = 1; L < 5; ++L) {
+            uint32_t lo = lay.lo[L], hi = lay.hi[L];
+            if (lo == hi) continue;
+            int hit = -1;
+            if (lay.nonoverlap >> L & 1u) {
+                // last file with MinKey <= key; it is the only one that can cover the key
+                uint32_t a = lo, b = hi;
+                while (a < b) {
+                    const uint32_t mid = (a + b) >> 1;
+                    const RegSlot &sl = slots[mid];
+                    if (cmp_key(key, klen, k0, k1, sl.min_be, ranges + sl.min_off, sl.min_len) >= 0)
+                        a = mid + 1;
+                    else
+                        b = mid;
+                }
+                if (a > lo) {
+                    const RegSlot &sl = slots[a - 1];
+                    if (cmp_key(key, klen, k0, k1, sl.max_be, ranges + sl.max_off, sl.max_len) <= 0) hit = (int)a - 1;
+                }
+            } else {
+                for (uint32_t s = lo; s < hi && hit < 0; ++s) {
+                    const RegSlot &sl = slots[s];
+                    if (cmp_key(key, klen, k0, k1, sl.min_be, ranges + sl.min_off, sl.min_len) >= 0 &&
+                        cmp_key(key, klen, k0, k1, sl.max_be, ranges + sl.max_off, sl.max_len) <= 0)
+                        hit = (int)s;
+                }
             }
-            uint32_t acc = 1u;
-            for_positions<0, false>(h1, h2, sl.md, sl.md.k, [&](uint32_t, uint64_t p) {
-                if (acc) acc &= sl.words[p >> 5] >> (uint32_t)(p & 31);
-            });
-            mask |= (uint64_t)(acc & 1u) << sl.slot;
+            if (hit >= 0) mask |= (uint64_t)test_filter<KFIX, M32>(slots[hit], h1, h2) << slots[hit].slot;
         }
         maybe[i] = mask;
     }
 }
 
-hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const uint8_t *ranges,
-                           uint64_t *maybe, hipStream_t s) {
+hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
+                           const uint8_t *ranges, uint64_t *maybe, hipStream_t s) {
     if (kb.n == 0) return hipSuccess;
+    if (nslots > kMaxSlots) return hipErrorInvalidValue;
     uint64_t g = (kb.n + 255) / 256;
     if (g > 65536) g = 65536;
-    hipLaunchKernelGGL(k_multiget, dim3((unsigned)g), dim3(256), 0, s, kb, slots, nslots, ranges, maybe);
-    return hipGetLastError();
+    return with_src(kb, [&](auto src) {
+        using S = decltype(src);
+        if (lay.all_k7_m32)
+            hipLaunchKernelGGL((k_multiget<S, 7, true>), dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay,
+                               ranges, maybe);
+        else
+            hipLaunchKernelGGL((k_multiget<S, 0, false>), dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots,
+                               lay, ranges, maybe);
+        return hipGetLastError();
+    });
 }
 
 }  // namespace seb

@@ -623,3 +623,44 @@ def test_registry_multiget_matches_lsm_get_walk(seb, torch_cuda):
     with pytest.raises(seb.SebError):
         reg.remove(123456)
     reg.close()
+
+
+def test_registry_multiget_overlap_long_keys_generic_k(seb, torch_cuda):
+    """The branches the LSM bench layout does not reach: an overlapping level (the reference's
+    first-cover linear scan, lsm/lsm.go:184-196), range keys longer than the 16-byte LDS prefix
+    that tie on it (HBM tail compare), prefix-of relations, and filters with k != 7."""
+    rng = np.random.default_rng(29)
+    reg = seb.Registry(0)
+    files = []
+
+    def add(file_num, level, keys, fpr, seq):
+        m, k = oc.params(max(len(keys), 1), fpr)
+        arr = np.frombuffer(b"".join(keys), np.uint8)
+        lens = np.array([len(x) for x in keys], np.uint64)
+        off = np.zeros(len(keys) + 1, np.uint64)
+        np.cumsum(lens, out=off[1:])
+        bits = oc.build(m, k, arr, len(keys), offsets=off)
+        slot = reg.put(file_num, level, bn.encode(bits, m, k), min(keys), max(keys))
+        files.append(dict(file=file_num, level=level, min=min(keys), max=max(keys), bits=bits, m=m, k=k, seq=seq,
+                          slot=slot))
+
+    pre = b"tenant/0000000/" + b"x"  # 16-byte shared prefix
+    universe = sorted({pre + b"%06d" % int(i) + b"z" * int(rng.integers(0, 12)) for i in rng.integers(0, 50000, 6000)})
+    universe += [pre[:-1], pre, pre + b"\x00", pre[:10]]
+    universe = sorted(set(universe))
+    seq = 0
+    for lvl, parts, fpr in ((1, 5, 0.001), (2, 3, 0.05)):
+        chunks = np.array_split(np.array(universe, dtype=object), parts)
+        for j in range(parts):
+            lo = max(0, len(chunks[0]) * j - 200)  # overlap the previous chunk by ~200 keys
+            keys = universe[lo:lo + len(chunks[j]) + 200]
+            add(1000 * lvl + j, lvl, keys, fpr, seq)
+            seq += 1
+    add(3000, 3, universe[::7], 0.2, seq)
+    probes = list(rng.choice(universe, 2000).tolist())
+    probes += [pre + b"%06d" % int(i) for i in rng.integers(0, 50000, 1500)]
+    probes += [pre, pre[:-1], pre[:15] + b"y", pre + b"\x00", pre + b"\x00\x00", b"", b"tenant/", universe[-1] + b"!"]
+    got = reg.multiget(probes)
+    want = np.array([_lsm_get_model(files, p) for p in probes], dtype=np.uint64)
+    assert np.array_equal(got, want)
+    reg.close()
