@@ -41,7 +41,7 @@ GOLDEN_C5 = "0668715db8804f529bc6795461a1cbd9905bbaab44b18b88a3b29881cd29f375"  
 GOLDEN_LSM = "caf8282a71e15e15141639089e86e2ae5adabdfc91f69ea47e28fe5d71a941f9"  # sha256(MultiGet masks)
 OPTIONS = ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "bucket_min_keys",
            "multi_interleave", "varlen_prehash_min_keys", "varlen_sort_min_keys", "scatter_threads",
-           "stream_nt", "probe_persistent", "scatter_kpt")
+           "stream_nt", "probe_persistent", "scatter_kpt", "probe_mode")
 
 
 def sha(b) -> str:

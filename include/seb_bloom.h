@@ -76,8 +76,16 @@ int seb_abi_version(void);
  *   "probe_kpt"       k == 7 probes: keys per thread (1, 2, 4) — gathers in flight per lane
  *   "bucket_min_keys" auto build_algo: radix-partitioned from this many keys on
  *   "grid_cap"        maximum workgroups of the grid-stride kernels
- * Environment variables SEB_BUILD_ALGO, SEB_PROBE_SPLIT, SEB_BUCKET_MIN_KEYS, SEB_GRID_CAP set the
- * initial values. */
+ *   "probe_slice_shift" k == 7, m < 2^32 probes: slice of 2^shift words gathered per phase (0 = off)
+ *   "probe_slice_grid"  sliced probe: workgroup cap (0 = grid_cap)
+ *   "probe_mode"      sliced probe gather order 0-3 (see k_probe_sliced)
+ *   "probe_persistent" sliced probe: persistent 1024-thread workgroups (0 = off)
+ *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
+ *   "scatter_threads", "scatter_kpt"  radix-partitioned build: workgroup size, keys per thread
+ *   "stream_nt"       non-temporal loads of 16-B key batches (0/1)
+ *   "varlen_prehash_min_keys", "varlen_sort_min_keys"  variable-length batches: LDS pre-hash and
+ *                     global length-sort thresholds
+ * Environment variables SEB_<NAME> (upper case) set the initial values. */
 int seb_set_option(const char *name, int64_t value);
 int seb_get_option(const char *name, int64_t *value);
 const char *seb_last_error(void);

@@ -27,7 +27,6 @@ constexpr int kBktShift = 16;                            // 64 Ki bits per bucke
 constexpr uint32_t kBktWords = 1u << (kBktShift - 5);   // 2048 u32 words = 8 KiB of LDS
 constexpr uint32_t kMaxBuckets = 4096;                   // m <= 2^28 bits
 constexpr uint32_t kTilePos = 28672;                     // positions per tile sorted in LDS (112 KiB)
-constexpr uint32_t kKpt7 = 4;                            // keys per thread per round when k == 7
 constexpr uint32_t kMaxTiles = 1024;                     // super-tiles (workgroups) per launch
 constexpr uint32_t kTargetTiles = 256;                   // workgroups per CU x 256 CUs
 
@@ -64,7 +63,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *w
 // fixed-capacity region (bucket b, tile t) in HBM.  A run that would overflow its region (never
 // for hash-distributed keys: cap = mean + 8 sigma + 32) is OR-ed straight into the filter with
 // device-scope atomics instead, which k_bkt_apply's read-modify-write OR preserves.
-// LDS: sorted[kTilePos] u32 | cursor[nb] | fill[nb] | wsum[16]
+// LDS: sorted[THREADS*KPT7*7] u32 | cursor[nb] | fill[nb] | wsum[16] | ovf
 template <typename Src, int KFIX, int THREADS, int KPT7>
 __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, ModArg md, uint32_t nb,
                                                               uint32_t tile_keys, uint32_t ntiles, uint32_t cap,
@@ -77,11 +76,13 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, Mo
     uint32_t *cursor = smem + kPos;
     uint32_t *fill = cursor + nb;
     uint32_t *wsum = fill + nb;
+    uint32_t *ovf = wsum + 16;
     const uint32_t t = blockIdx.x;
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
         cursor[b] = 0u;
         fill[b] = 0u;
     }
+    if (threadIdx.x == 0) *ovf = 0u;
     __syncthreads();
     const uint32_t round_keys = KFIX > 0 ? KPT7 * THREADS : kPos / md.k;
     const uint64_t t0 = (uint64_t)t * tile_keys;
@@ -150,25 +151,40 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, Mo
             }
         }
         __syncthreads();
-        // cursor[b] is now the END of bucket b's run in `sorted`, its start is cursor[b-1]: turn
-        // fill[b] into (fill - start) so an element's region slot is fill[b] + its sorted index.
-        for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) fill[b] -= b ? cursor[b - 1] : 0u;
+        // cursor[b] is now the END of bucket b's run in `sorted` and its start is cursor[b-1].
+        // Turn fill[b] into the region element index of sorted[0] (mod 2^32), so that sorted[idx]
+        // belongs at regions[fill[b] + idx], and flag a run that would overflow its region.
+        for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+            const uint32_t start = b ? cursor[b - 1] : 0u;
+            const uint32_t fb = fill[b];
+            if (fb + (cursor[b] - start) > cap) *ovf = 1u;
+            fill[b] = (b * ntiles + t) * cap + fb - start;
+        }
         __syncthreads();
         const uint32_t cnt = (uint32_t)(k1 - k0) * md.k;
-        for (uint32_t idx = threadIdx.x; idx < cnt; idx += blockDim.x) {
-            const uint32_t p = sorted[idx];
-            const uint32_t b = p >> kBktShift;
-            const uint32_t slot = fill[b] + idx;
-            if (slot < cap)
-                regions[((uint64_t)b * ntiles + t) * cap + slot] = (uint16_t)p;
-            else
-                __hip_atomic_fetch_or(words + (p >> 5), 1u << (p & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (*ovf == 0u) {  // every run fits (hash-distributed keys): one LDS read + store each
+#pragma unroll 5
+            for (uint32_t idx = threadIdx.x; idx < cnt; idx += blockDim.x) {
+                const uint32_t p = sorted[idx];
+                regions[fill[p >> kBktShift] + idx] = (uint16_t)p;
+            }
+        } else {
+            for (uint32_t idx = threadIdx.x; idx < cnt; idx += blockDim.x) {
+                const uint32_t p = sorted[idx];
+                const uint32_t b = p >> kBktShift;
+                const uint32_t e = fill[b] + idx;
+                if (e - (b * ntiles + t) * cap < cap)
+                    regions[e] = (uint16_t)p;
+                else
+                    __hip_atomic_fetch_or(words + (p >> 5), 1u << (p & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         __syncthreads();
         for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
-            fill[b] += cursor[b];  // (fill - start) + end = fill + this round's count
+            fill[b] += cursor[b] - (b * ntiles + t) * cap;  // fill + this round's count
             cursor[b] = 0u;
         }
+        if (threadIdx.x == 0) *ovf = 0u;
         __syncthreads();
     }
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) counts[(uint64_t)b * ntiles + t] = min(fill[b], cap);
@@ -219,15 +235,22 @@ struct BktPlan {
 };
 
 static uint32_t scatter_threads() { return options().scatter_threads == 512 ? 512u : 1024u; }
-static uint32_t scatter_kpt() { return options().scatter_kpt == 5 ? 5u : 4u; }
+// 5 keys per thread per round only while its sort buffer and the two per-bucket arrays fit the
+// 160 KiB of LDS (nb <= 2551 at 1024 threads, m <= ~167M bits); 4 otherwise.
+static uint32_t scatter_kpt(uint32_t nb) {
+    const uint32_t thr = scatter_threads();
+    if (options().scatter_kpt == 5 && ((uint64_t)thr * 5 * 7 + 2 * nb + 17) * 4 <= 160u * 1024) return 5u;
+    return 4u;
+}
 
 static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k) {
     BktPlan p{};
     const uint64_t nwords = (m + 31) / 32;
     p.nb = (uint32_t)((nwords + kBktWords - 1) / kBktWords);
     const uint32_t thr = scatter_threads();
-    const uint32_t pos = thr * scatter_kpt() * 7;
-    const uint32_t round_keys = k == 7 ? scatter_kpt() * thr : pos / k;
+    const uint32_t kpt = scatter_kpt(p.nb);
+    const uint32_t pos = thr * kpt * 7;
+    const uint32_t round_keys = k == 7 ? kpt * thr : pos / k;
     const uint32_t target = kTargetTiles * (1024 / thr);
     uint64_t rounds_total = (n + round_keys - 1) / round_keys;
     uint64_t rounds_per_tile = (rounds_total + target - 1) / target;
@@ -275,13 +298,14 @@ hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModA
             sub.data = kb.data + k0 * (uint64_t)kb.stride;
         const BktPlan p = plan_bucketed(sub.n, md.m, md.k);
         if (p.bytes > ws_bytes || p.ntiles > kMaxTiles) return hipErrorInvalidValue;
+        if ((uint64_t)p.nb * p.ntiles * p.cap >= (1ull << 31)) return hipErrorInvalidValue;  // u32 region index
         uint8_t *w = (uint8_t *)ws;
         uint16_t *regions = (uint16_t *)(w + p.off_regions);
         uint32_t *counts = (uint32_t *)(w + p.off_counts);
         const uint64_t nwords = (md.m + 31) / 32;
         const uint32_t thr = scatter_threads();
-        const uint32_t kpt = scatter_kpt();
-        const size_t lds = ((size_t)thr * kpt * 7 + 2 * p.nb + 16) * sizeof(uint32_t);
+        const uint32_t kpt = scatter_kpt(p.nb);
+        const size_t lds = ((size_t)thr * kpt * 7 + 2 * p.nb + 17) * sizeof(uint32_t);
         hipError_t e = with_src(sub, [&](auto src) -> hipError_t {
             using S = decltype(src);
             auto scat = thr == 512 ? (md.k == 7 ? k_bkt_scatter<S, 7, 512, 4> : k_bkt_scatter<S, 0, 512, 4>)

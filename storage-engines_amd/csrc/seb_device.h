@@ -166,16 +166,21 @@ __device__ __forceinline__ void for_positions(uint64_t h1, uint64_t h2, const Mo
         const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
         uint32_t r = (uint32_t)mod64(h1, md.m, md.mu);
         const uint32_t b = (uint32_t)mod64(h2, md.m, md.mu);
+        // Step addend: b, or (b - c) mod m when the u64 sum wraps.  Kept negated (m - a, in
+        // [1, m]) so r + a mod m is one subtract, one compare and a conditional add of m, with
+        // no u32 overflow for any m < 2^32.
+        const uint32_t nb = m - b;
+        const uint32_t bc = b >= c ? b - c : b + (m - c);
+        const uint32_t nd = m - bc;
         f(0u, (uint64_t)r);
 #pragma unroll
         for (uint32_t i = 1; i < k; ++i) {
             uint64_t xn = x + h2;
-            bool carry = xn < x;
+            const bool carry = xn < x;
             x = xn;
-            uint32_t s = r + b;
-            s = (s < r || s >= m) ? s - m : s;
-            uint32_t t = s >= c ? s - c : s + (m - c);
-            r = carry ? t : s;
+            const uint32_t na = carry ? nd : nb;
+            const uint32_t t = r - na;
+            r = r >= na ? t : t + m;
             f(i, (uint64_t)r);
         }
     } else {

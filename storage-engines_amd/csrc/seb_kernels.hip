@@ -99,7 +99,27 @@ __global__ __launch_bounds__(256) void k_probe(Src src, uint64_t n, const uint32
 // one XCD then share a single slice in that XCD's L2 instead of thrashing the whole filter; a
 // key whose bits so far include a clear one skips its remaining gathers.  Which slice a gather
 // belongs to changes only when it is issued, never the answer.
-template <typename Src, int KPT>
+// MODE selects how the gathers of one thread are ordered (the answers never change):
+//   0  per position, skipping the rest of a key once a clear bit is seen.  Every gather then
+//      depends on the previous one, so a wave has a single gather in flight.
+//   1  per slice: the key's liveness is sampled once at the start of each slice, so the gathers
+//      of one slice are independent and overlap; a dead key skips the later slices.
+//   2  no slices: the 7 positions are sorted ascending (16-comparator network) and all gathers
+//      are issued back to back, so lanes of a wave sweep the filter in the same direction.
+//   3  per slice without the liveness test (every position gathered once, all independent).
+template <int KPT>
+__device__ __forceinline__ void sort7(uint32_t (&p)[KPT][7], int r) {
+    constexpr int net[16][2] = {{0, 6}, {2, 3}, {4, 5}, {0, 2}, {1, 4}, {3, 6}, {0, 1}, {2, 5},
+                                {3, 4}, {1, 2}, {4, 6}, {2, 3}, {4, 5}, {1, 2}, {3, 4}, {5, 6}};
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const uint32_t a = p[r][net[c][0]], b = p[r][net[c][1]];
+        p[r][net[c][0]] = min(a, b);
+        p[r][net[c][1]] = max(a, b);
+    }
+}
+
+template <typename Src, int KPT, int MODE>
 __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, const uint32_t *__restrict__ words,
                                                       ModArg md, uint8_t *__restrict__ out, uint32_t slice_shift,
                                                       uint32_t nslices) {
@@ -115,14 +135,47 @@ __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, const
             for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
             acc[r] = i < n ? 1u : 0u;
         }
-        for (uint32_t sl = 0; sl < nslices; ++sl) {
+        if constexpr (MODE == 2) {
+#pragma unroll
+            for (int r = 0; r < KPT; ++r) sort7<KPT>(pos, r);
+            uint32_t v[KPT][7];
+#pragma unroll
+            for (int q = 0; q < 7; ++q)
+#pragma unroll
+                for (int r = 0; r < KPT; ++r) v[r][q] = words[pos[r][q] >> 5];
 #pragma unroll
             for (int r = 0; r < KPT; ++r)
 #pragma unroll
-                for (int q = 0; q < 7; ++q) {
-                    const uint32_t w = pos[r][q] >> 5;
-                    if ((acc[r] & 1u) && (w >> slice_shift) == sl) acc[r] &= words[w] >> (pos[r][q] & 31);
-                }
+                for (int q = 0; q < 7; ++q) acc[r] &= v[r][q] >> (pos[r][q] & 31);
+        } else if constexpr (MODE == 0) {
+            for (uint32_t sl = 0; sl < nslices; ++sl) {
+#pragma unroll
+                for (int r = 0; r < KPT; ++r)
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) {
+                        const uint32_t w = pos[r][q] >> 5;
+                        if ((acc[r] & 1u) && (w >> slice_shift) == sl) acc[r] &= words[w] >> (pos[r][q] & 31);
+                    }
+            }
+        } else {
+            for (uint32_t sl = 0; sl < nslices; ++sl) {
+                uint32_t live[KPT];
+#pragma unroll
+                for (int r = 0; r < KPT; ++r) live[r] = MODE == 1 ? (acc[r] & 1u) : 1u;
+                uint32_t v[KPT][7];
+#pragma unroll
+                for (int r = 0; r < KPT; ++r)
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) {
+                        const uint32_t w = pos[r][q] >> 5;
+                        v[r][q] = ~0u;
+                        if (live[r] && (w >> slice_shift) == sl) v[r][q] = words[w];
+                    }
+#pragma unroll
+                for (int r = 0; r < KPT; ++r)
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) acc[r] &= v[r][q] >> (pos[r][q] & 31);
+            }
         }
 #pragma unroll
         for (int r = 0; r < KPT; ++r) {
@@ -342,7 +395,23 @@ static hipError_t launch_sliced_t(const Src &src, uint64_t n, const uint32_t *wo
         return hipGetLastError();
     }
     unsigned g = grid_for((n + KPT - 1) / KPT, 256, o.probe_slice_grid ? o.probe_slice_grid : o.grid_cap);
-    hipLaunchKernelGGL((k_probe_sliced<Src, KPT>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift, nslices);
+    switch (o.probe_mode) {
+        case 1:
+            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 1>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
+                               nslices);
+            break;
+        case 2:
+            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 2>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
+                               nslices);
+            break;
+        case 3:
+            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 3>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
+                               nslices);
+            break;
+        default:
+            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 0>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
+                               nslices);
+    }
     return hipGetLastError();
 }
 

@@ -664,3 +664,32 @@ def test_registry_multiget_overlap_long_keys_generic_k(seb, torch_cuda):
     want = np.array([_lsm_get_model(files, p) for p in probes], dtype=np.uint64)
     assert np.array_equal(got, want)
     reg.close()
+
+
+@pytest.mark.parametrize("case", ["duplicates", "skewed", "large_m"])
+def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
+    """Radix-partitioned build paths a hash-distributed batch never takes: runs that overflow
+    their fixed-capacity region (identical keys put a tile's positions into 7 buckets; skewed: a
+    few distinct keys repeated) fall back to device-scope atomic OR, and a filter with more
+    buckets than the 5-keys-per-thread LDS layout holds (m = 200M bits) uses 4 keys per thread.
+    The bit array must equal the oracle's either way."""
+    torch = torch_cuda
+    seb.set_option("build_algo", 2)
+    try:
+        rng = np.random.default_rng(5)
+        if case == "duplicates":
+            n, m, k = 400_000, 3_834_024, 7
+            keys = np.tile(kg.key16(np.array([42])), (n, 1))
+        elif case == "skewed":
+            n, m, k = 400_000, 3_834_024, 7
+            keys = kg.key16(rng.integers(0, 50, n))
+        else:
+            n, m, k = 300_000, 200_000_000, 7
+            keys = kg.key16(np.arange(n))
+        kd = seb.dev_keys(to_dev(torch, keys), n=n, stride=16)
+        words, bits = dev_build_bits(seb, torch, kd, m, k)
+        uniq = np.unique(keys, axis=0)
+        ref = oc.build(m, k, np.ascontiguousarray(uniq).ravel(), len(uniq), stride=16)
+        assert np.array_equal(bits, ref)
+    finally:
+        seb.set_option("build_algo", 0)
