@@ -107,6 +107,8 @@ __global__ __launch_bounds__(256) void k_probe(Src src, uint64_t n, const uint32
 //   2  no slices: the 7 positions are sorted ascending (16-comparator network) and all gathers
 //      are issued back to back, so lanes of a wave sweep the filter in the same direction.
 //   3  per slice without the liveness test (every position gathered once, all independent).
+//   4  no slices: positions sorted ascending, gathered in that order with mode 0's early exit, so
+//      a workgroup generation sweeps the filter low to high without per-slice tests.
 template <int KPT>
 __device__ __forceinline__ void sort7(uint32_t (&p)[KPT][7], int r) {
     constexpr int net[16][2] = {{0, 6}, {2, 3}, {4, 5}, {0, 2}, {1, 4}, {3, 6}, {0, 1}, {2, 5},
@@ -135,7 +137,15 @@ __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, const
             for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
             acc[r] = i < n ? 1u : 0u;
         }
-        if constexpr (MODE == 2) {
+        if constexpr (MODE == 4) {
+#pragma unroll
+            for (int r = 0; r < KPT; ++r) {
+                sort7<KPT>(pos, r);
+#pragma unroll
+                for (int q = 0; q < 7; ++q)
+                    if (acc[r] & 1u) acc[r] &= words[pos[r][q] >> 5] >> (pos[r][q] & 31);
+            }
+        } else if constexpr (MODE == 2) {
 #pragma unroll
             for (int r = 0; r < KPT; ++r) sort7<KPT>(pos, r);
             uint32_t v[KPT][7];
@@ -402,6 +412,10 @@ static hipError_t launch_sliced_t(const Src &src, uint64_t n, const uint32_t *wo
             break;
         case 2:
             hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 2>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
+                               nslices);
+            break;
+        case 4:
+            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 4>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
                                nslices);
             break;
         case 3:
