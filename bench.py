@@ -39,6 +39,9 @@ GOLDEN_C2 = "a86f3c69041ea0caac1dc559cfb36b06d5d5513d4ee203d22878715f612a0c3a"  
 GOLDEN_C3 = "aba77536fae51d566de525f519cd4c573799880d63000d88a2ce3052d0b90f95"  # sha256(answers)
 GOLDEN_C5 = "0668715db8804f529bc6795461a1cbd9905bbaab44b18b88a3b29881cd29f375"  # sha256(u64 masks)
 GOLDEN_LSM = "caf8282a71e15e15141639089e86e2ae5adabdfc91f69ea47e28fe5d71a941f9"  # sha256(MultiGet masks)
+GOLDEN_ROUTE = "d4ba568830284e7cac12e54c58ea3b6e35b5acd0fbe1cafe90269f177f778ff0"  # sha256(u32 perm), 10M, 8 bits
+GOLDEN_ROUTE_BEGIN = "0afec9b77141e0845ef7750736ed4667d1d1adf3df91c0ab47e85c09302ba1ff"  # sha256(u64 shard_begin)
+GOLDEN_WAL = "7d661e321c2804cebf541abd9c1a34463b70fe27fce3c5459a71408ac91b3e01"  # sha256(u32 CRCs), 2M records
 OPTIONS = ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "bucket_min_keys",
            "multi_interleave", "varlen_prehash_min_keys", "varlen_sort_min_keys", "scatter_threads",
            "stream_nt", "probe_persistent", "scatter_kpt", "probe_mode")
@@ -53,7 +56,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "lsm"])
+    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "lsm", "route", "wal"])
     ap.add_argument("--keys", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
@@ -70,6 +73,9 @@ class Setup:
     """Inputs resident in HBM plus the per-step work of one config."""
 
     workload = ""
+    unit = "Mkeys/s"
+    probe_name = "probe"
+    dtype = "u64"
     parallelism = ""
     scaling = "weak"
     units_per_step = 0.0
@@ -250,6 +256,76 @@ def setup_lsm(args, seb, kg, torch, dev, rank, world, dist):
     return st
 
 
+def setup_route(args, seb, kg, torch, dev, rank, world, dist):
+    """the hash index's shard routing (FNV-1a 32 & 255, hashindex/shard.go:47-52)
+    and UpdateBatch's distribution of a batch over the 256 shards (:104-122) as one stable partition
+    of 10M x 16-B keys per GPU (independent batches: weak scaling)."""
+    st = Setup()
+    n, bits = args.keys, 8
+    st.m, st.k, st.n = 0, 0, n
+    keys = torch.from_numpy(kg.key16(rank * n + np.arange(n))).to(dev)
+    st.kd = seb.dev_keys(keys, n=n, stride=16)
+    st.perm = torch.zeros(n, dtype=torch.int32, device=dev)
+    st.begin = torch.zeros((1 << bits) + 1, dtype=torch.int64, device=dev)
+    st.ws = torch.empty(seb.dev_shard_partition_workspace_size(n, bits), dtype=torch.uint8, device=dev)
+    st.kernel_bytes = {"route": 16.0 * n + 4.0 * n + 8.0 * ((1 << bits) + 1)}
+    st.units_per_step = float(n) * world
+    st.probe_name = "route"
+    st.dtype = "u32"
+    st.workload = ("hash-index shard routing (SURVEY 8(f) row 4): FNV-1a32 & 255 of 10M x 16-B keys + stable "
+                   "partition into the 256 shards (UpdateBatch's distribution step)")
+    st.parallelism = f"independent batch per gpu x{world}"
+    st.probe = lambda j: seb.dev_shard_partition(st.kd, bits, st.perm, st.begin, None, st.ws)
+
+    def parity(j):
+        if rank != 0 or n != 10_000_000:
+            return None
+        ok = (sha(st.perm.cpu().numpy().view(np.uint32).astype("<u4").tobytes()) == GOLDEN_ROUTE and
+              sha(st.begin.cpu().numpy().view(np.uint64).astype("<u8").tobytes()) == GOLDEN_ROUTE_BEGIN)
+        return "bit-exact (sha256 of the 10M-entry permutation and shard bounds match tests/golden route)" if ok \
+            else "MISMATCH partition"
+
+    st.parity = parity
+    return st
+
+
+def setup_wal(args, seb, kg, torch, dev, rank, world, dist):
+    """ReadAll's integrity check of a WAL image (lsm/wal.go:98-133) on the GPU:
+    CRC32-IEEE of every record's [4:] against its stored field, plus framing.  2M records of
+    key16 + 100-B values (every 16th a Delete), sealed at generation by zlib.crc32."""
+    st = Setup()
+    lay = kg.WAL_LAYOUT
+    img, off = kg.wal_image(lay["records"], lay["value_size"], lay["delete_every"])
+    n = lay["records"]
+    st.m, st.k, st.n = 0, 0, n
+    st.img = torch.from_numpy(img).to(dev)
+    st.off = torch.from_numpy(off.view(np.int64)).to(dev)
+    st.stored = img[off[:-1].astype(np.int64)[:, None] + np.arange(4)].copy().view("<u4").ravel()
+    st.crc = torch.zeros(n, dtype=torch.int32, device=dev)
+    st.ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    st.kernel_bytes = {"wal_verify": float(img.size) + 8.0 * (n + 1) + 5.0 * n}
+    st.units_per_step = float(n) * world
+    st.unit = "Mrecords/s"
+    st.probe_name = "wal_verify"
+    st.dtype = "u32"
+    st.workload = (f"WAL integrity check (SURVEY 8(f) row 4): CRC32-IEEE + framing of {n} records "
+                   f"({img.size / 1e6:.1f} MB; 16-B keys, 100-B values, every 16th a Delete)")
+    st.parallelism = f"independent WAL image per gpu x{world}"
+    st.probe = lambda j: seb.dev_wal_crc(st.img, st.off, seb.WAL_VERIFY, st.crc, st.ok)
+
+    def parity(j):
+        if rank != 0:
+            return None
+        crc = st.crc.cpu().numpy().view(np.uint32)
+        ok = bool(st.ok.cpu().numpy().all()) and np.array_equal(crc, st.stored) and \
+            sha(crc.astype("<u4").tobytes()) == GOLDEN_WAL
+        return "bit-exact (every CRC equals its zlib-sealed field; sha256 of the CRCs matches tests/golden wal)" \
+            if ok else "MISMATCH crc"
+
+    st.parity = parity
+    return st
+
+
 def main():
     args = parse()
     import torch
@@ -278,7 +354,8 @@ def main():
         if v is not None:
             seb.set_option(o, v)
 
-    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "lsm": setup_lsm}[args.config]
+    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "lsm": setup_lsm, "route": setup_route,
+             "wal": setup_wal}[args.config]
     st = setup(args, seb, kg, torch, dev, rank, world, dist)
     torch.cuda.synchronize()
     overlap = bool(args.overlap) and st.build is not None
@@ -345,7 +422,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kern_ms = {name: float(np.mean([a.elapsed_time(b) for a, b in pairs])) for name, pairs in times.items() if pairs}
+    kern_ms = {(st.probe_name if name == "probe" else name): float(np.mean([a.elapsed_time(b) for a, b in pairs]))
+               for name, pairs in times.items() if pairs}
     value = st.units_per_step * args.steps / elapsed / 1e6
     result = None
     if rank == 0:
@@ -358,9 +436,10 @@ def main():
                 traffic = json.load(f).get(args.config, {}).get(dom, {}).get("hbm_bytes_per_launch")
         ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
         result = {
-            "metric": METRIC, "value": round(value, 2), "unit": "Mkeys/s", "n_gpus": world,
+            "metric": METRIC if args.config in ("c2c3", "c4", "c5", "lsm") else f"{args.config} {st.unit}",
+            "value": round(value, 2), "unit": st.unit, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),
-            "higher_is_better": True, "scaling": st.scaling, "vs_baseline": None, "dtype": "u64",
+            "higher_is_better": True, "scaling": st.scaling, "vs_baseline": None, "dtype": st.dtype,
             "data": "synthetic (reference key format user%010d+2B, common/benchmark/keygen.go:89-109)",
             "config": {"workload": st.workload, "keys_per_gpu": st.n, "fpr": 0.01, "num_bits": st.m,
                        "num_hashes": st.k, "parallelism": st.parallelism},

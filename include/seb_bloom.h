@@ -193,6 +193,35 @@ int seb_registry_slots(seb_registry *reg, uint64_t *file_nums, int32_t *levels, 
 int seb_registry_multiget(seb_registry *reg, const seb_keys *keys, uint64_t *maybe);          /* host keys */
 int seb_registry_multiget_dev(seb_registry *reg, const seb_keys *keys, uint64_t *maybe, void *stream);
 
+/* ---------- hash-index shard routing + WAL record checksums (off the bloom path) ---- */
+/* shard[i] = FNV-1a32(key i) & ((1 << shard_bits) - 1), the reference's getShard
+ * (hashindex/shard.go:47-52; 256 shards = shard_bits 8).  hash[i] (nullable) = the full FNV-1a32.
+ * shard (nullable) is one u16 per key; shard_bits <= 16.  Device pointers. */
+int seb_dev_shard_route(const seb_keys *keys, uint32_t shard_bits, uint16_t *shard, uint32_t *hash, void *stream);
+/* Stable partition of a key batch by shard: UpdateBatch's distribution step (hashindex/shard.go:104-122).
+ * perm = key indices grouped by shard ascending, input order inside a shard; shard s owns
+ * perm[shard_begin[s], shard_begin[s+1]) (shard_begin nullable, 2^shard_bits + 1 entries); shard
+ * (nullable) as above.  shard_bits <= 12, n < 2^32; workspace of
+ * seb_dev_shard_partition_workspace_size bytes.  The reference distributes a Go map, whose order
+ * is random: it defines only the set per shard, which this order refines. */
+uint64_t seb_dev_shard_partition_workspace_size(uint64_t n, uint32_t shard_bits);
+int seb_dev_shard_partition(const seb_keys *keys, uint32_t shard_bits, uint32_t *perm, uint64_t *shard_begin,
+                            uint16_t *shard, void *workspace, uint64_t workspace_bytes, void *stream);
+/* WAL records (lsm/wal.go:31-62): record i = data[rec_off[i], rec_off[i+1]) =
+ * [crc32 u32][seq u64][keySize u32][valueSize u32][deleted u8][key][value], all little-endian,
+ * crc = crc32.ChecksumIEEE(record[4:]).  SEB_WAL_CRC: crc[i] only; SEB_WAL_SEAL: also store it in
+ * the record (Append, :59-60); SEB_WAL_VERIFY: ok[i] = 1 iff the record is framed (length >= 21
+ * and 21 + keySize + valueSize == length) and its stored CRC matches (ReadAll, :98-133).  crc and
+ * ok are nullable except ok for VERIFY.  Device pointers. */
+enum seb_wal_mode { SEB_WAL_CRC = 0, SEB_WAL_SEAL = 1, SEB_WAL_VERIFY = 2 };
+int seb_dev_wal_crc(uint8_t *data, const uint64_t *rec_off, uint64_t n, int mode, uint32_t *crc, uint8_t *ok,
+                    void *stream);
+/* Host: walk a WAL image's framing as ReadAll does (21-byte header, then keySize + valueSize bytes)
+ * into rec_off (cap entries).  *n = complete records; rec_off[0..*n] are their boundaries.
+ * SEB_OK if the image ends on a record boundary, SEB_ERR_SHORT if the tail is a truncated header or
+ * payload (ReadAll's "failed to read WAL header/data" error), SEB_ERR_INVALID if cap < records + 1. */
+int seb_wal_scan(const uint8_t *data, uint64_t bytes, uint64_t *rec_off, uint64_t cap, uint64_t *n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1182,3 +1182,76 @@ extern "C" int seb_registry_multiget(seb_registry *r, const seb_keys *kb, uint64
     HIP_OR_FAIL(hipStreamSynchronize(c->s_d2h));
     return SEB_OK;
 }
+
+// ------------------------------------------------ shard routing + WAL checksums (§8(f) row 4)
+
+extern "C" int seb_dev_shard_route(const seb_keys *keys, uint32_t bits, uint16_t *shard, uint32_t *hash,
+                                   void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc;
+    if ((rc = check_keys(keys, "seb_dev_shard_route"))) return rc;
+    if (bits > 16) return fail(SEB_ERR_INVALID, "seb_dev_shard_route: shard_bits %u > 16", bits);
+    HIP_OR_FAIL(launch_route(key_batch(keys), bits, shard, hash, (hipStream_t)stream));
+    return SEB_OK;
+}
+
+extern "C" uint64_t seb_dev_shard_partition_workspace_size(uint64_t n, uint32_t bits) {
+    return bits > 12 ? 0 : route_workspace_bytes(n, bits);
+}
+
+extern "C" int seb_dev_shard_partition(const seb_keys *keys, uint32_t bits, uint32_t *perm, uint64_t *shard_begin,
+                                       uint16_t *shard, void *ws, uint64_t ws_bytes, void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc;
+    if ((rc = check_keys(keys, "seb_dev_shard_partition"))) return rc;
+    if (bits > 12) return fail(SEB_ERR_INVALID, "seb_dev_shard_partition: shard_bits %u > 12", bits);
+    if (keys->n >= (1ull << 32)) return fail(SEB_ERR_INVALID, "seb_dev_shard_partition: n >= 2^32");
+    if (keys->n && (!perm || !ws)) return fail(SEB_ERR_INVALID, "seb_dev_shard_partition: null perm/workspace");
+    if (ws_bytes < route_workspace_bytes(keys->n, bits))
+        return fail(SEB_ERR_INVALID, "seb_dev_shard_partition: workspace %llu < %llu bytes",
+                    (unsigned long long)ws_bytes, (unsigned long long)route_workspace_bytes(keys->n, bits));
+    HIP_OR_FAIL(launch_route_partition(key_batch(keys), bits, perm, shard_begin, shard, ws, ws_bytes,
+                                       (hipStream_t)stream));
+    return SEB_OK;
+}
+
+extern "C" int seb_dev_wal_crc(uint8_t *data, const uint64_t *rec_off, uint64_t n, int mode, uint32_t *crc,
+                               uint8_t *ok, void *stream) {
+    std::call_once(g_env_once, load_env);
+    if (mode < SEB_WAL_CRC || mode > SEB_WAL_VERIFY) return fail(SEB_ERR_INVALID, "seb_dev_wal_crc: bad mode %d", mode);
+    if (n && (!data || !rec_off)) return fail(SEB_ERR_INVALID, "seb_dev_wal_crc: null data/offsets");
+    if (n && mode == SEB_WAL_VERIFY && !ok) return fail(SEB_ERR_INVALID, "seb_dev_wal_crc: VERIFY needs ok[]");
+    HIP_OR_FAIL(launch_wal_crc(data, rec_off, n, mode, crc, ok, (hipStream_t)stream));
+    return SEB_OK;
+}
+
+// ReadAll's framing walk (lsm/wal.go:98-121): a 21-byte header, then keySize + valueSize bytes.
+extern "C" int seb_wal_scan(const uint8_t *data, uint64_t bytes, uint64_t *rec_off, uint64_t cap, uint64_t *n) {
+    if (!n || (bytes && !data)) return fail(SEB_ERR_INVALID, "seb_wal_scan: null argument");
+    *n = 0;
+    if (cap < 1 || !rec_off) return fail(SEB_ERR_INVALID, "seb_wal_scan: offsets capacity 0");
+    uint64_t at = 0, cnt = 0;
+    rec_off[0] = 0;
+    while (at < bytes) {
+        if (bytes - at < 21) {
+            *n = cnt;
+            return fail(SEB_ERR_SHORT, "seb_wal_scan: truncated header at byte %llu", (unsigned long long)at);
+        }
+        uint32_t ks, vs;
+        memcpy(&ks, data + at + 12, 4);
+        memcpy(&vs, data + at + 16, 4);
+        const uint64_t len = 21ull + ks + vs;
+        if (bytes - at < len) {
+            *n = cnt;
+            return fail(SEB_ERR_SHORT, "seb_wal_scan: truncated record at byte %llu", (unsigned long long)at);
+        }
+        if (cnt + 2 > cap) {
+            *n = cnt;
+            return fail(SEB_ERR_INVALID, "seb_wal_scan: more than %llu records", (unsigned long long)(cap - 1));
+        }
+        at += len;
+        rec_off[++cnt] = at;
+    }
+    *n = cnt;
+    return SEB_OK;
+}

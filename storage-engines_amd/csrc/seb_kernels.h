@@ -62,6 +62,13 @@ struct RegLayout {          // slot index ranges per level (lookup order) + shap
     uint32_t nonoverlap;    // bit L: level L's files are disjoint and in MinKey order (bisection exact)
     uint32_t all_k7_m32;    // every filter has k == 7 and m < 2^32
 };
+// seb_codec.hip: shard routing (FNV-1a32) and WAL CRC32
+hipError_t launch_route(const KeyBatch &kb, uint32_t bits, uint16_t *shard, uint32_t *hash, hipStream_t s);
+uint64_t route_workspace_bytes(uint64_t n, uint32_t bits);
+hipError_t launch_route_partition(const KeyBatch &kb, uint32_t bits, uint32_t *perm, uint64_t *shard_begin,
+                                  uint16_t *shard_out, void *ws, uint64_t ws_bytes, hipStream_t s);
+hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mode, uint32_t *crc, uint8_t *ok,
+                          hipStream_t s);
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
                            const uint8_t *ranges, uint64_t *maybe, hipStream_t s);
 

@@ -135,3 +135,54 @@ def lsm_probe_indices(lay=LSM_LAYOUT):
     n = lay["probes"]
     r = rng.integers(0, lay["l1_files"] * lay["l1_keys"], n)
     return np.where(np.arange(n) % 2 == 0, 2 * r, 2 * r + 1)
+
+
+# ---- synthetic WAL image for the checksum config (bench.py --config wal)
+WAL_LAYOUT = {"records": 2_000_000, "value_size": 100, "delete_every": 16, "seed": 12345}
+
+
+def wal_image(n: int, value_size: int = 100, delete_every: int = 16, seal: bool = True):
+    """A WAL image of n records laid out as lsm/wal.go:31-62 Append writes them:
+    [crc32][seq u64][keySize u32][valueSize u32][deleted u8][key][value], little-endian.
+    Record i: key16(i), seq i+1; every delete_every-th record (i % delete_every == delete_every-1)
+    is a Delete (lsm/lsm.go:209: value nil, deleted 1), the rest carry value_size splitmix64
+    bytes (the reference benchmark's 100-B random values, common/benchmark/compare.go:37).
+    seal=True fills the CRC field with zlib.crc32(record[4:]) (= Go's crc32.ChecksumIEEE).
+    Returns (uint8 image, uint64 offsets[n+1])."""
+    import zlib
+    idx = np.arange(n, dtype=np.int64)
+    deleted = (idx % delete_every == delete_every - 1) if delete_every else np.zeros(n, bool)
+    vlen = np.where(deleted, 0, value_size).astype(np.int64)
+    rlen = 21 + 16 + vlen
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(rlen, out=off[1:])
+    img = np.zeros(int(off[-1]), np.uint8)
+    st = off[:-1].astype(np.int64)
+    seq = (idx + 1).astype("<u8").view(np.uint8).reshape(-1, 8)
+    for b in range(8):
+        img[st + 4 + b] = seq[:, b]
+    img[st + 12] = 16
+    vl = vlen.astype("<u4").view(np.uint8).reshape(-1, 4)
+    for b in range(4):
+        img[st + 16 + b] = vl[:, b]
+    img[st + 20] = deleted.astype(np.uint8)
+    keys = key16(idx)
+    for b in range(16):
+        img[st + 21 + b] = keys[:, b]
+    if value_size:
+        live = np.nonzero(~deleted)[0]
+        words = (value_size + 7) // 8
+        with np.errstate(over="ignore"):
+            seed = KEY_SEED ^ (live.astype(np.uint64) * PAYLOAD_MUL)
+        for w in range(words):
+            with np.errstate(over="ignore"):
+                wb = splitmix64(seed + _U64(w) * GOLDEN).astype("<u8").view(np.uint8).reshape(-1, 8)
+            for b in range(min(8, value_size - 8 * w)):
+                img[st[live] + 37 + 8 * w + b] = wb[:, b]
+    if seal:
+        mv = memoryview(img)
+        crc = np.fromiter((zlib.crc32(mv[int(s) + 4:int(e)]) for s, e in zip(off[:-1], off[1:])), np.uint32, n)
+        cb = crc.astype("<u4").view(np.uint8).reshape(-1, 4)
+        for b in range(4):
+            img[st + b] = cb[:, b]
+    return img, off

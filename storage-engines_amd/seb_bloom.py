@@ -99,7 +99,14 @@ _SIGS = {
     "seb_registry_slots": (_i, [_vp, C.POINTER(_u64), C.POINTER(C.c_int32), _u32]),
     "seb_registry_multiget": (_i, [_vp, C.POINTER(seb_keys), _vp]),
     "seb_registry_multiget_dev": (_i, [_vp, C.POINTER(seb_keys), _vp, _vp]),
+    "seb_dev_shard_route": (_i, [C.POINTER(seb_keys), _u32, _vp, _vp, _vp]),
+    "seb_dev_shard_partition_workspace_size": (_u64, [_u64, _u32]),
+    "seb_dev_shard_partition": (_i, [C.POINTER(seb_keys), _u32, _vp, _vp, _vp, _vp, _u64, _vp]),
+    "seb_dev_wal_crc": (_i, [_vp, _vp, _u64, _i, _vp, _vp, _vp]),
+    "seb_wal_scan": (_i, [_vp, _u64, _vp, _u64, C.POINTER(_u64)]),
 }
+
+WAL_CRC, WAL_SEAL, WAL_VERIFY = 0, 1, 2
 
 
 def build_library() -> str:
@@ -430,3 +437,49 @@ def new_words(m: int, device="cuda"):
 def words_to_bits(words, m: int) -> np.ndarray:
     """First ceil(m/8) bytes of a device word array = the reference's bits slice."""
     return words.cpu().numpy().view(np.uint8)[: (m + 7) // 8].copy()
+
+
+# ------------------------------------------------ shard routing + WAL checksums (§8(f) row 4)
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def dev_shard_route(keys: seb_keys, shard_bits: int, shard=None, hash=None, stream=None) -> None:
+    """shard[i] = FNV-1a32(key i) & (2^bits - 1) (hashindex/shard.go:47-52); hash[i] = the hash."""
+    check(lib().seb_dev_shard_route(C.byref(keys), shard_bits, _ptr(shard), _ptr(hash), _stream(stream)))
+
+
+def dev_shard_partition_workspace_size(n: int, shard_bits: int) -> int:
+    return lib().seb_dev_shard_partition_workspace_size(n, shard_bits)
+
+
+def dev_shard_partition(keys: seb_keys, shard_bits: int, perm, shard_begin=None, shard=None, ws=None,
+                        stream=None) -> None:
+    """Stable partition by shard (hashindex/shard.go:104-122): perm grouped by shard, input order
+    inside a shard; shard_begin (2^bits + 1 u64) delimits the groups."""
+    import torch
+    if ws is None:
+        ws = torch.empty(max(dev_shard_partition_workspace_size(keys.n, shard_bits), 1), dtype=torch.uint8,
+                         device=perm.device)
+    check(lib().seb_dev_shard_partition(C.byref(keys), shard_bits, _ptr(perm), _ptr(shard_begin), _ptr(shard),
+                                        ws.data_ptr(), ws.numel(), _stream(stream)))
+
+
+def dev_wal_crc(data, rec_off, mode: int = WAL_CRC, crc=None, ok=None, stream=None) -> None:
+    """CRC32-IEEE of WAL records data[rec_off[i]+4, rec_off[i+1]) (lsm/wal.go:59); SEAL stores it,
+    VERIFY sets ok[i] (framing + stored CRC, lsm/wal.go:123-133)."""
+    check(lib().seb_dev_wal_crc(data.data_ptr(), rec_off.data_ptr(), rec_off.numel() - 1, mode, _ptr(crc), _ptr(ok),
+                                _stream(stream)))
+
+
+def wal_scan(image: bytes | np.ndarray) -> tuple[np.ndarray, int]:
+    """ReadAll's framing walk (lsm/wal.go:98-121) on the host: (offsets[0..n], status)."""
+    buf = np.frombuffer(image, np.uint8) if isinstance(image, (bytes, bytearray)) else image
+    cap = buf.size // 21 + 2
+    off = np.zeros(cap, np.uint64)
+    n = _u64(0)
+    rc = lib().seb_wal_scan(buf.ctypes.data, buf.size, off.ctypes.data, cap, C.byref(n))
+    if rc not in (0, -5):
+        check(rc)
+    return off[: n.value + 1].copy(), rc

@@ -23,6 +23,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "storage-engines_amd"))
 
 from oracle import bloom_np as bn  # noqa: E402
+from oracle import codec_c as cc  # noqa: E402
 from oracle import oracle_c as oc  # noqa: E402
 import keygen as kg  # noqa: E402
 
@@ -164,7 +165,46 @@ def lsm_case(lay=kg.LSM_LAYOUT) -> dict:
             "mask_popcount": int(np.unpackbits(mask.astype("<u8").view(np.uint8)).sum())}
 
 
+def _fnv32a_np(keys: np.ndarray) -> np.ndarray:
+    """Vectorised FNV-1a 32 over fixed-width keys (second restatement, checks codec_oracle.c)."""
+    h = np.full(keys.shape[0], 0x811C9DC5, np.uint32)
+    with np.errstate(over="ignore"):
+        for b in range(keys.shape[1]):
+            h = (h ^ keys[:, b].astype(np.uint32)) * np.uint32(0x01000193)
+    return h
+
+
+def route_case(n: int = 10_000_000, bits: int = 8) -> dict:
+    """hashindex shard routing + stable partition of key16(0..n-1) (bench.py --config route)."""
+    keys = kg.key16(np.arange(n))
+    h = cc.fnv32a_batch(keys, n, stride=16)
+    assert np.array_equal(h, _fnv32a_np(keys))
+    shard = (h & ((1 << bits) - 1)).astype(np.uint16)
+    perm, begin = cc.partition(shard, bits)
+    assert np.array_equal(perm, np.argsort(shard, kind="stable"))
+    return {"n": n, "bits": bits, "hash_sha256": sha(h.astype("<u4").tobytes()),
+            "perm_sha256": sha(perm.astype("<u4").tobytes()), "begin_sha256": sha(begin.astype("<u8").tobytes())}
+
+
+def wal_case(lay=kg.WAL_LAYOUT) -> dict:
+    """WAL image of bench.py --config wal: every stored CRC (zlib) equals the oracle's CRC."""
+    img, off = kg.wal_image(lay["records"], lay["value_size"], lay["delete_every"])
+    crc, ok = cc.wal_crc(img, off)
+    assert ok.all()
+    return {"layout": lay, "bytes": int(img.size), "image_sha256": sha(img.tobytes()),
+            "crc_sha256": sha(crc.astype("<u4").tobytes())}
+
+
 def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--add":  # refresh only the named entries
+        with open(OUT) as f:
+            out = json.load(f)
+        for name in sys.argv[2].split(","):
+            out[name] = {"route": route_case, "wal": wal_case, "lsm": lsm_case, "c5": c5_case}[name]()
+            print(name, out[name], flush=True)
+        with open(OUT, "w") as f:
+            json.dump(out, f, indent=1)
+        return
     out: dict = {"generator": "tests/golden/gen_golden.py", "key_format": "key16(i) = b'user%010d' % i + "
                  "bytes([i & 0xff, (i + 1) & 0xff]) (common/benchmark/keygen.go:89-109)",
                  "probe_rule": "q even -> key(q) present; q odd -> key(n + q) absent"}
@@ -214,6 +254,8 @@ def main():
     out["multi"] = [multi_case(8, 10000, 160000, 0.01), multi_case(64, 2000, 256000, 0.01)]
     out["c5"] = c5_case()
     out["lsm"] = lsm_case()
+    out["route"] = route_case()
+    out["wal"] = wal_case()
     with open(OUT, "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", OUT)
