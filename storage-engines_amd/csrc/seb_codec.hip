@@ -4,8 +4,8 @@
 //       h := fnv.New32a(); h.Write([]byte(key)); shard = h.Sum32() & shardMask
 //     (hashindex/shard.go:47-52 getShard, and :104-122 where UpdateBatch distributes a whole batch
 //     of updates and deletions over the 256 shards).  k_route hashes a key batch with FNV-1a 32
-//     (offset 0x811c9dc5, prime 0x01000193); k_route_hist / k_route_scatter turn the shard ids
-//     into a stable partition (keys grouped by shard, input order inside a shard).
+//     (offset 0x811c9dc5, prime 0x01000193); k_route_tile / k_route_scan_rows / k_route_scatter
+//     turn a batch into a stable partition (keys grouped by shard, input order inside a shard).
 //  B  WAL record checksums.  A record is [crc32 u32][seq u64][keySize u32][valueSize u32]
 //     [deleted u8][key][value], crc = crc32.ChecksumIEEE(record[4:]) (lsm/wal.go:31-62 Append;
 //     ReadAll re-checks it at :123-133).  k_wal_crc computes the CRC of many records at once,
@@ -75,22 +75,32 @@ __global__ __launch_bounds__(256) void k_route(KeyBatch kb, uint32_t mask, uint1
     }
 }
 
-// ---- stable partition by shard: per-tile histograms (bin-major), a two-level exclusive scan,
-// then a scatter that ranks equal shards in input order with wave ballots (no LDS atomics on the
-// ranking path, so the permutation is deterministic).
+// ---- stable partition by shard (keys grouped by shard, input order inside a shard), three launches:
+//   k_route_tile       hash a 4096-key tile, write its shard ids, per-tile histogram (bin-major)
+//   k_route_scan_rows  per bin: exclusive prefix of its row of tile counts, row total
+//   k_route_scatter    every workgroup scans the bin totals itself (<= 4096 values), then each wave
+//                      ranks its own contiguous 1024 keys: pass 1 counts per (wave, bin), pass 2
+//                      places keys, equal shards ordered by __ballot peer masks (one ballot per shard
+//                      bit).  No atomic decides a position, so the permutation is deterministic.
 constexpr uint32_t kRouteThreads = 256;
-constexpr uint32_t kRouteTile = 4096;  // keys per tile: 16 rounds of 256
+constexpr uint32_t kRouteWaves = kRouteThreads / 64;
+constexpr uint32_t kRoutePerLane = 16;
+constexpr uint32_t kRouteTile = kRouteThreads * kRoutePerLane;  // 4096 keys
 constexpr uint32_t kRouteMaxBits = 12;
 
-__global__ __launch_bounds__(kRouteThreads) void k_route_hist(const uint16_t *__restrict__ shard, uint64_t n,
-                                                              uint32_t nbins, uint32_t ntiles,
+__global__ __launch_bounds__(kRouteThreads) void k_route_tile(KeyBatch kb, uint32_t mask, uint32_t nbins,
+                                                              uint32_t ntiles, uint16_t *__restrict__ shard,
                                                               uint32_t *__restrict__ counts) {
     extern __shared__ uint32_t hist[];
     for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) hist[b] = 0u;
     __syncthreads();
     const uint64_t t0 = (uint64_t)blockIdx.x * kRouteTile;
-    const uint64_t t1 = t0 + kRouteTile < n ? t0 + kRouteTile : n;
-    for (uint64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) atomicAdd(&hist[shard[i]], 1u);
+    const uint64_t t1 = t0 + kRouteTile < kb.n ? t0 + kRouteTile : kb.n;
+    for (uint64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+        const uint32_t sh = route_hash(kb, i) & mask;
+        shard[i] = (uint16_t)sh;
+        atomicAdd(&hist[sh], 1u);
+    }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) counts[(uint64_t)b * ntiles + blockIdx.x] = hist[b];
 }
@@ -125,72 +135,96 @@ __global__ __launch_bounds__(1024) void k_route_scan_rows(uint32_t *__restrict__
     if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
-// Exclusive scan of the nbins (<= 4096) bin totals in one workgroup; shard_begin[nbins] = n.
-__global__ __launch_bounds__(1024) void k_route_scan_bins(const uint32_t *__restrict__ totals, uint32_t nbins,
-                                                          uint32_t *__restrict__ bin_base,
-                                                          uint64_t *__restrict__ shard_begin) {
-    __shared__ uint32_t v[4096];
-    for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) v[b] = totals[b];
-    __syncthreads();
-    if (threadIdx.x == 0) {  // <= 4096 adds
-        uint64_t run = 0;
-        for (uint32_t b = 0; b < nbins; ++b) {
-            const uint32_t c = v[b];
-            bin_base[b] = (uint32_t)run;
-            if (shard_begin) shard_begin[b] = run;
-            run += c;
-        }
-        if (shard_begin) shard_begin[nbins] = run;
+// Lanes of this wave holding the same shard as this lane (live lanes only).
+__device__ __forceinline__ uint64_t shard_peers(bool live, uint32_t s, uint32_t bits) {
+    uint64_t peers = __ballot(live);
+    for (uint32_t b = 0; b < bits; ++b) {
+        const uint64_t on = __ballot(live && ((s >> b) & 1u));
+        peers &= ((s >> b) & 1u) ? on : ~on;
     }
+    return peers;
 }
 
+// LDS: wrun[kRouteWaves][nbins] | wsum[kRouteWaves]
 __global__ __launch_bounds__(kRouteThreads) void k_route_scatter(const uint16_t *__restrict__ shard, uint64_t n,
                                                                  uint32_t nbins, uint32_t bits, uint32_t ntiles,
                                                                  const uint32_t *__restrict__ counts,
-                                                                 const uint32_t *__restrict__ bin_base,
+                                                                 const uint32_t *__restrict__ totals,
+                                                                 uint64_t *__restrict__ shard_begin,
                                                                  uint32_t *__restrict__ perm) {
     extern __shared__ uint32_t smem[];
-    uint32_t *run = smem;                 // [nbins]  next output slot of each bin for this tile
-    uint32_t *wcnt = smem + nbins;        // [4][nbins] per-wave counts of the current round
-    constexpr uint32_t kWaves = kRouteThreads / 64;
-    for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) {
-        run[b] = bin_base[b] + counts[(uint64_t)b * ntiles + blockIdx.x];
-        for (uint32_t w = 0; w < kWaves; ++w) wcnt[w * nbins + b] = 0u;
+    uint32_t *wrun = smem;                         // [wave][bin]
+    uint32_t *wsum = smem + kRouteWaves * nbins;   // [wave]
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // 1. bin bases: exclusive scan of the bin totals, thread t owns bins [t*per, (t+1)*per)
+    const uint32_t per = (nbins + kRouteThreads - 1) / kRouteThreads;
+    const uint32_t b0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t j = 0; j < per; ++j)
+        if (b0 + j < nbins) sum += totals[b0 + j];
+    uint32_t v = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v += y;
+    }
+    if (lane == 63) wsum[wid] = v;
+    for (uint32_t w = 0; w < kRouteWaves; ++w)
+        for (uint32_t j = threadIdx.x; j < nbins; j += kRouteThreads) wrun[w * nbins + j] = 0u;
+    __syncthreads();
+    uint32_t run = v - sum;
+    for (uint32_t w = 0; w < wid; ++w) run += wsum[w];
+    // run = first output slot of bin b0; this tile's slots in bin b start at base_b + row prefix
+    uint32_t tile_base[16];
+    for (uint32_t j = 0; j < per; ++j)
+        if (b0 + j < nbins) {
+            const uint32_t c = totals[b0 + j];
+            if (blockIdx.x == 0 && shard_begin) shard_begin[b0 + j] = run;
+            tile_base[j] = run + counts[(uint64_t)(b0 + j) * ntiles + blockIdx.x];
+            run += c;
+        }
+    if (blockIdx.x == 0 && shard_begin && threadIdx.x == kRouteThreads - 1) shard_begin[nbins] = n;
+    // 2. pass 1: per-(wave, bin) counts of this wave's 1024 contiguous keys
+    const uint64_t w0 = (uint64_t)blockIdx.x * kRouteTile + (uint64_t)wid * 64 * kRoutePerLane;
+    uint32_t sv[kRoutePerLane];
+#pragma unroll
+    for (uint32_t r = 0; r < kRoutePerLane; ++r) {
+        const uint64_t i = w0 + (uint64_t)r * 64 + lane;
+        sv[r] = i < n ? shard[i] : 0xffffffffu;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kRoutePerLane; ++r) {
+        const bool live = sv[r] != 0xffffffffu;
+        const uint64_t peers = shard_peers(live, sv[r], bits);
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        if (live && (peers & lt) == 0ull) wrun[wid * nbins + sv[r]] += (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
-    const uint64_t t0 = (uint64_t)blockIdx.x * kRouteTile;
-    const uint64_t t1 = t0 + kRouteTile < n ? t0 + kRouteTile : n;
-    for (uint64_t r0 = t0; r0 < t1; r0 += blockDim.x) {
-        const uint64_t i = r0 + threadIdx.x;
-        const bool live = i < t1;
-        const uint32_t s = live ? shard[i] : 0u;
-        // lanes of this wave with the same shard (8-12 ballots, one per shard bit)
-        uint64_t peers = __ballot(live);
-        for (uint32_t b = 0; b < bits; ++b) {
-            const uint64_t on = __ballot(live && ((s >> b) & 1u));
-            peers &= ((s >> b) & 1u) ? on : ~on;
-        }
-        const uint32_t rank = (uint32_t)__popcll(peers & lt);
-        const bool leader = live && (peers & lt) == 0ull;
-        if (leader) wcnt[wid * nbins + s] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (live) {
-            uint32_t before = run[s];
-            for (uint32_t w = 0; w < wid; ++w) before += wcnt[w * nbins + s];
-            perm[before + rank] = (uint32_t)i;
-        }
-        __syncthreads();
-        for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) {
-            uint32_t add = 0;
-            for (uint32_t w = 0; w < kWaves; ++w) {
-                add += wcnt[w * nbins + b];
-                wcnt[w * nbins + b] = 0u;
+    // 3. wave bases per bin: tile base + the counts of the waves before
+    for (uint32_t j = 0; j < per; ++j)
+        if (b0 + j < nbins) {
+            uint32_t acc = tile_base[j];
+            for (uint32_t w = 0; w < kRouteWaves; ++w) {
+                const uint32_t c = wrun[w * nbins + b0 + j];
+                wrun[w * nbins + b0 + j] = acc;
+                acc += c;
             }
-            run[b] += add;
         }
-        __syncthreads();
+    __syncthreads();
+    // 4. pass 2: place; the group leader advances the wave's cursor after every lane has read it
+#pragma unroll
+    for (uint32_t r = 0; r < kRoutePerLane; ++r) {
+        const bool live = sv[r] != 0xffffffffu;
+        const uint64_t peers = shard_peers(live, sv[r], bits);
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        uint32_t at = 0;
+        if (live) at = wrun[wid * nbins + sv[r]];
+        __builtin_amdgcn_wave_barrier();
+        if (live) {
+            perm[at + (uint32_t)__popcll(peers & lt)] = (uint32_t)(w0 + (uint64_t)r * 64 + lane);
+            if ((peers & lt) == 0ull) wrun[wid * nbins + sv[r]] = at + (uint32_t)__popcll(peers);
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -198,7 +232,7 @@ uint64_t route_workspace_bytes(uint64_t n, uint32_t bits) {
     const uint64_t ntiles = (n + kRouteTile - 1) / kRouteTile;
     const uint64_t nbins = 1ull << bits;
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-    return al(n * 2) + al(nbins * ntiles * 4) + al(nbins * 4) * 2;
+    return al(n * 2) + al(nbins * ntiles * 4) + al(nbins * 4);
 }
 
 hipError_t launch_route(const KeyBatch &kb, uint32_t bits, uint16_t *shard, uint32_t *hash, hipStream_t s) {
@@ -226,18 +260,14 @@ hipError_t launch_route_partition(const KeyBatch &kb, uint32_t bits, uint32_t *p
     uint16_t *shard = (uint16_t *)w;
     uint32_t *counts = (uint32_t *)(w + al(kb.n * 2));
     uint32_t *totals = (uint32_t *)(w + al(kb.n * 2) + al((uint64_t)nbins * ntiles * 4));
-    uint32_t *bin_base = totals + al((uint64_t)nbins * 4) / 4;
-    hipError_t e = launch_route(kb, bits, shard, nullptr, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_route_hist, dim3(ntiles), dim3(kRouteThreads), nbins * sizeof(uint32_t), s, shard, kb.n,
-                       nbins, ntiles, counts);
+    hipLaunchKernelGGL(k_route_tile, dim3(ntiles), dim3(kRouteThreads), nbins * sizeof(uint32_t), s, kb,
+                       nbins - 1, nbins, ntiles, shard, counts);
     hipLaunchKernelGGL(k_route_scan_rows, dim3(nbins), dim3(1024), 0, s, counts, ntiles, totals);
-    hipLaunchKernelGGL(k_route_scan_bins, dim3(1), dim3(1024), 0, s, totals, nbins, bin_base, shard_begin);
-    const size_t lds = (size_t)nbins * (1 + kRouteThreads / 64) * sizeof(uint32_t);
+    const size_t lds = ((size_t)kRouteWaves * nbins + kRouteWaves) * sizeof(uint32_t);
     hipLaunchKernelGGL(k_route_scatter, dim3(ntiles), dim3(kRouteThreads), lds, s, shard, kb.n, nbins, bits, ntiles,
-                       counts, bin_base, perm);
+                       counts, totals, shard_begin, perm);
     if (shard_out) {
-        e = hipMemcpyAsync(shard_out, shard, kb.n * 2, hipMemcpyDeviceToDevice, s);
+        hipError_t e = hipMemcpyAsync(shard_out, shard, kb.n * 2, hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) return e;
     }
     return hipGetLastError();
@@ -287,45 +317,100 @@ __device__ __forceinline__ uint32_t ld_u32_le(const uint8_t *p) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+__device__ __forceinline__ void wal_finish(uint8_t *data, uint64_t s, uint64_t len, uint32_t crc, int mode,
+                                           uint32_t ks, uint32_t vs, uint32_t stored, uint64_t i,
+                                           uint32_t *crc_out, uint8_t *ok) {
+    if (crc_out) crc_out[i] = crc;
+    if (mode == 1 && len >= 4) {
+        data[s] = (uint8_t)crc;
+        data[s + 1] = (uint8_t)(crc >> 8);
+        data[s + 2] = (uint8_t)(crc >> 16);
+        data[s + 3] = (uint8_t)(crc >> 24);
+    } else if (mode == 2) {
+        ok[i] = (len >= 21 && 21ull + ks + vs == len && stored == crc) ? 1 : 0;
+    }
+}
+
 // mode 0: crc[i] = ChecksumIEEE(record i [4:]); mode 1: also store it into the record's first 4
 // bytes (Append's sealing); mode 2: ok[i] = framing holds (len >= 21, 21 + keySize + valueSize ==
 // len) and the stored CRC matches (ReadAll's check).  Records i = data[off[i], off[i+1]).
-__global__ __launch_bounds__(256) void k_wal_crc(uint8_t *__restrict__ data, const uint64_t *__restrict__ off,
-                                                 uint64_t n, int mode, uint32_t *__restrict__ crc_out,
-                                                 uint8_t *__restrict__ ok) {
+//
+// A workgroup owns kWalRecs consecutive records.  Their byte span is copied into LDS with
+// coalesced 16-B loads (one lane per record would otherwise make every wave-wide load touch 64
+// different cache lines), and each lane then runs the table CRC over its record from LDS, four
+// bytes per step through a funnel shift of two aligned LDS dwords.  A span larger than the LDS
+// window is checksummed straight from HBM.
+constexpr uint32_t kWalRecs = 256;
+constexpr uint32_t kWalLds = 48 * 1024;
+
+__global__ __launch_bounds__(kWalRecs) void k_wal_crc(uint8_t *__restrict__ data, const uint64_t *__restrict__ off,
+                                                      uint64_t n, int mode, uint32_t *__restrict__ crc_out,
+                                                      uint8_t *__restrict__ ok) {
     __shared__ uint32_t tab[4][256];
+    __shared__ uint4 stage[kWalLds / 16 + 1];
     for (uint32_t j = threadIdx.x; j < 1024; j += blockDim.x) (&tab[0][0])[j] = (&kCrcTab.t[0][0])[j];
+    const uint64_t r0 = (uint64_t)blockIdx.x * kWalRecs;
+    const uint64_t r1 = r0 + kWalRecs < n ? r0 + kWalRecs : n;
+    const uintptr_t base = ((uintptr_t)(data + off[r0])) & ~(uintptr_t)15;
+    const uintptr_t end = (uintptr_t)(data + off[r1]);
+    const bool staged = end - base <= kWalLds;
+    if (staged) {
+        const uint32_t chunks = (uint32_t)((end - base + 15) >> 4);
+        const uint4 *src = (const uint4 *)base;
+        for (uint32_t c = threadIdx.x; c < chunks; c += blockDim.x) stage[c] = src[c];
+    }
     __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t s = off[i], e = off[i + 1];
-        const uint64_t len = e > s ? e - s : 0;
-        uint32_t crc = 0u;
-        if (len >= 4) crc = ~crc_range(~0u, data, s + 4, e, tab);
-        else crc = 0u;  // no payload to checksum (an invalid record)
-        if (crc_out) crc_out[i] = crc;
-        if (mode == 1 && len >= 4) {
-            data[s] = (uint8_t)crc;
-            data[s + 1] = (uint8_t)(crc >> 8);
-            data[s + 2] = (uint8_t)(crc >> 16);
-            data[s + 3] = (uint8_t)(crc >> 24);
-        } else if (mode == 2) {
-            bool good = len >= 21;
-            if (good) {
-                const uint64_t ks = ld_u32_le(data + s + 12), vs = ld_u32_le(data + s + 16);
-                good = 21 + ks + vs == len && ld_u32_le(data + s) == crc;
+    const uint64_t i = r0 + threadIdx.x;
+    if (i >= r1) return;
+    const uint64_t s = off[i], e = off[i + 1];
+    const uint64_t len = e > s ? e - s : 0;
+    uint32_t crc = 0u, ks = 0u, vs = 0u, stored = 0u;
+    if (staged) {
+        const uint8_t *lb = (const uint8_t *)stage;
+        const uint32_t b = (uint32_t)((uintptr_t)(data + s) - base);
+        if (len >= 4) {
+            const uint32_t *lw = (const uint32_t *)stage;
+            const uint32_t p = b + 4, L = (uint32_t)len - 4, sh = p & 3u;
+            uint32_t wi = p >> 2, cur = lw[wi], c = ~0u;
+            for (uint32_t j = 0; j + 4 <= L; j += 4) {
+                const uint32_t nxt = lw[++wi];
+                c = crc_word(c, __builtin_amdgcn_alignbyte(nxt, cur, sh), tab);
+                cur = nxt;
             }
-            ok[i] = good ? 1 : 0;
+            const uint32_t r = L & 3u;
+            if (r) {
+                const uint32_t w = __builtin_amdgcn_alignbyte(lw[wi + 1], cur, sh);
+                for (uint32_t j = 0; j < r; ++j) c = crc_byte(c, (w >> (8 * j)) & 0xffu, tab);
+            }
+            crc = ~c;
+            stored = (uint32_t)lb[b] | ((uint32_t)lb[b + 1] << 8) | ((uint32_t)lb[b + 2] << 16) |
+                     ((uint32_t)lb[b + 3] << 24);
+        }
+        if (len >= 21) {
+            ks = (uint32_t)lb[b + 12] | ((uint32_t)lb[b + 13] << 8) | ((uint32_t)lb[b + 14] << 16) |
+                 ((uint32_t)lb[b + 15] << 24);
+            vs = (uint32_t)lb[b + 16] | ((uint32_t)lb[b + 17] << 8) | ((uint32_t)lb[b + 18] << 16) |
+                 ((uint32_t)lb[b + 19] << 24);
+        }
+    } else {
+        if (len >= 4) {
+            crc = ~crc_range(~0u, data, s + 4, e, tab);
+            stored = ld_u32_le(data + s);
+        }
+        if (len >= 21) {
+            ks = ld_u32_le(data + s + 12);
+            vs = ld_u32_le(data + s + 16);
         }
     }
+    wal_finish(data, s, len, crc, mode, ks, vs, stored, i, crc_out, ok);
 }
 
 hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mode, uint32_t *crc, uint8_t *ok,
                           hipStream_t s) {
     if (n == 0) return hipSuccess;
-    uint64_t g = (n + 255) / 256;
-    if (g > 65536) g = 65536;
-    hipLaunchKernelGGL(k_wal_crc, dim3((unsigned)g), dim3(256), 0, s, data, off, n, mode, crc, ok);
+    const uint64_t g = (n + kWalRecs - 1) / kWalRecs;
+    if (g >= (1ull << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_wal_crc, dim3((unsigned)g), dim3(kWalRecs), 0, s, data, off, n, mode, crc, ok);
     return hipGetLastError();
 }
 
