@@ -27,9 +27,14 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STEP_KERNELS = {
-    "build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned", "k_hash_varlen"),
-    "probe": ("k_probe", "k_hash_varlen"),
+STEP_KERNELS = {  # per config: timed step name -> kernels launched by that step
+    "c2c3": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned"), "probe": ("k_probe",)},
+    "c4": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned", "k_hash_varlen"),
+           "probe": ("k_probe", "k_hash_varlen")},
+    "c5": {"probe": ("k_probe_interleaved", "k_interleave", "k_probe_multi")},
+    "lsm": {"probe": ("k_multiget",)},
+    "route": {"route": ("k_route_tile", "k_route_scan_rows", "k_route_scatter")},
+    "wal": {"wal_verify": ("k_wal_crc",)},
 }
 
 
@@ -37,7 +42,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
     ap.add_argument("--config", default="c2c3")
-    ap.add_argument("--key-bytes", type=float, default=16.0 * 10_000_000)
+    ap.add_argument("--key-bytes", type=float, default=16.0 * 10_000_000,
+                    help="bytes of the 16-B-per-lane stream (keys; the WAL image for --config wal)")
     ap.add_argument("--out-tag", default=None)
     a = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
@@ -57,11 +63,11 @@ def main():
             w.writerow([k, c, f"{v:.6g}", cnt])
     mean = {(k, c): v for k, c, v, _ in rows}
     steps = {}
-    for step, pats in STEP_KERNELS.items():
+    for step, pats in STEP_KERNELS[a.config].items():
         fetch = write = 0.0
         kernels = []
         for (k, c), v in mean.items():
-            if any(p in k for p in pats) and "seb::" in k or (step == "build" and "fillBufferAligned" in k):
+            if any(p in k for p in pats) and ("seb::" in k or "fillBufferAligned" in k):
                 if c == "FETCH_SIZE":
                     fetch += v
                     kernels.append(k)
