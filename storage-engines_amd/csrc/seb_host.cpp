@@ -104,7 +104,7 @@ static void load_env() {
     if (env_flag("SEB_STREAM_NT", &v)) o.stream_nt = (int)v;
     if (env_flag("SEB_SCATTER_KPT", &v)) o.scatter_kpt = (int)v;
     if (env_flag("SEB_PROBE_PERSISTENT", &v)) o.probe_persistent = (int)v;
-    if (env_flag("SEB_PROBE_MODE", &v) && v >= 0 && v <= 4) o.probe_mode = (int)v;
+    if (env_flag("SEB_PROBE_MODE", &v) && v >= 0 && v <= 7) o.probe_mode = (int)v;
     if (env_flag("SEB_WAL_LDS_KIB", &v) && (v == 36 || v == 48)) o.wal_lds_kib = (int)v;
     if (env_flag("SEB_VARLEN_SORT_MIN_KEYS", &v) && v >= 0) o.varlen_sort_min_keys = (uint64_t)v;
     if (env_flag("SEB_VARLEN_PREHASH_MIN_KEYS", &v) && v >= 0) o.varlen_prehash_min_keys = (uint64_t)v;
@@ -119,7 +119,7 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     Options &o = options();
     if (!strcmp(name, "build_algo") && value >= 0 && value <= 2) o.build_algo = (int)value;
     else if (!strcmp(name, "probe_split") && (value == 0 || value == 2 || value == 3)) o.probe_split = (int)value;
-    else if (!strcmp(name, "probe_kpt") && (value == 1 || value == 2 || value == 4)) o.probe_kpt = (int)value;
+    else if (!strcmp(name, "probe_kpt") && (value == 1 || value == 2 || value == 4 || value == 6 || value == 8)) o.probe_kpt = (int)value;
     else if (!strcmp(name, "probe_slice_shift") && value >= 0 && value <= 26) o.probe_slice_shift = (int)value;
     else if (!strcmp(name, "probe_slice_grid") && value >= 0) o.probe_slice_grid = (unsigned)value;
     else if (!strcmp(name, "multi_interleave") && (value == 0 || value == 1)) o.multi_interleave = (int)value;
@@ -127,7 +127,7 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     else if (!strcmp(name, "stream_nt") && (value == 0 || value == 1)) o.stream_nt = (int)value;
     else if (!strcmp(name, "scatter_kpt") && (value == 4 || value == 5)) o.scatter_kpt = (int)value;
     else if (!strcmp(name, "probe_persistent") && value >= 0 && value <= 65536) o.probe_persistent = (int)value;
-    else if (!strcmp(name, "probe_mode") && value >= 0 && value <= 4) o.probe_mode = (int)value;
+    else if (!strcmp(name, "probe_mode") && value >= 0 && value <= 7) o.probe_mode = (int)value;
     else if (!strcmp(name, "wal_lds_kib") && (value == 36 || value == 48)) o.wal_lds_kib = (int)value;
     else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;

@@ -88,7 +88,7 @@ struct Options {
     int stream_nt = 1;            // non-temporal loads for 16-B key batches (keeps filter lines in L2)
     int probe_persistent = 0;     // sliced probe: persistent 1024-thread workgroups, barrier per slice (0 = off)
     int wal_lds_kib = 36;         // WAL CRC: LDS staging window per 256-record workgroup (36 or 48)
-    int probe_mode = 0;           // sliced probe gather order (k_probe_sliced MODE 0-4)
+    int probe_mode = 0;           // sliced probe gather order (k_probe_sliced MODE 0-6; 7 = k_probe_compact)
     unsigned grid_cap = 1u << 20;
 };
 Options &options();

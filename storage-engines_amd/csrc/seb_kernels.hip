@@ -109,6 +109,10 @@ __global__ __launch_bounds__(256) void k_probe(Src src, uint64_t n, const uint32
 //   3  per slice without the liveness test (every position gathered once, all independent).
 //   4  no slices: positions sorted ascending, gathered in that order with mode 0's early exit, so
 //      a workgroup generation sweeps the filter low to high without per-slice tests.
+//   5  mode 0's gathers and early exit (the same gathers are issued), ordered position-major
+//      across the thread's KPT keys: the KPT gathers of one position step are independent, so a
+//      wave keeps up to KPT gathers in flight instead of one.
+//   6  mode 4 (sorted, no slices) ordered position-major across the KPT keys like mode 5.
 template <int KPT>
 __device__ __forceinline__ void sort7(uint32_t (&p)[KPT][7], int r) {
     constexpr int net[16][2] = {{0, 6}, {2, 3}, {4, 5}, {0, 2}, {1, 4}, {3, 6}, {0, 1}, {2, 5},
@@ -144,6 +148,35 @@ __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, const
 #pragma unroll
                 for (int q = 0; q < 7; ++q)
                     if (acc[r] & 1u) acc[r] &= words[pos[r][q] >> 5] >> (pos[r][q] & 31);
+            }
+        } else if constexpr (MODE == 5) {
+            for (uint32_t sl = 0; sl < nslices; ++sl) {
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    uint32_t v[KPT];
+#pragma unroll
+                    for (int r = 0; r < KPT; ++r) {
+                        const uint32_t w = pos[r][q] >> 5;
+                        v[r] = ~0u;
+                        if ((acc[r] & 1u) && (w >> slice_shift) == sl) v[r] = words[w];
+                    }
+#pragma unroll
+                    for (int r = 0; r < KPT; ++r) acc[r] &= v[r] >> (pos[r][q] & 31);
+                }
+            }
+        } else if constexpr (MODE == 6) {
+#pragma unroll
+            for (int r = 0; r < KPT; ++r) sort7<KPT>(pos, r);
+#pragma unroll
+            for (int q = 0; q < 7; ++q) {
+                uint32_t v[KPT];
+#pragma unroll
+                for (int r = 0; r < KPT; ++r) {
+                    v[r] = ~0u;
+                    if (acc[r] & 1u) v[r] = words[pos[r][q] >> 5];
+                }
+#pragma unroll
+                for (int r = 0; r < KPT; ++r) acc[r] &= v[r] >> (pos[r][q] & 31);
             }
         } else if constexpr (MODE == 2) {
 #pragma unroll
@@ -191,6 +224,76 @@ __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, const
         for (int r = 0; r < KPT; ++r) {
             const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
             if (i < n) out[src.index(i)] = (uint8_t)(acc[r] & 1u);
+        }
+    }
+}
+
+// Compact sliced probe (MODE 7; k == 7, m < 2^32).  The sliced probe's L2 reuse grows with the
+// number of keys an XCD has in flight during one sweep over the slices, and holding 7 positions per
+// key in registers caps that (68 VGPRs at 2 keys per thread).  Here a key costs 4 registers: its
+// first residue r0, the two negated step addends (nb = m - b, nd = m - ((b - c) mod m)) and a word
+// of flags (bit i = the u64 sum h1 + i*h2 wrapped at step i; bit 0 = no clear bit seen yet).  Each
+// slice phase regenerates the 7 residues with 3 VALU ops per step (for_positions' recurrence) and
+// gathers, position-major across the thread's KPT keys, only the words that lie in the slice for
+// keys still alive: the same gathers and early exit as MODE 0, with KPT independent gathers per
+// step in flight.
+template <typename Src, int KPT>
+__global__ __launch_bounds__(256) void k_probe_compact(Src src, uint64_t n, const uint32_t *__restrict__ words,
+                                                       ModArg md, uint8_t *__restrict__ out, uint32_t slice_shift,
+                                                       uint32_t nslices) {
+    const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
+    const uint64_t span = (uint64_t)blockDim.x * KPT;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
+        uint32_t r0[KPT], nb[KPT], nd[KPT], fl[KPT];
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            uint64_t h1 = 0, h2 = 0;
+            if (i < n) src.hash(i, h1, h2);
+            r0[r] = (uint32_t)mod64(h1, md.m, md.mu);
+            const uint32_t b = (uint32_t)mod64(h2, md.m, md.mu);
+            const uint32_t bc = b >= c ? b - c : b + (m - c);
+            nb[r] = m - b;
+            nd[r] = m - bc;
+            uint32_t f = i < n ? 1u : 0u;
+            uint64_t x = h1;
+#pragma unroll
+            for (uint32_t q = 1; q < 7; ++q) {
+                const uint64_t xn = x + h2;
+                f |= (xn < x ? 1u : 0u) << q;
+                x = xn;
+            }
+            fl[r] = f;
+        }
+        const uint32_t wshift = slice_shift + 5;  // residue -> slice
+        for (uint32_t sl = 0; sl < nslices; ++sl) {
+            uint32_t rc[KPT];
+#pragma unroll
+            for (int r = 0; r < KPT; ++r) rc[r] = r0[r];
+#pragma unroll
+            for (int q = 0; q < 7; ++q) {
+                if (q > 0) {
+#pragma unroll
+                    for (int r = 0; r < KPT; ++r) {
+                        const uint32_t na = (fl[r] >> q) & 1u ? nd[r] : nb[r];
+                        const uint32_t t = rc[r] - na;
+                        rc[r] = rc[r] >= na ? t : t + m;
+                    }
+                }
+                uint32_t v[KPT];
+#pragma unroll
+                for (int r = 0; r < KPT; ++r) {
+                    v[r] = ~0u;
+                    if ((fl[r] & 1u) && (rc[r] >> wshift) == sl) v[r] = words[rc[r] >> 5];
+                }
+#pragma unroll
+                for (int r = 0; r < KPT; ++r) fl[r] &= ~1u | (v[r] >> (rc[r] & 31));
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            if (i < n) out[src.index(i)] = (uint8_t)(fl[r] & 1u);
         }
     }
 }
@@ -422,10 +525,27 @@ static hipError_t launch_sliced_t(const Src &src, uint64_t n, const uint32_t *wo
             hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 3>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
                                nslices);
             break;
+        case 5:
+            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 5>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
+                               nslices);
+            break;
+        case 6:
+            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 6>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
+                               nslices);
+            break;
         default:
             hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 0>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
                                nslices);
     }
+    return hipGetLastError();
+}
+
+template <typename Src, int KPT>
+static hipError_t launch_compact_t(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
+                                   uint32_t shift, uint32_t nslices, hipStream_t s) {
+    const Options &o = options();
+    unsigned g = grid_for((n + KPT - 1) / KPT, 256, o.probe_slice_grid ? o.probe_slice_grid : o.grid_cap);
+    hipLaunchKernelGGL((k_probe_compact<Src, KPT>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift, nslices);
     return hipGetLastError();
 }
 
@@ -437,6 +557,14 @@ static hipError_t launch_probe7(const Src &src, uint64_t n, const uint32_t *word
     if constexpr (M32) {
         if (o.probe_slice_shift > 0 && (nwords >> o.probe_slice_shift) > 0) {  // filter spans > 1 slice
             const uint32_t nsl = (uint32_t)((nwords + (1ull << o.probe_slice_shift) - 1) >> o.probe_slice_shift);
+            if (o.probe_mode == 7) {
+                switch (o.probe_kpt) {
+                    case 2: return launch_compact_t<Src, 2>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
+                    case 6: return launch_compact_t<Src, 6>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
+                    case 8: return launch_compact_t<Src, 8>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
+                    default: return launch_compact_t<Src, 4>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
+                }
+            }
             switch (o.probe_kpt) {
                 case 1: return launch_sliced_t<Src, 1>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
                 case 4: return launch_sliced_t<Src, 4>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
