@@ -370,32 +370,48 @@ def main():
             return None
         return dist.broadcast(st.broadcast_bufs[j % 2], src=0, async_op=True)
 
+    # Launch-duration timers: HIP events created without the system-scope completion fence
+    # (seb.Timer); a torch.cuda.Event flushes L2 when it completes, ~15 us per record between two
+    # kernels, which would both slow the step and perturb the kernel it brackets.  Each record
+    # still costs a few us of command-processor time between two kernels, so adjacent boundaries
+    # share one timer: a step's end is the next step's start, and with nothing between build and
+    # probe (no broadcast to wait for, one stream) the build's end is the probe's start.
+    shared = not overlap and st.broadcast_bufs is None
+    prev_end = [None]
+    pool = [seb.Timer() for _ in range(4 * args.steps + 1)]  # created before the timed region
+
+    def mark(stream):
+        t = pool.pop()
+        t.record(stream)
+        return t
+
     def step(j, pending, record):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
         nxt = broadcast(j + 1)  # the next batch rides xGMI while this step computes
+        b_end = None
         if st.build is not None:
             with torch.cuda.stream(sb):
                 if overlap:
                     sb.wait_event(probed[j % 2])  # probe j-2 is done with this filter buffer
-                if record:
-                    ev[0].record(sb)
+                b_start = (prev_end[0] if shared and prev_end[0] is not None else mark(sb)) if record else None
                 st.build(j)
                 if record:
-                    ev[1].record(sb)
-                built[j % 2].record(sb)
+                    b_end = mark(sb)
+                    times["build"].append((b_start, b_end))
+                if overlap:
+                    built[j % 2].record(sb)
             if overlap:
                 sp.wait_event(built[j % 2])
         if pending is not None:
             pending.wait()
         if record:
-            ev[2].record(sp)
+            p_start = b_end if shared and b_end is not None else \
+                (prev_end[0] if shared and prev_end[0] is not None else mark(sp))
         st.probe(j)
         if record:
-            ev[3].record(sp)
-            if st.build is not None:
-                times["build"].append((ev[0], ev[1]))
-            times["probe"].append((ev[2], ev[3]))
-        probed[j % 2].record(sp)
+            prev_end[0] = mark(sp)
+            times["probe"].append((p_start, prev_end[0]))
+        if overlap:
+            probed[j % 2].record(sp)
         return nxt
 
     pending = broadcast(0)
@@ -422,7 +438,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kern_ms = {(st.probe_name if name == "probe" else name): float(np.mean([a.elapsed_time(b) for a, b in pairs]))
+    kern_ms = {(st.probe_name if name == "probe" else name): float(np.mean([a.elapsed_ms(b) for a, b in pairs]))
                for name, pairs in times.items() if pairs}
     value = st.units_per_step * args.steps / elapsed / 1e6
     result = None

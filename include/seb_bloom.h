@@ -127,6 +127,13 @@ int seb_host_free(void *ptr);
 int seb_memcpy_h2d(void *dst, const void *src, uint64_t bytes, void *stream);
 int seb_memcpy_d2h(void *dst, const void *src, uint64_t bytes, void *stream);
 int seb_stream_sync(void *stream);
+/* Timing events created with hipEventDisableSystemFence: a default event's completion fence
+ * writes back and invalidates L2 (~15 us between two kernels on gfx950).  elapsed waits for
+ * `end`; use only for timing, not to order host reads after device writes. */
+int seb_timer_create(void **event);
+int seb_timer_record(void *event, void *stream);
+int seb_timer_elapsed_ms(void *start, void *end, float *ms);
+int seb_timer_destroy(void *event);
 
 /* ------------------------------------------- host-buffer batched entry points ------------ */
 /* Keys and bits in host memory: H2D, kernels and D2H on the context's streams, synchronous.

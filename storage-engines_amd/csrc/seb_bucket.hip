@@ -89,10 +89,26 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, Mo
     const uint64_t t1 = t0 + tile_keys < n ? t0 + tile_keys : n;
     const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;  // <= 8 buckets per thread in the scan
 
+    constexpr int KP = KFIX > 0 ? KPT7 : 1;
+    constexpr int KQ = KFIX > 0 ? KFIX : 1;
+    // 16-B sources: the keys of round j+1 are loaded while round j sorts and writes (the whole
+    // workgroup passes each barrier together, so a load issued at a round's start would stall
+    // every wave of the CU at once).
+    constexpr bool kPre = KFIX > 0 && SplitLoad<Src>::value;
+    uint4 kv[kPre ? KP : 1];
+    auto prefetch = [&](uint64_t r0) {
+        if constexpr (kPre) {
+            const uint64_t r1 = r0 + round_keys < t1 ? r0 + round_keys : t1;
+#pragma unroll
+            for (int r = 0; r < KP; ++r) {
+                const uint64_t i = r0 + (uint64_t)r * blockDim.x + threadIdx.x;
+                if (i < r1) kv[r] = src.load(i);
+            }
+        }
+    };
+    prefetch(t0);
     for (uint64_t k0 = t0; k0 < t1; k0 += round_keys) {
         const uint64_t k1 = k0 + round_keys < t1 ? k0 + round_keys : t1;
-        constexpr int KP = KFIX > 0 ? KPT7 : 1;
-        constexpr int KQ = KFIX > 0 ? KFIX : 1;
         uint32_t pos[KP][KQ];
         if constexpr (KFIX > 0) {  // positions stay in registers between counting and placing
 #pragma unroll
@@ -100,12 +116,16 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, Mo
                 const uint64_t i = k0 + (uint64_t)r * blockDim.x + threadIdx.x;
                 if (i < k1) {
                     uint64_t h1, h2;
-                    src.hash(i, h1, h2);
+                    if constexpr (kPre)
+                        Src::hash_raw(kv[r], h1, h2);
+                    else
+                        src.hash(i, h1, h2);
                     for_positions<KFIX, true>(h1, h2, md, KFIX, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
 #pragma unroll
                     for (int q = 0; q < KQ; ++q) atomicAdd(&cursor[pos[r][q] >> kBktShift], 1u);
                 }
             }
+            if (k1 < t1) prefetch(k1);
         } else {
             for (uint64_t i = k0 + threadIdx.x; i < k1; i += blockDim.x) {
                 uint64_t h1, h2;

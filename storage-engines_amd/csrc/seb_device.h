@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "seb_kernels.h"
 
 namespace seb {
@@ -41,33 +43,37 @@ __device__ __forceinline__ void fnv_word_part(uint32_t w, uint32_t lo, uint32_t 
 }
 
 // Key sources.  Each provides hash(i, h1, h2) for key i.
+__device__ __forceinline__ void fnv_key16(const uint4 v, uint64_t &h1, uint64_t &h2) {
+    h1 = kFnvOffset;
+    h2 = kFnvOffset;
+    fnv_word(v.x, h1, h2);
+    fnv_word(v.y, h1, h2);
+    fnv_word(v.z, h1, h2);
+    fnv_word(v.w, h1, h2);
+}
+
+// Sources with kSplit = true also expose load(i) -> uint4 and hash_raw(raw, h1, h2), so a kernel
+// can issue the loads of its next batch of keys before it hashes them (software prefetch).
 struct Keys16 {  // fixed 16-B keys, 16-B aligned: one dwordx4 per lane, 1 KiB per wave, coalesced
+    static constexpr bool kSplit = true;
     const uint4 *p;
     __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
-    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
-        uint4 v = p[i];
-        h1 = kFnvOffset;
-        h2 = kFnvOffset;
-        fnv_word(v.x, h1, h2);
-        fnv_word(v.y, h1, h2);
-        fnv_word(v.z, h1, h2);
-        fnv_word(v.w, h1, h2);
-    }
+    __device__ __forceinline__ uint4 load(uint64_t i) const { return p[i]; }
+    __device__ __forceinline__ static void hash_raw(const uint4 v, uint64_t &h1, uint64_t &h2) { fnv_key16(v, h1, h2); }
+    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const { fnv_key16(p[i], h1, h2); }
 };
 
 struct Keys16NT {  // Keys16 with non-temporal loads: the streamed batch does not evict filter lines from L2
+    static constexpr bool kSplit = true;
     const uint4 *p;
     __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
-    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
+    __device__ __forceinline__ uint4 load(uint64_t i) const {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(p + i));
-        h1 = kFnvOffset;
-        h2 = kFnvOffset;
-        fnv_word(v.x, h1, h2);
-        fnv_word(v.y, h1, h2);
-        fnv_word(v.z, h1, h2);
-        fnv_word(v.w, h1, h2);
+        return make_uint4(v.x, v.y, v.z, v.w);
     }
+    __device__ __forceinline__ static void hash_raw(const uint4 v, uint64_t &h1, uint64_t &h2) { fnv_key16(v, h1, h2); }
+    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const { fnv_key16(load(i), h1, h2); }
 };
 
 struct KeysStrideW {  // fixed stride, multiple of 4 bytes, 4-B aligned
@@ -134,14 +140,21 @@ struct KeysVarPerm {  // variable length, processed in length-bucketed order: i-
 };
 
 struct KeysHashed {  // pre-hashed batch (k_hash_varlen): one coalesced 16-B load per key
+    static constexpr bool kSplit = true;
     const uint4 *h;
     __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
-    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
-        const uint4 v = h[i];
+    __device__ __forceinline__ uint4 load(uint64_t i) const { return h[i]; }
+    __device__ __forceinline__ static void hash_raw(const uint4 v, uint64_t &h1, uint64_t &h2) {
         h1 = (uint64_t)v.x | ((uint64_t)v.y << 32);
         h2 = (uint64_t)v.z | ((uint64_t)v.w << 32);
     }
+    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const { hash_raw(h[i], h1, h2); }
 };
+
+template <typename S, typename = void>
+struct SplitLoad { static constexpr bool value = false; };
+template <typename S>
+struct SplitLoad<S, std::void_t<decltype(S::kSplit)>> { static constexpr bool value = S::kSplit; };
 
 // --------------------------------------------------------------- positions -----------------
 

@@ -456,6 +456,34 @@ extern "C" int seb_stream_sync(void *stream) {
     return SEB_OK;
 }
 
+// Timing events without the system-scope fence a default HIP event performs when it completes:
+// that fence writes back and invalidates L2 and costs ~15 us between two kernels on gfx950
+// (profiles/r02_event_gaps), which would inflate the very step it measures.
+extern "C" int seb_timer_create(void **ev) {
+    if (!ev) return fail(SEB_ERR_INVALID, "seb_timer_create: null");
+    hipEvent_t e;
+    HIP_OR_FAIL(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    *ev = (void *)e;
+    return SEB_OK;
+}
+
+extern "C" int seb_timer_record(void *ev, void *stream) {
+    HIP_OR_FAIL(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream));
+    return SEB_OK;
+}
+
+extern "C" int seb_timer_elapsed_ms(void *start, void *end, float *ms) {
+    if (!ms) return fail(SEB_ERR_INVALID, "seb_timer_elapsed_ms: null");
+    HIP_OR_FAIL(hipEventSynchronize((hipEvent_t)end));
+    HIP_OR_FAIL(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end));
+    return SEB_OK;
+}
+
+extern "C" int seb_timer_destroy(void *ev) {
+    if (ev) HIP_OR_FAIL(hipEventDestroy((hipEvent_t)ev));
+    return SEB_OK;
+}
+
 // ------------------------------------------------------- contexts (host-buffer API) ----------
 
 struct DevBuf {

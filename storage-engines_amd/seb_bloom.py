@@ -104,6 +104,10 @@ _SIGS = {
     "seb_dev_shard_partition": (_i, [C.POINTER(seb_keys), _u32, _vp, _vp, _vp, _vp, _u64, _vp]),
     "seb_dev_wal_crc": (_i, [_vp, _vp, _u64, _i, _vp, _vp, _vp]),
     "seb_wal_scan": (_i, [_vp, _u64, _vp, _u64, C.POINTER(_u64)]),
+    "seb_timer_create": (_i, [C.POINTER(_vp)]),
+    "seb_timer_record": (_i, [_vp, _vp]),
+    "seb_timer_elapsed_ms": (_i, [_vp, _vp, C.POINTER(C.c_float)]),
+    "seb_timer_destroy": (_i, [_vp]),
 }
 
 WAL_CRC, WAL_SEAL, WAL_VERIFY = 0, 1, 2
@@ -380,6 +384,28 @@ def _stream(stream=None) -> int:
     import torch
     s = torch.cuda.current_stream() if stream is None else stream
     return s.cuda_stream
+
+
+class Timer:
+    """A HIP timing event without the system-scope completion fence (seb_timer_*): recording it
+    between two kernels does not flush L2 the way torch.cuda.Event does."""
+
+    def __init__(self):
+        self._e = _vp()
+        check(lib().seb_timer_create(C.byref(self._e)))
+
+    def record(self, stream=None) -> None:
+        check(lib().seb_timer_record(self._e, _stream(stream)))
+
+    def elapsed_ms(self, end: "Timer") -> float:
+        ms = C.c_float()
+        check(lib().seb_timer_elapsed_ms(self._e, end._e, C.byref(ms)))
+        return ms.value
+
+    def __del__(self):
+        if getattr(self, "_e", None) and _lib is not None:
+            _lib.seb_timer_destroy(self._e)
+            self._e = None
 
 
 def dev_keys(data, offsets=None, n: int | None = None, stride: int = 16) -> seb_keys:

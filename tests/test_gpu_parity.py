@@ -224,6 +224,33 @@ def test_c2_c3_10m_device_resident(seb, golden, torch_cuda, build_algo):
     assert np.array_equal(ans[:200000], oc.probe(bits, m, k, kg.key16(sl), 200000, stride=16))
 
 
+def test_sliced_probe_gather_orders(seb, golden, torch_cuda):
+    """Every gather order of the sliced probe (k_probe_sliced modes 0-6, k_probe_compact = mode 7)
+    and keys-per-thread choice gives the C3 answers bit for bit, also for a ragged batch whose
+    last workgroup is partly empty."""
+    torch = torch_cuda
+    row = next(r for r in golden["fixed16"] if r["n"] == 10_000_000)
+    n, m, k = row["n"], row["m"], row["k"]
+    kd = seb.dev_keys(to_dev(torch, kg.key16(np.arange(n))), n=n, stride=16)
+    words, bits = dev_build_bits(seb, torch, kd, m, k)
+    pk = to_dev(torch, kg.key16(kg.probe_indices(n)))
+    ragged = 999_983
+    ref_ragged = oc.probe(bits, m, k, kg.key16(kg.probe_indices(n)[:ragged]), ragged, stride=16)
+    cases = [(mode, kpt) for mode in range(7) for kpt in (1, 2, 4)] + [(7, kpt) for kpt in (2, 4, 6, 8)]
+    for mode, kpt in cases:
+        with seb.option("probe_mode", mode), seb.option("probe_kpt", kpt), seb.option("probe_slice_shift", 19):
+            out = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+            seb.dev_probe(seb.dev_keys(pk, n=n, stride=16), words, m, k, out)
+            torch.cuda.synchronize()
+            assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"], (mode, kpt)
+            outr = torch.full((ragged + 1,), 7, dtype=torch.uint8, device="cuda")
+            seb.dev_probe(seb.dev_keys(pk[:ragged], n=ragged, stride=16), words, m, k, outr)
+            torch.cuda.synchronize()
+            got = outr.cpu().numpy()
+            assert np.array_equal(got[:ragged], ref_ragged), (mode, kpt)
+            assert got[ragged] == 7, (mode, kpt)  # nothing written past the batch
+
+
 @pytest.mark.parametrize("n", [1000, 100000, 1000000])
 def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
     torch = torch_cuda
