@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--bcast", default="packed", choices=["packed", "keys"],
+                    help="c2c3, N > 1: broadcast 8-B packed residues (hashed once on rank 0) or the 16-B keys")
     ap.add_argument("--overlap", type=int, default=0,
                     help="c2c3/c4: build step j+1 (second filter buffer, own stream) while step j probes")
     for o in OPTIONS:
@@ -83,6 +85,8 @@ class Setup:
     build = None
     build_host = probe_host = None
     broadcast_bufs = None
+    pre_broadcast = None  # rank 0: prepares broadcast buffer j % 2 for batch j
+    pmc_key = None        # profiles/pmc_r01.json entry whose per-launch traffic applies (None: config name)
 
 
 def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
@@ -104,9 +108,22 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
     nb = (m + 7) // 8
     st.kernel_bytes = {"build": 16.0 * n + 2 * nb, "probe": 16.0 * n + nb + n}
     st.units_per_step = 2.0 * n * world
-    st.broadcast_bufs = st.pbufs if world > 1 else None
+    # N > 1: every rank's filter has the same (m, k) (one SSTable size), so rank 0 hashes the batch
+    # once into 8-byte packed residues and broadcasts those: 80 MB per step over xGMI instead of
+    # 160 MB of keys.  Every rank still tests all 10M keys against its own filter.
+    packed = world > 1 and args.bcast == "packed" and k == 7 and m < (1 << 29)
     st.workload = ("C2+C3: per GPU build one filter from 10M x 16B keys @1% FPR (m=95,850,584, k=7) "
                    "+ probe a 10M-key batch (50% present) RCCL-broadcast from rank 0")
+    if packed:
+        st.packed = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(2)]
+        st.broadcast_bufs = st.packed
+        st.kernel_bytes["probe"] = 8.0 * n + nb + n
+        st.workload += " as 8-B packed residues (hashed once on rank 0)"
+        st.pmc_key = "c2c3_packed"
+        if rank == 0:
+            st.pre_broadcast = lambda j: seb.dev_pack_residues(st.pk[j % 2], m, k, st.packed[j % 2])
+    else:
+        st.broadcast_bufs = st.pbufs if world > 1 else None
     st.parallelism = f"filter-per-gpu x{world}, probe batch broadcast (RCCL)"
 
     def build(j):
@@ -115,7 +132,10 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
         seb.dev_build(st.kb, w, m, k)
 
     def probe(j):
-        seb.dev_probe(st.pk[j % 2], st.wbufs[j % len(st.wbufs)], m, k, st.out)
+        if packed:
+            seb.dev_probe_packed(st.packed[j % 2], n, st.wbufs[j % len(st.wbufs)], m, k, st.out)
+        else:
+            seb.dev_probe(st.pk[j % 2], st.wbufs[j % len(st.wbufs)], m, k, st.out)
 
     def parity(j):
         if n != 10_000_000 or rank != 0:
@@ -368,6 +388,8 @@ def main():
     def broadcast(j):
         if st.broadcast_bufs is None:
             return None
+        if st.pre_broadcast is not None:
+            st.pre_broadcast(j)  # on the compute stream; the collective waits for it
         return dist.broadcast(st.broadcast_bufs[j % 2], src=0, async_op=True)
 
     # Launch-duration timers: HIP events created without the system-scope completion fence
@@ -449,7 +471,7 @@ def main():
         pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
-                traffic = json.load(f).get(args.config, {}).get(dom, {}).get("hbm_bytes_per_launch")
+                traffic = json.load(f).get(st.pmc_key or args.config, {}).get(dom, {}).get("hbm_bytes_per_launch")
         ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
         result = {
             "metric": METRIC if args.config in ("c2c3", "c4", "c5", "lsm") else f"{args.config} {st.unit}",

@@ -107,6 +107,16 @@ int seb_dev_build_ws(const seb_keys *keys, uint32_t *words, uint64_t num_bits, u
 /* out[i] = MayContain(key i) as 0/1 bytes (bloom.go:82-92; Go []bool layout). */
 int seb_dev_probe(const seb_keys *keys, const uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
                   uint8_t *out, void *stream);
+/* Packed residues, for one probe batch shared by several filters of the same (num_bits, num_hashes)
+ * (multi-GPU: hash once on the root, broadcast 8 bytes per key instead of the key).  Requires
+ * num_hashes == 7 and num_bits < 2^29.  packed[i] = r0 | b << 29 | carries << 58 with
+ * r0 = hash1 mod m, b = hash2 mod m and bit q-1 of carries set when hash1 + q*hash2 wraps 2^64 at
+ * step q (q = 1..6); seb_dev_probe_packed gives the answers seb_dev_probe gives for the keys
+ * (MayContain of lsm/bloom.go:82-92). */
+int seb_dev_pack_residues(const seb_keys *keys, uint64_t num_bits, uint32_t num_hashes, uint64_t *packed,
+                          void *stream);
+int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, uint64_t num_bits,
+                         uint32_t num_hashes, uint8_t *out, void *stream);
 /* Multi-filter probe: bit f of mask[i] = MayContain of filters[f] on key i.  mask_bytes is the
  * width of one mask element (1, 2, 4 or 8) and must cover num_filters bits (<= 64). `filters`
  * is a HOST array whose .bits are device word arrays. */

@@ -334,6 +334,39 @@ extern "C" int seb_dev_probe(const seb_keys *keys, const uint32_t *words, uint64
     return probe_dispatch(key_batch(keys), words, mod_arg(m, k), out, (hipStream_t)stream);
 }
 
+// Packed residues: one 8-byte word per key (r0, b, carry flags) for k == 7 and m < 2^29.
+static int check_packed_args(uint64_t m, uint32_t k, const char *who) {
+    int rc = check_filter_args(m, k, who);
+    if (rc) return rc;
+    if (k != 7 || m >= (1ull << kPackBits))
+        return fail(SEB_ERR_INVALID, "%s: packed residues need k == 7 and m < 2^%u (k=%u m=%llu)", who, kPackBits, k,
+                    (unsigned long long)m);
+    return SEB_OK;
+}
+
+extern "C" int seb_dev_pack_residues(const seb_keys *keys, uint64_t m, uint32_t k, uint64_t *packed, void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc;
+    if ((rc = check_keys(keys, "seb_dev_pack_residues")) || (rc = check_packed_args(m, k, "seb_dev_pack_residues")))
+        return rc;
+    if (!packed && keys->n) return fail(SEB_ERR_INVALID, "seb_dev_pack_residues: null packed");
+    KeyBatch kb = key_batch(keys);
+    void *ws;
+    if ((rc = prepare_probe_keys(kb, (hipStream_t)stream, 0, &ws))) return rc;
+    HIP_OR_FAIL(launch_pack_residues(kb, mod_arg(m, k), packed, (hipStream_t)stream));
+    return SEB_OK;
+}
+
+extern "C" int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, uint64_t m, uint32_t k,
+                                    uint8_t *out, void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc = check_packed_args(m, k, "seb_dev_probe_packed");
+    if (rc) return rc;
+    if (n && (!packed || !words || !out)) return fail(SEB_ERR_INVALID, "seb_dev_probe_packed: null pointer");
+    HIP_OR_FAIL(launch_probe_packed(packed, n, words, mod_arg(m, k), out, (hipStream_t)stream));
+    return SEB_OK;
+}
+
 static int fill_multi(const seb_filter_ref *filters, uint32_t nf, uint32_t mask_bytes, MultiArg *ma,
                       const char *who) {
     if (!filters || nf == 0) return fail(SEB_ERR_INVALID, "%s: no filters", who);

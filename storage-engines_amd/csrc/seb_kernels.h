@@ -118,4 +118,10 @@ hipError_t launch_probe_interleaved(const KeyBatch &kb, const MultiArg &ma, void
                                     hipStream_t s);
 hipError_t launch_build_many_lds(const KeyBatch &kb, const ManyArg &ma, uint32_t lds_bytes, hipStream_t s);
 
+// Packed residues (k == 7, m < 2^kPackBits): 8 bytes per key instead of the key itself.
+constexpr uint32_t kPackBits = 29;
+hipError_t launch_pack_residues(const KeyBatch &kb, const ModArg &md, uint64_t *packed, hipStream_t s);
+hipError_t launch_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
+                               uint8_t *out, hipStream_t s);
+
 }  // namespace seb

@@ -298,6 +298,76 @@ __global__ __launch_bounds__(256) void k_probe_compact(Src src, uint64_t n, cons
     }
 }
 
+// ---- packed residues: a probe batch shared by several filters of one size (the filters of one
+// SSTable size on different GPUs, compaction outputs) is hashed once into 8 bytes per key and the
+// packed words travel instead of the keys (half the bytes of a 16-B key over xGMI).  Layout
+// (kPackBits = 29, so m < 2^29): bits 0-28 r0 = h1 mod m, 29-57 b = h2 mod m, 58-63 bit q-1 =
+// "the u64 sum h1 + q*h2 wrapped at step q" for q = 1..6.  Positions follow for_positions'
+// recurrence, so they are exactly (h1 + q*h2 mod 2^64) mod m of lsm/bloom.go:64.
+template <typename Src>
+__global__ __launch_bounds__(256) void k_pack_residues(Src src, uint64_t n, ModArg md, uint64_t *__restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t h1, h2;
+        src.hash(i, h1, h2);
+        const uint64_t r0 = mod64(h1, md.m, md.mu), b = mod64(h2, md.m, md.mu);
+        uint64_t f = 0, x = h1;
+#pragma unroll
+        for (uint32_t q = 1; q < 7; ++q) {
+            const uint64_t xn = x + h2;
+            f |= (uint64_t)(xn < x) << (q - 1);
+            x = xn;
+        }
+        out[src.index(i)] = r0 | (b << kPackBits) | (f << (2 * kPackBits));
+    }
+}
+
+// Sliced probe (MODE 0 gather order) over packed residues; k == 7.
+template <int KPT>
+__global__ __launch_bounds__(256) void k_probe_packed(const uint64_t *__restrict__ packed, uint64_t n,
+                                                      const uint32_t *__restrict__ words, ModArg md,
+                                                      uint8_t *__restrict__ out, uint32_t slice_shift,
+                                                      uint32_t nslices) {
+    const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
+    constexpr uint64_t kMask = (1ull << kPackBits) - 1;
+    const uint64_t span = (uint64_t)blockDim.x * KPT;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
+        uint32_t pos[KPT][7];
+        uint32_t acc[KPT];
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            const uint64_t v = i < n ? __builtin_nontemporal_load(packed + i) : 0ull;
+            uint32_t x = (uint32_t)(v & kMask);
+            const uint32_t b = (uint32_t)((v >> kPackBits) & kMask), f = (uint32_t)(v >> (2 * kPackBits));
+            const uint32_t nb = m - b, bc = b >= c ? b - c : b + (m - c), nd = m - bc;
+            pos[r][0] = x;
+#pragma unroll
+            for (int q = 1; q < 7; ++q) {
+                const uint32_t na = (f >> (q - 1)) & 1u ? nd : nb;
+                const uint32_t t = x - na;
+                x = x >= na ? t : t + m;
+                pos[r][q] = x;
+            }
+            acc[r] = i < n ? 1u : 0u;
+        }
+        for (uint32_t sl = 0; sl < nslices; ++sl) {
+#pragma unroll
+            for (int r = 0; r < KPT; ++r)
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    const uint32_t w = pos[r][q] >> 5;
+                    if ((acc[r] & 1u) && (w >> slice_shift) == sl) acc[r] &= words[w] >> (pos[r][q] & 31);
+                }
+        }
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            if (i < n) out[i] = (uint8_t)(acc[r] & 1u);
+        }
+    }
+}
+
 // Persistent variant of the sliced probe: `gridDim.x` 1024-thread workgroups loop over batches of
 // 1024*KPT keys and finish each slice phase with a workgroup barrier, so all 16 waves of a CU's
 // workgroup gather from one slice at a time (workgroups on one XCD start together and do equal
@@ -697,6 +767,28 @@ hipError_t launch_build_many_lds(const KeyBatch &kb, const ManyArg &ma, uint32_t
         if (m32) return k7 ? go(k_build_many_lds<S, 7, true>) : go(k_build_many_lds<S, 0, true>);
         return k7 ? go(k_build_many_lds<S, 7, false>) : go(k_build_many_lds<S, 0, false>);
     });
+}
+
+hipError_t launch_pack_residues(const KeyBatch &kb, const ModArg &md, uint64_t *packed, hipStream_t s) {
+    if (kb.n == 0) return hipSuccess;
+    return with_src(kb, [&](auto src) {
+        using S = decltype(src);
+        hipLaunchKernelGGL(k_pack_residues<S>, dim3(grid_for(kb.n, 256, options().grid_cap)), dim3(256), 0, s, src,
+                           kb.n, md, packed);
+        return hipGetLastError();
+    });
+}
+
+hipError_t launch_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
+                               uint8_t *out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const Options &o = options();
+    const uint64_t nwords = (md.m + 31) / 32;
+    const uint32_t shift = o.probe_slice_shift > 0 ? (uint32_t)o.probe_slice_shift : 31u;
+    const uint32_t nsl = shift >= 31 ? 1u : (uint32_t)((nwords + (1ull << shift) - 1) >> shift);
+    const unsigned g = grid_for((n + 1) / 2, 256, o.probe_slice_grid ? o.probe_slice_grid : o.grid_cap);
+    hipLaunchKernelGGL(k_probe_packed<2>, dim3(g), dim3(256), 0, s, packed, n, words, md, out, shift, nsl);
+    return hipGetLastError();
 }
 
 }  // namespace seb

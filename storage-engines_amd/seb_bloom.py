@@ -104,6 +104,8 @@ _SIGS = {
     "seb_dev_shard_partition": (_i, [C.POINTER(seb_keys), _u32, _vp, _vp, _vp, _vp, _u64, _vp]),
     "seb_dev_wal_crc": (_i, [_vp, _vp, _u64, _i, _vp, _vp, _vp]),
     "seb_wal_scan": (_i, [_vp, _u64, _vp, _u64, C.POINTER(_u64)]),
+    "seb_dev_pack_residues": (_i, [C.POINTER(seb_keys), _u64, _u32, _vp, _vp]),
+    "seb_dev_probe_packed": (_i, [_vp, _u64, _vp, _u64, _u32, _vp, _vp]),
     "seb_timer_create": (_i, [C.POINTER(_vp)]),
     "seb_timer_record": (_i, [_vp, _vp]),
     "seb_timer_elapsed_ms": (_i, [_vp, _vp, C.POINTER(C.c_float)]),
@@ -439,6 +441,15 @@ def dev_build_ws(keys: seb_keys, words, m: int, k: int, ws, stream=None) -> None
 
 def dev_probe(keys: seb_keys, words, m: int, k: int, out, stream=None) -> None:
     check(lib().seb_dev_probe(C.byref(keys), words.data_ptr(), m, k, out.data_ptr(), _stream(stream)))
+
+
+def dev_pack_residues(keys: seb_keys, m: int, k: int, packed, stream=None) -> None:
+    """8-byte packed residues per key (k == 7, m < 2^29) for a batch shared by same-size filters."""
+    check(lib().seb_dev_pack_residues(C.byref(keys), m, k, packed.data_ptr(), _stream(stream)))
+
+
+def dev_probe_packed(packed, n: int, words, m: int, k: int, out, stream=None) -> None:
+    check(lib().seb_dev_probe_packed(packed.data_ptr(), n, words.data_ptr(), m, k, out.data_ptr(), _stream(stream)))
 
 
 def dev_probe_multi(keys: seb_keys, filters: list[tuple[object, int, int]], mask, stream=None) -> None:

@@ -251,6 +251,63 @@ def test_sliced_probe_gather_orders(seb, golden, torch_cuda):
             assert got[ragged] == 7, (mode, kpt)  # nothing written past the batch
 
 
+def unpack_positions(packed: np.ndarray, m: int) -> np.ndarray:
+    """Test-side decoding of seb_dev_pack_residues' words into the 7 positions (the recurrence
+    of for_positions, in Python integers)."""
+    mask = (1 << 29) - 1
+    c = (1 << 64) % m
+    out = np.zeros((packed.size, 7), np.uint64)
+    for j, v in enumerate(int(x) for x in packed):
+        r, b, f = v & mask, (v >> 29) & mask, v >> 58
+        out[j, 0] = r
+        for q in range(1, 7):
+            r = (r + b - (c if (f >> (q - 1)) & 1 else 0)) % m
+            out[j, q] = r
+    return out
+
+
+def test_packed_residues(seb, golden, torch_cuda):
+    """Packed residues (the multi-GPU broadcast form): positions equal the oracle's
+    (h1 + i*h2 mod 2^64) mod m, and probing them gives the C3 answers bit for bit, for fixed 16-B
+    and variable-length batches; unsupported (k, m) are rejected."""
+    torch = torch_cuda
+    row = next(r for r in golden["fixed16"] if r["n"] == 10_000_000)
+    n, m, k = row["n"], row["m"], row["k"]
+    kd = seb.dev_keys(to_dev(torch, kg.key16(np.arange(n))), n=n, stride=16)
+    words, bits = dev_build_bits(seb, torch, kd, m, k)
+    pidx = kg.probe_indices(n)
+    pk = seb.dev_keys(to_dev(torch, kg.key16(pidx)), n=n, stride=16)
+    packed = torch.zeros(n, dtype=torch.int64, device="cuda")
+    seb.dev_pack_residues(pk, m, k, packed)
+    out = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    seb.dev_probe_packed(packed, n, words, m, k, out)
+    torch.cuda.synchronize()
+    assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
+    host = packed.cpu().numpy().view(np.uint64)
+    sample = np.r_[0:2000, n - 2000:n]
+    want = np.array([oc.positions(kg.key16_bytes(int(i)), m, k) for i in pidx[sample]], np.uint64)
+    assert np.array_equal(unpack_positions(host[sample], m), want)
+    # ragged tail and a variable-length batch against the oracle
+    nv = 50001
+    data, off = kg.varlen_keys(np.arange(nv))
+    mv, kv = oc.params(nv, 0.01)
+    vkd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
+    vwords, vbits = dev_build_bits(seb, torch, vkd, mv, kv)
+    pdata, poff = kg.varlen_keys(kg.probe_indices(nv))
+    vpk = seb.dev_keys(to_dev(torch, pdata), to_dev(torch, poff))
+    vpacked = torch.zeros(nv, dtype=torch.int64, device="cuda")
+    seb.dev_pack_residues(vpk, mv, kv, vpacked)
+    vout = torch.full((nv + 1,), 7, dtype=torch.uint8, device="cuda")
+    seb.dev_probe_packed(vpacked, nv, vwords, mv, kv, vout)
+    torch.cuda.synchronize()
+    got = vout.cpu().numpy()
+    assert np.array_equal(got[:nv], oc.probe(vbits, mv, kv, pdata, nv, offsets=poff))
+    assert got[nv] == 7
+    for bad_m, bad_k in ((1 << 29, 7), (m, 6)):
+        with pytest.raises(seb.SebError):
+            seb.dev_pack_residues(pk, bad_m, bad_k, packed)
+
+
 @pytest.mark.parametrize("n", [1000, 100000, 1000000])
 def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
     torch = torch_cuda
