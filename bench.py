@@ -6,8 +6,10 @@
 c2c3 (default, the metric's config): one step on every GPU = clear + build one SSTable filter
 from 10M x 16-B keys @1% FPR (BASELINE C2; m = 95,850,584, k = 7) and probe a 10M-key batch
 against it (C3, 50% present).  Rank g builds the filter of its own SSTable (keys key16(g*n + i));
-the probe batch arrives on rank 0 and is RCCL-broadcast to every GPU, double-buffered so the
-broadcast of batch j+1 overlaps step j.  Per-GPU work is fixed as N grows (weak scaling); value =
+the probe batch arrives on rank 0 and is RCCL-broadcast to every GPU ahead of the step that
+probes it, so the transfer overlaps compute.  Since every rank's filter has the same (m, k), the
+batch travels as 8-byte packed residues that rank 0's own probe emits (--bcast packed, default;
+--bcast keys sends the 16-B keys).  Per-GPU work is fixed as N grows (weak scaling); value =
 (build + probe keys over all ranks) / max-over-ranks wall time, inputs already resident in HBM.
 c4: the same with variable-length keys (8-256 B, zipf); no broadcast.
 c5: 64 compaction-sized filters (100K keys each) sharded over the ranks, a 10M-key batch
@@ -85,7 +87,8 @@ class Setup:
     build = None
     build_host = probe_host = None
     broadcast_bufs = None
-    pre_broadcast = None  # rank 0: prepares broadcast buffer j % 2 for batch j
+    bcast_lead = 1        # batch j + lead is broadcast during step j (buffers: lead + 1)
+    bcast_prologue = None # rank 0, before the loop: fill broadcast buffer b for batch b < lead
     pmc_key = None        # profiles/pmc_r01.json entry whose per-launch traffic applies (None: config name)
 
 
@@ -108,20 +111,22 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
     nb = (m + 7) // 8
     st.kernel_bytes = {"build": 16.0 * n + 2 * nb, "probe": 16.0 * n + nb + n}
     st.units_per_step = 2.0 * n * world
-    # N > 1: every rank's filter has the same (m, k) (one SSTable size), so rank 0 hashes the batch
-    # once into 8-byte packed residues and broadcasts those: 80 MB per step over xGMI instead of
-    # 160 MB of keys.  Every rank still tests all 10M keys against its own filter.
+    # N > 1: every rank's filter has the same (m, k) (one SSTable size), so the batch travels as
+    # 8-byte packed residues instead of 16-byte keys (80 MB per step over xGMI instead of 160 MB).
+    # Rank 0 produces them inside its own probe of the keys (seb_dev_probe_emit_packed), two
+    # batches ahead, and broadcasts them right after; the other ranks probe the packed words.
+    # Every rank still tests all 10M keys against its own filter in every step.
     packed = world > 1 and args.bcast == "packed" and k == 7 and m < (1 << 29)
     st.workload = ("C2+C3: per GPU build one filter from 10M x 16B keys @1% FPR (m=95,850,584, k=7) "
                    "+ probe a 10M-key batch (50% present) RCCL-broadcast from rank 0")
     if packed:
-        st.packed = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(2)]
+        st.bcast_lead = 2
+        st.packed = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(st.bcast_lead + 1)]
         st.broadcast_bufs = st.packed
-        st.kernel_bytes["probe"] = 8.0 * n + nb + n
-        st.workload += " as 8-B packed residues (hashed once on rank 0)"
+        st.kernel_bytes["probe"] = (16.0 * n + 8.0 * n if rank == 0 else 8.0 * n) + nb + n
+        st.workload += " as 8-B packed residues (hashed once, inside rank 0's probe)"
         st.pmc_key = "c2c3_packed"
-        if rank == 0:
-            st.pre_broadcast = lambda j: seb.dev_pack_residues(st.pk[j % 2], m, k, st.packed[j % 2])
+        st.bcast_prologue = lambda b: seb.dev_pack_residues(st.pk[0], m, k, st.packed[b])
     else:
         st.broadcast_bufs = st.pbufs if world > 1 else None
     st.parallelism = f"filter-per-gpu x{world}, probe batch broadcast (RCCL)"
@@ -132,10 +137,13 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
         seb.dev_build(st.kb, w, m, k)
 
     def probe(j):
-        if packed:
-            seb.dev_probe_packed(st.packed[j % 2], n, st.wbufs[j % len(st.wbufs)], m, k, st.out)
+        w = st.wbufs[j % len(st.wbufs)]
+        if packed and rank == 0:  # answers batch j + 2's keys and emits its packed form
+            seb.dev_probe_emit_packed(st.pk[0], w, m, k, st.out, st.packed[(j + 2) % 3])
+        elif packed:
+            seb.dev_probe_packed(st.packed[j % 3], n, w, m, k, st.out)
         else:
-            seb.dev_probe(st.pk[j % 2], st.wbufs[j % len(st.wbufs)], m, k, st.out)
+            seb.dev_probe(st.pk[j % 2], w, m, k, st.out)
 
     def parity(j):
         if n != 10_000_000 or rank != 0:
@@ -385,12 +393,24 @@ def main():
     probed = [torch.cuda.Event() for _ in range(2)]
     times = {"build": [], "probe": []}
 
-    def broadcast(j):
-        if st.broadcast_bufs is None:
-            return None
-        if st.pre_broadcast is not None:
-            st.pre_broadcast(j)  # on the compute stream; the collective waits for it
-        return dist.broadcast(st.broadcast_bufs[j % 2], src=0, async_op=True)
+    # Probe batches reach ranks > 0 by RCCL broadcast from rank 0, issued `lead` steps ahead on
+    # torch's nccl stream so xGMI transfer overlaps compute; a rank's probe of batch j waits (on the
+    # GPU, not the host) for that batch's broadcast.  lead 1: the keys (rank 0's buffers never
+    # change, so rank 0 never waits) are broadcast at the start of the step before.  lead 2 (packed residues): rank 0
+    # writes batch j+2's buffer in its probe of step j and broadcasts it right after, so it first
+    # waits for the broadcast that last used that buffer (batch j-1).
+    lead = st.bcast_lead
+    nbuf = lead + 1
+    handles = {}
+
+    def broadcast(b):
+        if st.broadcast_bufs is not None:
+            handles[b] = dist.broadcast(st.broadcast_bufs[b % nbuf], src=0, async_op=True)
+
+    def wait_batch(b):
+        h = handles.pop(b, None)
+        if h is not None:
+            h.wait()
 
     # Launch-duration timers: HIP events created without the system-scope completion fence
     # (seb.Timer); a torch.cuda.Event flushes L2 when it completes, ~15 us per record between two
@@ -407,8 +427,9 @@ def main():
         t.record(stream)
         return t
 
-    def step(j, pending, record):
-        nxt = broadcast(j + 1)  # the next batch rides xGMI while this step computes
+    def step(j, record):
+        if lead == 1:
+            broadcast(j + 1)  # the next batch rides xGMI while this step computes
         b_end = None
         if st.build is not None:
             with torch.cuda.stream(sb):
@@ -423,8 +444,10 @@ def main():
                     built[j % 2].record(sb)
             if overlap:
                 sp.wait_event(built[j % 2])
-        if pending is not None:
-            pending.wait()
+        if rank > 0:
+            wait_batch(j)
+        elif lead > 1:
+            wait_batch(j - 1)
         if record:
             p_start = b_end if shared and b_end is not None else \
                 (prev_end[0] if shared and prev_end[0] is not None else mark(sp))
@@ -434,11 +457,16 @@ def main():
             times["probe"].append((p_start, prev_end[0]))
         if overlap:
             probed[j % 2].record(sp)
-        return nxt
+        if lead > 1:
+            broadcast(j + lead)
 
-    pending = broadcast(0)
+    if st.broadcast_bufs is not None:
+        for b in range(lead):
+            if rank == 0 and st.bcast_prologue is not None:
+                st.bcast_prologue(b)
+            broadcast(b)
     for j in range(args.warmup):
-        pending = step(j, pending, False)
+        step(j, False)
     torch.cuda.synchronize()
     parity = st.parity(args.warmup - 1)  # on the same run, after the warm-up steps
 
@@ -447,14 +475,14 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for j in range(args.warmup, args.warmup + args.steps):
-        pending = step(j, pending, True)
+        step(j, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if pending is not None:
-        pending.wait()
+    for b in sorted(handles):
+        wait_batch(b)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

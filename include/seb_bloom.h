@@ -117,6 +117,9 @@ int seb_dev_pack_residues(const seb_keys *keys, uint64_t num_bits, uint32_t num_
                           void *stream);
 int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, uint64_t num_bits,
                          uint32_t num_hashes, uint8_t *out, void *stream);
+/* seb_dev_probe plus the batch's packed residues in one pass (the broadcast root's probe). */
+int seb_dev_probe_emit_packed(const seb_keys *keys, const uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
+                              uint8_t *out, uint64_t *packed, void *stream);
 /* Multi-filter probe: bit f of mask[i] = MayContain of filters[f] on key i.  mask_bytes is the
  * width of one mask element (1, 2, 4 or 8) and must cover num_filters bits (<= 64). `filters`
  * is a HOST array whose .bits are device word arrays. */

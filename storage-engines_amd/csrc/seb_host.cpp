@@ -367,6 +367,21 @@ extern "C" int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const ui
     return SEB_OK;
 }
 
+extern "C" int seb_dev_probe_emit_packed(const seb_keys *keys, const uint32_t *words, uint64_t m, uint32_t k,
+                                         uint8_t *out, uint64_t *packed, void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc;
+    if ((rc = check_keys(keys, "seb_dev_probe_emit_packed")) ||
+        (rc = check_packed_args(m, k, "seb_dev_probe_emit_packed")))
+        return rc;
+    if (keys->n && (!words || !out || !packed)) return fail(SEB_ERR_INVALID, "seb_dev_probe_emit_packed: null pointer");
+    KeyBatch kb = key_batch(keys);
+    void *ws;
+    if ((rc = prepare_probe_keys(kb, (hipStream_t)stream, 0, &ws))) return rc;
+    HIP_OR_FAIL(launch_probe_emit(kb, words, mod_arg(m, k), out, packed, (hipStream_t)stream));
+    return SEB_OK;
+}
+
 static int fill_multi(const seb_filter_ref *filters, uint32_t nf, uint32_t mask_bytes, MultiArg *ma,
                       const char *who) {
     if (!filters || nf == 0) return fail(SEB_ERR_INVALID, "%s: no filters", who);

@@ -123,5 +123,8 @@ constexpr uint32_t kPackBits = 29;
 hipError_t launch_pack_residues(const KeyBatch &kb, const ModArg &md, uint64_t *packed, hipStream_t s);
 hipError_t launch_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
                                uint8_t *out, hipStream_t s);
+// Probe from keys that also writes the batch's packed residues.
+hipError_t launch_probe_emit(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out,
+                             uint64_t *packed, hipStream_t s);
 
 }  // namespace seb

@@ -322,6 +322,54 @@ __global__ __launch_bounds__(256) void k_pack_residues(Src src, uint64_t n, ModA
     }
 }
 
+// Sliced probe (MODE 0) from keys that also writes each key's packed residues: the root of a
+// multi-GPU probe answers a batch for its own filter and produces the broadcast form in one pass.
+template <typename Src, int KPT>
+__global__ __launch_bounds__(256) void k_probe_sliced_emit(Src src, uint64_t n, const uint32_t *__restrict__ words,
+                                                           ModArg md, uint8_t *__restrict__ out,
+                                                           uint64_t *__restrict__ packed, uint32_t slice_shift,
+                                                           uint32_t nslices) {
+    const uint64_t span = (uint64_t)blockDim.x * KPT;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
+        uint32_t pos[KPT][7];
+        uint32_t acc[KPT];
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            uint64_t h1 = 0, h2 = 0;
+            if (i < n) src.hash(i, h1, h2);
+            for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
+            acc[r] = i < n ? 1u : 0u;
+            if (i < n) {
+                uint64_t f = 0, x = h1;
+#pragma unroll
+                for (uint32_t q = 1; q < 7; ++q) {
+                    const uint64_t xn = x + h2;
+                    f |= (uint64_t)(xn < x) << (q - 1);
+                    x = xn;
+                }
+                const uint64_t b = mod64(h2, md.m, md.mu);
+                __builtin_nontemporal_store((uint64_t)pos[r][0] | (b << kPackBits) | (f << (2 * kPackBits)),
+                                            packed + src.index(i));
+            }
+        }
+        for (uint32_t sl = 0; sl < nslices; ++sl) {
+#pragma unroll
+            for (int r = 0; r < KPT; ++r)
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    const uint32_t w = pos[r][q] >> 5;
+                    if ((acc[r] & 1u) && (w >> slice_shift) == sl) acc[r] &= words[w] >> (pos[r][q] & 31);
+                }
+        }
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            if (i < n) out[src.index(i)] = (uint8_t)(acc[r] & 1u);
+        }
+    }
+}
+
 // Sliced probe (MODE 0 gather order) over packed residues; k == 7.
 template <int KPT>
 __global__ __launch_bounds__(256) void k_probe_packed(const uint64_t *__restrict__ packed, uint64_t n,
@@ -789,6 +837,22 @@ hipError_t launch_probe_packed(const uint64_t *packed, uint64_t n, const uint32_
     const unsigned g = grid_for((n + 1) / 2, 256, o.probe_slice_grid ? o.probe_slice_grid : o.grid_cap);
     hipLaunchKernelGGL(k_probe_packed<2>, dim3(g), dim3(256), 0, s, packed, n, words, md, out, shift, nsl);
     return hipGetLastError();
+}
+
+hipError_t launch_probe_emit(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out,
+                             uint64_t *packed, hipStream_t s) {
+    if (kb.n == 0) return hipSuccess;
+    const Options &o = options();
+    const uint64_t nwords = (md.m + 31) / 32;
+    const uint32_t shift = o.probe_slice_shift > 0 ? (uint32_t)o.probe_slice_shift : 31u;
+    const uint32_t nsl = shift >= 31 ? 1u : (uint32_t)((nwords + (1ull << shift) - 1) >> shift);
+    const unsigned g = grid_for((kb.n + 1) / 2, 256, o.probe_slice_grid ? o.probe_slice_grid : o.grid_cap);
+    return with_src(kb, [&](auto src) {
+        using S = decltype(src);
+        hipLaunchKernelGGL((k_probe_sliced_emit<S, 2>), dim3(g), dim3(256), 0, s, src, kb.n, words, md, out, packed,
+                           shift, nsl);
+        return hipGetLastError();
+    });
 }
 
 }  // namespace seb

@@ -106,6 +106,7 @@ _SIGS = {
     "seb_wal_scan": (_i, [_vp, _u64, _vp, _u64, C.POINTER(_u64)]),
     "seb_dev_pack_residues": (_i, [C.POINTER(seb_keys), _u64, _u32, _vp, _vp]),
     "seb_dev_probe_packed": (_i, [_vp, _u64, _vp, _u64, _u32, _vp, _vp]),
+    "seb_dev_probe_emit_packed": (_i, [C.POINTER(seb_keys), _vp, _u64, _u32, _vp, _vp, _vp]),
     "seb_timer_create": (_i, [C.POINTER(_vp)]),
     "seb_timer_record": (_i, [_vp, _vp]),
     "seb_timer_elapsed_ms": (_i, [_vp, _vp, C.POINTER(C.c_float)]),
@@ -450,6 +451,12 @@ def dev_pack_residues(keys: seb_keys, m: int, k: int, packed, stream=None) -> No
 
 def dev_probe_packed(packed, n: int, words, m: int, k: int, out, stream=None) -> None:
     check(lib().seb_dev_probe_packed(packed.data_ptr(), n, words.data_ptr(), m, k, out.data_ptr(), _stream(stream)))
+
+
+def dev_probe_emit_packed(keys: seb_keys, words, m: int, k: int, out, packed, stream=None) -> None:
+    """dev_probe that also writes the batch's packed residues (the broadcast root's probe)."""
+    check(lib().seb_dev_probe_emit_packed(C.byref(keys), words.data_ptr(), m, k, out.data_ptr(), packed.data_ptr(),
+                                          _stream(stream)))
 
 
 def dev_probe_multi(keys: seb_keys, filters: list[tuple[object, int, int]], mask, stream=None) -> None:

@@ -283,6 +283,13 @@ def test_packed_residues(seb, golden, torch_cuda):
     seb.dev_probe_packed(packed, n, words, m, k, out)
     torch.cuda.synchronize()
     assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
+    # the root's fused probe: the same answers and the same packed words in one pass
+    packed2 = torch.zeros(n, dtype=torch.int64, device="cuda")
+    out2 = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    seb.dev_probe_emit_packed(pk, words, m, k, out2, packed2)
+    torch.cuda.synchronize()
+    assert torch.equal(packed2, packed)
+    assert torch.equal(out2, out)
     host = packed.cpu().numpy().view(np.uint64)
     sample = np.r_[0:2000, n - 2000:n]
     want = np.array([oc.positions(kg.key16_bytes(int(i)), m, k) for i in pidx[sample]], np.uint64)
