@@ -78,7 +78,8 @@ int seb_abi_version(void);
  *   "grid_cap"        maximum workgroups of the grid-stride kernels
  *   "probe_slice_shift" k == 7, m < 2^32 probes: slice of 2^shift words gathered per phase (0 = off)
  *   "probe_slice_grid"  sliced probe: workgroup cap (0 = grid_cap)
- *   "probe_mode"      sliced probe gather order 0-7 (see k_probe_sliced)
+ *   "probe_mode"      k == 7 probe: 8 = phased, one launch per filter range (default); 0-7 sliced gather orders (k_probe_sliced)
+ *   "probe_phases"    phased probe (probe_mode 8): phases, 0 = one per 4 MiB of filter
  *   "probe_persistent" sliced probe: persistent 1024-thread workgroups (0 = off)
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
  *   "scatter_threads", "scatter_kpt"  radix-partitioned build: workgroup size, keys per thread

@@ -99,12 +99,13 @@ static void load_env() {
     if (env_flag("SEB_BUILD_ALGO", &v)) o.build_algo = (int)v;
     if (env_flag("SEB_PROBE_SPLIT", &v)) o.probe_split = (int)v;
     if (env_flag("SEB_PROBE_KPT", &v)) o.probe_kpt = (int)v;
+    if (env_flag("SEB_PROBE_PHASES", &v) && v >= 0 && v <= 64) o.probe_phases = (int)v;
     if (env_flag("SEB_MULTI_INTERLEAVE", &v)) o.multi_interleave = (int)v;
     if (env_flag("SEB_SCATTER_THREADS", &v)) o.scatter_threads = (int)v;
     if (env_flag("SEB_STREAM_NT", &v)) o.stream_nt = (int)v;
     if (env_flag("SEB_SCATTER_KPT", &v)) o.scatter_kpt = (int)v;
     if (env_flag("SEB_PROBE_PERSISTENT", &v)) o.probe_persistent = (int)v;
-    if (env_flag("SEB_PROBE_MODE", &v) && v >= 0 && v <= 7) o.probe_mode = (int)v;
+    if (env_flag("SEB_PROBE_MODE", &v) && v >= 0 && v <= 8) o.probe_mode = (int)v;
     if (env_flag("SEB_WAL_LDS_KIB", &v) && (v == 36 || v == 48)) o.wal_lds_kib = (int)v;
     if (env_flag("SEB_VARLEN_SORT_MIN_KEYS", &v) && v >= 0) o.varlen_sort_min_keys = (uint64_t)v;
     if (env_flag("SEB_VARLEN_PREHASH_MIN_KEYS", &v) && v >= 0) o.varlen_prehash_min_keys = (uint64_t)v;
@@ -127,7 +128,8 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     else if (!strcmp(name, "stream_nt") && (value == 0 || value == 1)) o.stream_nt = (int)value;
     else if (!strcmp(name, "scatter_kpt") && (value == 4 || value == 5)) o.scatter_kpt = (int)value;
     else if (!strcmp(name, "probe_persistent") && value >= 0 && value <= 65536) o.probe_persistent = (int)value;
-    else if (!strcmp(name, "probe_mode") && value >= 0 && value <= 7) o.probe_mode = (int)value;
+    else if (!strcmp(name, "probe_mode") && value >= 0 && value <= 8) o.probe_mode = (int)value;
+    else if (!strcmp(name, "probe_phases") && value >= 0 && value <= 64) o.probe_phases = (int)value;
     else if (!strcmp(name, "wal_lds_kib") && (value == 36 || value == 48)) o.wal_lds_kib = (int)value;
     else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
@@ -152,6 +154,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "scatter_kpt")) *value = o.scatter_kpt;
     else if (!strcmp(name, "probe_persistent")) *value = o.probe_persistent;
     else if (!strcmp(name, "probe_mode")) *value = o.probe_mode;
+    else if (!strcmp(name, "probe_phases")) *value = o.probe_phases;
     else if (!strcmp(name, "wal_lds_kib")) *value = o.wal_lds_kib;
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;
@@ -189,6 +192,7 @@ extern "C" int seb_dev_clear(uint32_t *words, uint64_t m, void *stream) {
 struct WsKey {
     int device;
     hipStream_t stream;
+    int tag;  // 0: build / key preparation scratch; 1: the phased probe's packed residues
 };
 struct WsEntry {
     WsKey key;
@@ -198,12 +202,12 @@ struct WsEntry {
 static std::mutex g_ws_mu;
 static std::vector<WsEntry> g_ws;
 
-static int cached_workspace(hipStream_t s, uint64_t bytes, void **out) {
+static int cached_workspace(hipStream_t s, uint64_t bytes, void **out, int tag = 0) {
     int dev = 0;
     HIP_OR_FAIL(hipGetDevice(&dev));
     std::lock_guard<std::mutex> g(g_ws_mu);
     for (auto &e : g_ws)
-        if (e.key.device == dev && e.key.stream == s) {
+        if (e.key.device == dev && e.key.stream == s && e.key.tag == tag) {
             if (e.bytes >= bytes) {
                 *out = e.p;
                 return SEB_OK;
@@ -221,7 +225,7 @@ static int cached_workspace(hipStream_t s, uint64_t bytes, void **out) {
     void *p = nullptr;
     hipError_t a = hipMalloc(&p, bytes);
     if (a != hipSuccess) return fail(SEB_ERR_NOMEM, "workspace hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(a));
-    g_ws.push_back({{dev, s}, p, bytes});
+    g_ws.push_back({{dev, s, tag}, p, bytes});
     *out = p;
     return SEB_OK;
 }
@@ -284,10 +288,24 @@ static int prepare_probe_keys(KeyBatch &kb, hipStream_t s, uint64_t extra, void 
     return SEB_OK;
 }
 
+// The phased probe applies to k == 7, m < 2^29 filters spanning more than one phase, with a
+// 4-byte aligned answer array.
+static bool want_phased(uint64_t n, const ModArg &md, const uint8_t *out) {
+    const Options &o = options();
+    if (o.probe_mode != 8 || md.k != 7 || md.m >= (1ull << kPackBits)) return false;
+    return probe_phase_count(md.m) > 1 && ((uintptr_t)out & 3) == 0 && n > 0;
+}
+
 static int probe_dispatch(KeyBatch kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s) {
     void *ws;
     int rc = prepare_probe_keys(kb, s, 0, &ws);
     if (rc) return rc;
+    if (want_phased(kb.n, md, out)) {  // packed residues in their own scratch (tag 1)
+        void *packed;
+        if ((rc = cached_workspace(s, kb.n * 8, &packed, 1))) return rc;
+        HIP_OR_FAIL(launch_probe_phased(&kb, kb.n, words, md, out, (uint64_t *)packed, s));
+        return SEB_OK;
+    }
     HIP_OR_FAIL(launch_probe(kb, words, md, out, s));
     return SEB_OK;
 }
@@ -363,7 +381,11 @@ extern "C" int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const ui
     int rc = check_packed_args(m, k, "seb_dev_probe_packed");
     if (rc) return rc;
     if (n && (!packed || !words || !out)) return fail(SEB_ERR_INVALID, "seb_dev_probe_packed: null pointer");
-    HIP_OR_FAIL(launch_probe_packed(packed, n, words, mod_arg(m, k), out, (hipStream_t)stream));
+    const ModArg md = mod_arg(m, k);
+    if (want_phased(n, md, out))
+        HIP_OR_FAIL(launch_probe_phased(nullptr, n, words, md, out, const_cast<uint64_t *>(packed), (hipStream_t)stream));
+    else
+        HIP_OR_FAIL(launch_probe_packed(packed, n, words, md, out, (hipStream_t)stream));
     return SEB_OK;
 }
 
@@ -378,7 +400,11 @@ extern "C" int seb_dev_probe_emit_packed(const seb_keys *keys, const uint32_t *w
     KeyBatch kb = key_batch(keys);
     void *ws;
     if ((rc = prepare_probe_keys(kb, (hipStream_t)stream, 0, &ws))) return rc;
-    HIP_OR_FAIL(launch_probe_emit(kb, words, mod_arg(m, k), out, packed, (hipStream_t)stream));
+    const ModArg md = mod_arg(m, k);
+    if (want_phased(kb.n, md, out))  // phase 0 writes the packed residues anyway
+        HIP_OR_FAIL(launch_probe_phased(&kb, kb.n, words, md, out, packed, (hipStream_t)stream));
+    else
+        HIP_OR_FAIL(launch_probe_emit(kb, words, md, out, packed, (hipStream_t)stream));
     return SEB_OK;
 }
 

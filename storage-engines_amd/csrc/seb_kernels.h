@@ -88,7 +88,8 @@ struct Options {
     int stream_nt = 1;            // non-temporal loads for 16-B key batches (keeps filter lines in L2)
     int probe_persistent = 0;     // sliced probe: persistent 1024-thread workgroups, barrier per slice (0 = off)
     int wal_lds_kib = 36;         // WAL CRC: LDS staging window per 256-record workgroup (36 or 48)
-    int probe_mode = 0;           // sliced probe gather order (k_probe_sliced MODE 0-6; 7 = k_probe_compact)
+    int probe_phases = 0;         // phased probe: number of phases (0 = one per 4 MiB of filter)
+    int probe_mode = 8;           // k == 7 probe: 8 = phased (one launch per filter range, default); 0-6 k_probe_sliced MODE, 7 k_probe_compact
     unsigned grid_cap = 1u << 20;
 };
 Options &options();
@@ -123,6 +124,12 @@ constexpr uint32_t kPackBits = 29;
 hipError_t launch_pack_residues(const KeyBatch &kb, const ModArg &md, uint64_t *packed, hipStream_t s);
 hipError_t launch_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
                                uint8_t *out, hipStream_t s);
+// Phased probe (probe_mode 8; k == 7, m < 2^kPackBits, 4-byte aligned out): one launch per word
+// range of the filter (probe_phase_count of them); `packed` is 8*n bytes of scratch.
+uint64_t probe_phase_count(uint64_t m);
+// kb == nullptr: probe the packed words themselves (no phase 0 hashing).
+hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
+                               uint64_t *packed, hipStream_t s);
 // Probe from keys that also writes the batch's packed residues.
 hipError_t launch_probe_emit(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out,
                              uint64_t *packed, hipStream_t s);

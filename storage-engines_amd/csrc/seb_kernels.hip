@@ -370,6 +370,157 @@ __global__ __launch_bounds__(256) void k_probe_sliced_emit(Src src, uint64_t n, 
     }
 }
 
+// ---- phased probe (MODE 8; k == 7, m < 2^29).  The sliced probe's cost is its L2 misses: its
+// workgroups are only loosely aligned in their sweep over the slices, so each XCD refills its L2
+// with the 12 MB filter ~2.3 times per workgroup generation (profiles/r01z).  Here every phase (a
+// contiguous word range of the filter, about one L2's worth) is its own launch, so all waves of
+// the chip gather from one range at a time and each XCD fetches it into its L2 about once.
+// Phase 0 hashes the keys, writes their packed residues (k_pack_residues' layout) and tests the
+// positions in range 0; phase p > 0 reads the answer bytes and, for keys still alive,
+// regenerates the positions from the packed words and tests those in range p, each gather only
+// while the key's bits so far are all set (MODE 0's early exit; sampling liveness once per phase
+// so a key's gathers overlap was measured slower: more gathers).  The answer is the AND of the k
+// bits, as MayContain (lsm/bloom.go:82-92) returns.
+template <typename Src>
+__global__ __launch_bounds__(256) void k_probe_phase0(Src src, uint64_t n, const uint32_t *__restrict__ words,
+                                                      ModArg md, uint8_t *__restrict__ out,
+                                                      uint64_t *__restrict__ packed, uint32_t hi) {
+    constexpr int KPT = 2;
+    const uint64_t span = (uint64_t)blockDim.x * KPT;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
+        uint32_t pos[KPT][7];
+        uint32_t acc[KPT];
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            uint64_t h1 = 0, h2 = 0;
+            if (i < n) src.hash(i, h1, h2);
+            for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
+            acc[r] = i < n ? 1u : 0u;
+            if (i < n) {
+                uint64_t f = 0, x = h1;
+#pragma unroll
+                for (uint32_t q = 1; q < 7; ++q) {
+                    const uint64_t xn = x + h2;
+                    f |= (uint64_t)(xn < x) << (q - 1);
+                    x = xn;
+                }
+                const uint64_t b = mod64(h2, md.m, md.mu);
+                __builtin_nontemporal_store((uint64_t)pos[r][0] | (b << kPackBits) | (f << (2 * kPackBits)),
+                                            packed + i);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < KPT; ++r)
+#pragma unroll
+            for (int q = 0; q < 7; ++q) {
+                const uint32_t w = pos[r][q] >> 5;
+                if ((acc[r] & 1u) && w < hi) acc[r] &= words[w] >> (pos[r][q] & 31);
+            }
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            if (i < n) out[i] = (uint8_t)(acc[r] & 1u);
+        }
+    }
+}
+
+// Phase p > 0 over words [lo, hi): thread t owns keys 4t..4t+3 (one u32 of answers, two 16-B
+// loads of packed words); `out` is 4-byte aligned (the host checks).  PMAJOR: walk the 7
+// positions of the 4 keys position-major (4 independent gathers per step) instead of key by key.
+template <bool PMAJOR>
+__global__ __launch_bounds__(256) void k_probe_phase(const uint64_t *__restrict__ packed, uint64_t n,
+                                                     const uint32_t *__restrict__ words, ModArg md,
+                                                     uint8_t *__restrict__ out, uint32_t lo, uint32_t hi,
+                                                     uint32_t first) {
+    const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
+    constexpr uint64_t kMask = (1ull << kPackBits) - 1;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+    for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < n; i0 += stride) {
+        const bool full = i0 + 4 <= n;
+        uint32_t a;
+        if (first) {  // a batch probed from packed words alone: every key starts alive
+            a = full ? 0x01010101u : 0x01010101u & ((1u << (8 * (uint32_t)(n - i0))) - 1u);
+        } else if (full) {
+            a = *(const uint32_t *)(out + i0);
+        } else {
+            a = 0;
+            for (uint32_t r = 0; i0 + r < n; ++r) a |= (uint32_t)out[i0 + r] << (8 * r);
+        }
+        if (a == 0u) continue;
+        uint64_t pv[4];
+        if (full) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 p0 = __builtin_nontemporal_load((const u32x4 *)(packed + i0));
+            const u32x4 p1 = __builtin_nontemporal_load((const u32x4 *)(packed + i0 + 2));
+            pv[0] = (uint64_t)p0.x | ((uint64_t)p0.y << 32);
+            pv[1] = (uint64_t)p0.z | ((uint64_t)p0.w << 32);
+            pv[2] = (uint64_t)p1.x | ((uint64_t)p1.y << 32);
+            pv[3] = (uint64_t)p1.z | ((uint64_t)p1.w << 32);
+        } else {
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) pv[r] = i0 + r < n ? packed[i0 + r] : 0ull;
+        }
+        uint32_t na = a;
+        if constexpr (PMAJOR) {
+            uint32_t live[4], x[4], nb[4], nd[4], f[4];
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) {
+                live[r] = (a >> (8 * r)) & 1u;
+                x[r] = (uint32_t)(pv[r] & kMask);
+                const uint32_t b = (uint32_t)((pv[r] >> kPackBits) & kMask);
+                f[r] = (uint32_t)(pv[r] >> (2 * kPackBits));
+                nb[r] = m - b;
+                nd[r] = m - (b >= c ? b - c : b + (m - c));
+            }
+#pragma unroll
+            for (int q = 0; q < 7; ++q) {
+                uint32_t v[4];
+#pragma unroll
+                for (uint32_t r = 0; r < 4; ++r) {
+                    if (q > 0) {
+                        const uint32_t d = (f[r] >> (q - 1)) & 1u ? nd[r] : nb[r];
+                        const uint32_t t = x[r] - d;
+                        x[r] = x[r] >= d ? t : t + m;
+                    }
+                    const uint32_t w = x[r] >> 5;
+                    v[r] = ~0u;
+                    if (live[r] && w >= lo && w < hi) v[r] = words[w];
+                }
+#pragma unroll
+                for (uint32_t r = 0; r < 4; ++r) live[r] &= v[r] >> (x[r] & 31);
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) na &= ~((((a >> (8 * r)) & 1u) & (live[r] ^ 1u)) << (8 * r));
+        } else {
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) {
+                uint32_t live = (a >> (8 * r)) & 1u;
+                uint32_t x = (uint32_t)(pv[r] & kMask);
+                const uint32_t b = (uint32_t)((pv[r] >> kPackBits) & kMask), f = (uint32_t)(pv[r] >> (2 * kPackBits));
+                const uint32_t nb = m - b, bc = b >= c ? b - c : b + (m - c), nd = m - bc;
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    if (q > 0) {
+                        const uint32_t d = (f >> (q - 1)) & 1u ? nd : nb;
+                        const uint32_t t = x - d;
+                        x = x >= d ? t : t + m;
+                    }
+                    const uint32_t w = x >> 5;
+                    if (live && w >= lo && w < hi) live &= words[w] >> (x & 31);
+                }
+                na &= ~((((a >> (8 * r)) & 1u) & (live ^ 1u)) << (8 * r));
+            }
+        }
+        if (na != a || first) {
+            if (full)
+                *(uint32_t *)(out + i0) = na;
+            else
+                for (uint32_t r = 0; i0 + r < n; ++r) out[i0 + r] = (uint8_t)(na >> (8 * r));
+        }
+    }
+}
+
 // Sliced probe (MODE 0 gather order) over packed residues; k == 7.
 template <int KPT>
 __global__ __launch_bounds__(256) void k_probe_packed(const uint64_t *__restrict__ packed, uint64_t n,
@@ -853,6 +1004,52 @@ hipError_t launch_probe_emit(const KeyBatch &kb, const uint32_t *words, const Mo
                            shift, nsl);
         return hipGetLastError();
     });
+}
+
+// Phased probe.  From keys (kb != nullptr): phase 0 hashes them and writes their packed residues
+// to `packed`; from packed words (kb == nullptr): every phase reads them.
+hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
+                               uint64_t *packed, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const Options &o = options();
+    const uint64_t nwords = (md.m + 31) / 32;
+    const uint64_t np = probe_phase_count(md.m);
+    auto bound = [&](uint64_t p) { return (uint32_t)(nwords * p / np); };
+    hipError_t e = hipSuccess;
+    uint64_t p0 = 0;
+    if (kb) {
+        const unsigned g0 = grid_for((n + 1) / 2, 256, o.grid_cap);
+        e = with_src(*kb, [&](auto src) {
+            using S = decltype(src);
+            hipLaunchKernelGGL(k_probe_phase0<S>, dim3(g0), dim3(256), 0, s, src, n, words, md, out, packed,
+                               bound(1));
+            return hipGetLastError();
+        });
+        if (e != hipSuccess) return e;
+        p0 = 1;
+    }
+    const unsigned g = grid_for((n + 3) / 4, 256, o.grid_cap);
+    for (uint64_t p = p0; p < np; ++p) {
+        const uint32_t first = p == 0 ? 1u : 0u;
+        if (o.probe_kpt == 4)
+            hipLaunchKernelGGL(k_probe_phase<true>, dim3(g), dim3(256), 0, s, packed, n, words, md, out, bound(p),
+                               bound(p + 1), first);
+        else
+            hipLaunchKernelGGL(k_probe_phase<false>, dim3(g), dim3(256), 0, s, packed, n, words, md, out, bound(p),
+                               bound(p + 1), first);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// Phases of the phased probe: probe_phases, or one per 4 MiB of filter (one XCD's L2).
+uint64_t probe_phase_count(uint64_t m) {
+    const int64_t want = options().probe_phases;
+    const uint64_t bytes = (m + 7) / 8;
+    uint64_t np = want > 0 ? (uint64_t)want : (bytes + (4ull << 20) - 1) / (4ull << 20);
+    const uint64_t nwords = (m + 31) / 32;
+    if (np > nwords) np = nwords;
+    return np < 1 ? 1 : np;
 }
 
 }  // namespace seb

@@ -225,7 +225,8 @@ def test_c2_c3_10m_device_resident(seb, golden, torch_cuda, build_algo):
 
 
 def test_sliced_probe_gather_orders(seb, golden, torch_cuda):
-    """Every gather order of the sliced probe (k_probe_sliced modes 0-6, k_probe_compact = mode 7)
+    """Every gather order of the sliced probe (k_probe_sliced modes 0-6, k_probe_compact = mode 7,
+    the phased probe = mode 8)
     and keys-per-thread choice gives the C3 answers bit for bit, also for a ragged batch whose
     last workgroup is partly empty."""
     torch = torch_cuda
@@ -236,9 +237,12 @@ def test_sliced_probe_gather_orders(seb, golden, torch_cuda):
     pk = to_dev(torch, kg.key16(kg.probe_indices(n)))
     ragged = 999_983
     ref_ragged = oc.probe(bits, m, k, kg.key16(kg.probe_indices(n)[:ragged]), ragged, stride=16)
-    cases = [(mode, kpt) for mode in range(7) for kpt in (1, 2, 4)] + [(7, kpt) for kpt in (2, 4, 6, 8)]
+    # mode 8 (phased): the second number is the phase count (0 = one per 4 MiB of filter)
+    cases = [(mode, kpt) for mode in range(7) for kpt in (1, 2, 4)] + [(7, kpt) for kpt in (2, 4, 6, 8)] + \
+        [(8, ph) for ph in (0, 2, 4, 7)]
     for mode, kpt in cases:
-        with seb.option("probe_mode", mode), seb.option("probe_kpt", kpt), seb.option("probe_slice_shift", 19):
+        with seb.option("probe_mode", mode), seb.option("probe_kpt", kpt if mode < 8 else 2), \
+                seb.option("probe_phases", kpt if mode == 8 else 0), seb.option("probe_slice_shift", 19):
             out = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
             seb.dev_probe(seb.dev_keys(pk, n=n, stride=16), words, m, k, out)
             torch.cuda.synchronize()
