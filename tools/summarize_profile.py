@@ -62,17 +62,24 @@ def main():
         for k, c, v, cnt in rows:
             w.writerow([k, c, f"{v:.6g}", cnt])
     mean = {(k, c): v for k, c, v, _ in rows}
+    count = {(k, c): cnt for k, c, _, cnt in rows}
     steps = {}
     for step, pats in STEP_KERNELS[a.config].items():
         fetch = write = 0.0
         kernels = []
-        for (k, c), v in mean.items():
-            if any(p in k for p in pats) and ("seb::" in k or "fillBufferAligned" in k):
-                if c == "FETCH_SIZE":
-                    fetch += v
-                    kernels.append(k)
-                elif c == "WRITE_SIZE":
-                    write += v
+        match = [(k, c) for (k, c) in mean if any(p in k for p in pats) and ("seb::" in k or "fillBufferAligned" in k)]
+        # the phased probe launches k_probe_phase (phases - 1) times per k_probe_phase0: weight it
+        # by its launches per phase-0 launch (every other kernel runs once per step)
+        p0 = [count[(k, c)] for k, c in match if "k_probe_phase0" in k and c == "FETCH_SIZE"]
+        for k, c in match:
+            v = mean[(k, c)]
+            if "k_probe_phase<" in k and p0:
+                v *= max(1, round(count[(k, c)] / p0[0]))
+            if c == "FETCH_SIZE":
+                fetch += v
+                kernels.append(k)
+            elif c == "WRITE_SIZE":
+                write += v
         read = fetch * 1024 + a.key_bytes / 2
         steps[step] = {"hbm_bytes_per_launch": int(read + write * 1024), "read_bytes": int(read),
                        "write_bytes": int(write * 1024), "fetch_size_kib": fetch, "write_size_kib": write,
