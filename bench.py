@@ -87,8 +87,8 @@ class Setup:
     build = None
     build_host = probe_host = None
     broadcast_bufs = None
-    bcast_lead = 1        # batch j + lead is broadcast during step j (buffers: lead + 1)
-    bcast_prologue = None # rank 0, before the loop: fill broadcast buffer b for batch b < lead
+    bcast_lead = 1        # batch j + lead is broadcast during step j (dist_probe.BroadcastPipeline)
+    bcast_prologue = None # rank 0, before the loop: produce(b, buf) fills the buffer of batch b < lead
     pmc_key = None        # profiles/pmc_r01.json entry whose per-launch traffic applies (None: config name)
 
 
@@ -126,7 +126,7 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
         st.kernel_bytes["probe"] = (16.0 * n + 8.0 * n if rank == 0 else 8.0 * n) + nb + n
         st.workload += " as 8-B packed residues (hashed once, inside rank 0's probe)"
         st.pmc_key = "c2c3_packed"
-        st.bcast_prologue = lambda b: seb.dev_pack_residues(st.pk[0], m, k, st.packed[b])
+        st.bcast_prologue = lambda b, buf: seb.dev_pack_residues(st.pk[0], m, k, buf)
     else:
         st.broadcast_bufs = st.pbufs if world > 1 else None
     st.parallelism = f"filter-per-gpu x{world}, probe batch broadcast (RCCL)"
@@ -136,12 +136,12 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
         seb.dev_clear(w, m)
         seb.dev_build(st.kb, w, m, k)
 
-    def probe(j):
+    def probe(j, buf, target):
         w = st.wbufs[j % len(st.wbufs)]
         if packed and rank == 0:  # answers batch j + 2's keys and emits its packed form
-            seb.dev_probe_emit_packed(st.pk[0], w, m, k, st.out, st.packed[(j + 2) % 3])
+            seb.dev_probe_emit_packed(st.pk[0], w, m, k, st.out, target)
         elif packed:
-            seb.dev_probe_packed(st.packed[j % 3], n, w, m, k, st.out)
+            seb.dev_probe_packed(buf, n, w, m, k, st.out)
         else:
             seb.dev_probe(st.pk[j % 2], w, m, k, st.out)
 
@@ -191,7 +191,7 @@ def setup_c4(args, seb, kg, torch, dev, rank, world, dist):
             else "MISMATCH: false negative"
 
     st.build = build
-    st.probe = lambda j: seb.dev_probe(st.pk[j % 2], st.wbufs[j % len(st.wbufs)], m, k, st.out)
+    st.probe = lambda j, buf, target: seb.dev_probe(st.pk[j % 2], st.wbufs[j % len(st.wbufs)], m, k, st.out)
     st.parity = parity
     return st
 
@@ -228,7 +228,7 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
                    "batch RCCL-broadcast from rank 0, multi-filter probe, u64 masks all-gathered")
     st.parallelism = f"filters sharded {nf}/{world} per gpu, batch broadcast + mask all-gather (RCCL)"
 
-    def probe(j):
+    def probe(j, buf, target):
         if shard.count:
             seb.dev_probe_multi(st.pk[j % 2], st.local, st.plane)
         if world > 1:
@@ -272,7 +272,7 @@ def setup_lsm(args, seb, kg, torch, dev, rank, world, dist):
     st.workload = ("LSM MultiGet (SURVEY 8(f)): registry of 28 SSTable filters (L0 4x250K overlapping, L1 8x1M, "
                    "L2 16x500K keys); one 10M-key batch resolved per LSM.Get's file walk + bloom checks")
     st.parallelism = f"registry-per-gpu x{world}"
-    st.probe = lambda j: st.reg.multiget_dev(st.pk, st.mask)
+    st.probe = lambda j, buf, target: st.reg.multiget_dev(st.pk, st.mask)
 
     def parity(j):
         if rank != 0:
@@ -303,7 +303,7 @@ def setup_route(args, seb, kg, torch, dev, rank, world, dist):
     st.workload = ("hash-index shard routing (SURVEY 8(f) row 4): FNV-1a32 & 255 of 10M x 16-B keys + stable "
                    "partition into the 256 shards (UpdateBatch's distribution step)")
     st.parallelism = f"independent batch per gpu x{world}"
-    st.probe = lambda j: seb.dev_shard_partition(st.kd, bits, st.perm, st.begin, None, st.ws)
+    st.probe = lambda j, buf, target: seb.dev_shard_partition(st.kd, bits, st.perm, st.begin, None, st.ws)
 
     def parity(j):
         if rank != 0 or n != 10_000_000:
@@ -339,7 +339,7 @@ def setup_wal(args, seb, kg, torch, dev, rank, world, dist):
     st.workload = (f"WAL integrity check (SURVEY 8(f) row 4): CRC32-IEEE + framing of {n} records "
                    f"({img.size / 1e6:.1f} MB; 16-B keys, 100-B values, every 16th a Delete)")
     st.parallelism = f"independent WAL image per gpu x{world}"
-    st.probe = lambda j: seb.dev_wal_crc(st.img, st.off, seb.WAL_VERIFY, st.crc, st.ok)
+    st.probe = lambda j, buf, target: seb.dev_wal_crc(st.img, st.off, seb.WAL_VERIFY, st.crc, st.ok)
 
     def parity(j):
         if rank != 0:
@@ -393,24 +393,15 @@ def main():
     probed = [torch.cuda.Event() for _ in range(2)]
     times = {"build": [], "probe": []}
 
-    # Probe batches reach ranks > 0 by RCCL broadcast from rank 0, issued `lead` steps ahead on
-    # torch's nccl stream so xGMI transfer overlaps compute; a rank's probe of batch j waits (on the
-    # GPU, not the host) for that batch's broadcast.  lead 1: the keys (rank 0's buffers never
-    # change, so rank 0 never waits) are broadcast at the start of the step before.  lead 2 (packed residues): rank 0
-    # writes batch j+2's buffer in its probe of step j and broadcasts it right after, so it first
-    # waits for the broadcast that last used that buffer (batch j-1).
-    lead = st.bcast_lead
-    nbuf = lead + 1
-    handles = {}
+    # Probe batches reach ranks > 0 by RCCL broadcast from rank 0, issued ahead of the step that
+    # probes them on torch's nccl stream, so the xGMI transfer overlaps compute; a rank's probe of
+    # batch j waits on the GPU (a stream wait, not the host) for that broadcast
+    # (dist_probe.BroadcastPipeline; its ordering is tested on CPU in tests/test_dist.py).
+    pipe = None
+    if st.broadcast_bufs is not None:
+        import dist_probe as dp
 
-    def broadcast(b):
-        if st.broadcast_bufs is not None:
-            handles[b] = dist.broadcast(st.broadcast_bufs[b % nbuf], src=0, async_op=True)
-
-    def wait_batch(b):
-        h = handles.pop(b, None)
-        if h is not None:
-            h.wait()
+        pipe = dp.BroadcastPipeline(st.broadcast_bufs, st.bcast_lead, rank, produce=st.bcast_prologue)
 
     # Launch-duration timers: HIP events created without the system-scope completion fence
     # (seb.Timer); a torch.cuda.Event flushes L2 when it completes, ~15 us per record between two
@@ -418,7 +409,7 @@ def main():
     # still costs a few us of command-processor time between two kernels, so adjacent boundaries
     # share one timer: a step's end is the next step's start, and with nothing between build and
     # probe (no broadcast to wait for, one stream) the build's end is the probe's start.
-    shared = not overlap and st.broadcast_bufs is None
+    shared = not overlap and pipe is None
     prev_end = [None]
     pool = [seb.Timer() for _ in range(4 * args.steps + 1)]  # created before the timed region
 
@@ -428,8 +419,8 @@ def main():
         return t
 
     def step(j, record):
-        if lead == 1:
-            broadcast(j + 1)  # the next batch rides xGMI while this step computes
+        if pipe is not None:
+            pipe.begin_step(j)
         b_end = None
         if st.build is not None:
             with torch.cuda.stream(sb):
@@ -444,27 +435,22 @@ def main():
                     built[j % 2].record(sb)
             if overlap:
                 sp.wait_event(built[j % 2])
-        if rank > 0:
-            wait_batch(j)
-        elif lead > 1:
-            wait_batch(j - 1)
+        buf = pipe.acquire(j) if pipe is not None else None
+        target = pipe.root_target(j) if pipe is not None and rank == 0 and pipe.lead > 1 else None
         if record:
             p_start = b_end if shared and b_end is not None else \
                 (prev_end[0] if shared and prev_end[0] is not None else mark(sp))
-        st.probe(j)
+        st.probe(j, buf, target)
         if record:
             prev_end[0] = mark(sp)
             times["probe"].append((p_start, prev_end[0]))
         if overlap:
             probed[j % 2].record(sp)
-        if lead > 1:
-            broadcast(j + lead)
+        if pipe is not None:
+            pipe.end_step(j)
 
-    if st.broadcast_bufs is not None:
-        for b in range(lead):
-            if rank == 0 and st.bcast_prologue is not None:
-                st.bcast_prologue(b)
-            broadcast(b)
+    if pipe is not None:
+        pipe.prologue()
     for j in range(args.warmup):
         step(j, False)
     torch.cuda.synchronize()
@@ -481,8 +467,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    for b in sorted(handles):
-        wait_batch(b)
+    if pipe is not None:
+        pipe.drain()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -123,3 +123,67 @@ def gpu_probe_fn(seb) -> ProbeFn:
         seb.dev_probe_multi(kd, list(local_filters), plane)
 
     return fn
+
+
+class BroadcastPipeline:
+    """Probe batches published by rank 0 and RCCL-broadcast to the other ranks ahead of the step
+    that probes them, so the xGMI transfer overlaps compute (bench.py, c2c3/c5 at N > 1).
+
+    `bufs` holds lead + 1 equally shaped tensors; batch b lives in bufs[b % (lead + 1)].
+      lead 1: rank 0's buffers hold the batch from the start and never change; batch j + 1 is
+              broadcast when step j begins (`begin_step`).
+      lead 2: rank 0 writes batch j + 2 during its step j (the bench: its probe of the keys emits
+              the packed residues) into `root_target(j)` and publishes it with `end_step(j)`.
+              Before that write, the broadcast that last read the buffer (batch j - 1) must be done:
+              `acquire(j)` waits for it on rank 0.
+    On ranks > 0, `acquire(j)` waits for batch j's broadcast and returns its buffer.  Waits are
+    `Work.wait()`: with nccl a stream-ordered wait (the host does not block), with gloo a host wait.
+    `produce(b, buf)`, if given, fills rank 0's buffer for batch b < lead in `prologue`.
+    """
+
+    def __init__(self, bufs: Sequence[torch.Tensor], lead: int, rank: int, group=None,
+                 produce: Callable[[int, torch.Tensor], None] | None = None):
+        if lead < 1 or len(bufs) != lead + 1:
+            raise ValueError("need lead >= 1 and lead + 1 buffers")
+        self.bufs, self.lead, self.rank, self.group, self.produce = list(bufs), lead, rank, group, produce
+        self.handles: dict[int, object] = {}
+
+    def _bcast(self, b: int) -> None:
+        self.handles[b] = dist.broadcast(self.bufs[b % len(self.bufs)], src=0, group=self.group, async_op=True)
+
+    def _wait(self, b: int) -> None:
+        h = self.handles.pop(b, None)
+        if h is not None:
+            h.wait()
+
+    def prologue(self) -> None:
+        for b in range(self.lead):
+            if self.rank == 0 and self.produce is not None:
+                self.produce(b, self.bufs[b % len(self.bufs)])
+            self._bcast(b)
+
+    def begin_step(self, j: int) -> None:
+        if self.lead == 1:
+            self._bcast(j + 1)
+
+    def acquire(self, j: int) -> torch.Tensor:
+        """The buffer holding batch j (ranks > 0), after its broadcast; on rank 0 with lead > 1,
+        also makes root_target(j) safe to overwrite."""
+        if self.rank > 0:
+            self._wait(j)
+        elif self.lead > 1:
+            self._wait(j - 1)
+        return self.bufs[j % len(self.bufs)]
+
+    def root_target(self, j: int) -> torch.Tensor:
+        """Rank 0, lead > 1: the buffer that batch j + lead is written into during step j."""
+        return self.bufs[(j + self.lead) % len(self.bufs)]
+
+    def end_step(self, j: int) -> None:
+        if self.lead > 1:
+            self._bcast(j + self.lead)
+
+    def drain(self) -> None:
+        for b in sorted(self.handles):
+            self._wait(b)
+

@@ -101,3 +101,71 @@ def test_assemble_mask_high_bits():
     p0 = torch.tensor([-32768], dtype=torch.int16)
     p1 = torch.tensor([1], dtype=torch.int16)
     assert dp.assemble_mask([p0, p1], 32)[0] == np.uint64((1 << 15) | (1 << 16))
+
+
+def _batch(b: int, n: int) -> torch.Tensor:
+    """Content of probe batch b in the pipeline test: the packed residues of keys key16(b*n + i)
+    (the oracle's positions, packed as seb_dev_pack_residues lays them out) - distinct per batch."""
+    m, _ = oc.params(10_000, 0.01)
+    words = []
+    for i in range(n):
+        h1, h2 = oc.fnv(kg.key16_bytes(b * n + i))
+        flags = 0
+        x = h1
+        for q in range(1, 7):
+            xn = (x + h2) & ((1 << 64) - 1)
+            flags |= int(xn < x) << (q - 1)
+            x = xn
+        words.append((h1 % m) | ((h2 % m) << 29) | (flags << 58))
+    return torch.tensor(np.array(words, dtype=np.uint64).view(np.int64))
+
+
+def _pipeline_worker(rank, world, port, lead, steps, n, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        bufs = [torch.zeros(n, dtype=torch.int64) for _ in range(lead + 1)]
+        const = _batch(7, n)
+        if lead == 1 and rank == 0:  # lead 1: rank 0's buffers hold the one batch throughout
+            for b in bufs:
+                b.copy_(const)
+        produce = (lambda b, buf: buf.copy_(_batch(b, n))) if lead > 1 else None
+        pipe = dp.BroadcastPipeline(bufs, lead, rank, produce=produce)
+        pipe.prologue()
+        seen = []
+        for j in range(steps):
+            pipe.begin_step(j)
+            buf = pipe.acquire(j)
+            if rank == 0 and lead > 1:
+                pipe.root_target(j).copy_(_batch(j + lead, n))  # the bench's probe emits batch j+lead here
+            elif rank > 0:
+                seen.append(buf.clone())
+            pipe.end_step(j)
+        pipe.drain()
+        q.put((rank, [s.numpy() for s in seen]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,lead", [(2, 1), (2, 2), (3, 2), (3, 1)])
+def test_broadcast_pipeline_delivers_each_batch_in_order(world, lead):
+    """bench.py's N>1 probe-batch pipeline (dist_probe.BroadcastPipeline): every rank > 0 sees
+    batch j at step j - with lead 2 the batches differ per step and rank 0 overwrites each buffer
+    while earlier broadcasts are in flight, so an ordering or reuse bug shows as a wrong batch."""
+    n, steps = 64, 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, lead, steps, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(1, world):
+        assert len(results[r]) == steps
+        for j, got in enumerate(results[r]):
+            want = _batch(7 if lead == 1 else j, n).numpy()
+            assert np.array_equal(got, want), (r, j)
