@@ -1014,7 +1014,15 @@ hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *w
     const Options &o = options();
     const uint64_t nwords = (md.m + 31) / 32;
     const uint64_t np = probe_phase_count(md.m);
-    auto bound = [&](uint64_t p) { return (uint32_t)(nwords * p / np); };
+    // probe_phase0_pct > 0: range 0 (where every key is still alive) takes that share of the
+    // filter and the other ranges split the rest evenly
+    const uint64_t pct = (uint64_t)o.probe_phase0_pct;
+    auto bound = [&](uint64_t p) {
+        if (p == 0) return 0u;
+        if (pct == 0 || np < 2 || p >= np) return (uint32_t)(nwords * p / np);
+        const uint64_t w0 = nwords * pct / 100;
+        return (uint32_t)(w0 + (nwords - w0) * (p - 1) / (np - 1));
+    };
     hipError_t e = hipSuccess;
     uint64_t p0 = 0;
     if (kb) {

@@ -431,6 +431,46 @@ def test_modulus_edge_cases(seb, torch_cuda, m, k, algo):
     seb.set_option("build_algo", 0)
 
 
+@pytest.mark.parametrize("m", [(1 << 29) - 3, 1 << 29, 33_554_433, 33_554_432 * 2 + 7])
+def test_phased_probe_ranges(seb, torch_cuda, m):
+    """The phased probe (default) at the edges of its domain: m just under 2^29 (the packed
+    residue width, 16 ranges), m = 2^29 (falls back to the sliced probe), filters one bit over
+    one and two 4 MiB ranges (2 and 3 ranges), and an answer array that is not 4-byte aligned
+    (falls back).  Answers equal the oracle's for present and absent keys."""
+    torch = torch_cuda
+    k = 7
+    rng = np.random.default_rng(m % 997)
+    n = 60_000
+    keys = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    words = seb.new_words(m)
+    seb.dev_build(seb.dev_keys(to_dev(torch, keys), n=n, stride=16), words, m, k)
+    probe = np.concatenate([keys[: n // 2], rng.integers(0, 256, (n - n // 2, 16), dtype=np.uint8)])
+    # the oracle's answers: every position of the key set in the built words
+    h1, h2 = bn.fnv_fixed(probe)
+    pos = bn.positions(h1, h2, m, k)
+    w = words.cpu().numpy().view(np.uint32)
+    want = np.all((w[(pos >> np.uint64(5)).astype(np.int64)] >> (pos & np.uint64(31)).astype(np.uint32)) & 1,
+                  axis=1).astype(np.uint8)
+    assert want[: n // 2].all()
+    pk = seb.dev_keys(to_dev(torch, probe), n=n, stride=16)
+    buf = torch.full((n + 8,), 7, dtype=torch.uint8, device="cuda")
+    for off in (0, 1):  # aligned (phased where it applies) and unaligned (fallback)
+        out = buf[off: off + n]
+        seb.dev_probe(pk, words, m, k, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want), off
+    if m < (1 << 29):  # packed forms
+        packed = torch.zeros(n, dtype=torch.int64, device="cuda")
+        out = buf[:n]
+        seb.dev_probe_emit_packed(pk, words, m, k, out, packed)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want)
+        out.fill_(7)
+        seb.dev_probe_packed(packed, n, words, m, k, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want)
+
+
 def test_probe_split_variants(seb, golden, torch_cuda, probe_split):
     """The split-round probe (first-round gathers, the rest only where all bits so far are set)
     returns exactly the single-round answers."""
