@@ -131,6 +131,7 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     else if (!strcmp(name, "probe_mode") && value >= 0 && value <= 8) o.probe_mode = (int)value;
     else if (!strcmp(name, "probe_phases") && value >= 0 && value <= 64) o.probe_phases = (int)value;
     else if (!strcmp(name, "probe_phase0_pct") && value >= 0 && value <= 90) o.probe_phase0_pct = (int)value;
+    else if (!strcmp(name, "probe_phase0_kpt") && (value == 1 || value == 2 || value == 4)) o.probe_phase0_kpt = (int)value;
     else if (!strcmp(name, "wal_lds_kib") && (value == 36 || value == 48)) o.wal_lds_kib = (int)value;
     else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
@@ -157,6 +158,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "probe_mode")) *value = o.probe_mode;
     else if (!strcmp(name, "probe_phases")) *value = o.probe_phases;
     else if (!strcmp(name, "probe_phase0_pct")) *value = o.probe_phase0_pct;
+    else if (!strcmp(name, "probe_phase0_kpt")) *value = o.probe_phase0_kpt;
     else if (!strcmp(name, "wal_lds_kib")) *value = o.wal_lds_kib;
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;

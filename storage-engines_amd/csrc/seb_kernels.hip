@@ -381,11 +381,10 @@ __global__ __launch_bounds__(256) void k_probe_sliced_emit(Src src, uint64_t n, 
 // while the key's bits so far are all set (MODE 0's early exit; sampling liveness once per phase
 // so a key's gathers overlap was measured slower: more gathers).  The answer is the AND of the k
 // bits, as MayContain (lsm/bloom.go:82-92) returns.
-template <typename Src>
+template <typename Src, int KPT>
 __global__ __launch_bounds__(256) void k_probe_phase0(Src src, uint64_t n, const uint32_t *__restrict__ words,
                                                       ModArg md, uint8_t *__restrict__ out,
                                                       uint64_t *__restrict__ packed, uint32_t hi) {
-    constexpr int KPT = 2;
     const uint64_t span = (uint64_t)blockDim.x * KPT;
     for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
         uint32_t pos[KPT][7];
@@ -1026,11 +1025,12 @@ hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *w
     hipError_t e = hipSuccess;
     uint64_t p0 = 0;
     if (kb) {
-        const unsigned g0 = grid_for((n + 1) / 2, 256, o.grid_cap);
+        const uint32_t kpt0 = o.probe_phase0_kpt == 1 || o.probe_phase0_kpt == 4 ? (uint32_t)o.probe_phase0_kpt : 2u;
+        const unsigned g0 = grid_for((n + kpt0 - 1) / kpt0, 256, o.grid_cap);
         e = with_src(*kb, [&](auto src) {
             using S = decltype(src);
-            hipLaunchKernelGGL(k_probe_phase0<S>, dim3(g0), dim3(256), 0, s, src, n, words, md, out, packed,
-                               bound(1));
+            auto k0 = kpt0 == 1 ? k_probe_phase0<S, 1> : kpt0 == 4 ? k_probe_phase0<S, 4> : k_probe_phase0<S, 2>;
+            hipLaunchKernelGGL(k0, dim3(g0), dim3(256), 0, s, src, n, words, md, out, packed, bound(1));
             return hipGetLastError();
         });
         if (e != hipSuccess) return e;
