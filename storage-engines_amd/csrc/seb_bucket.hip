@@ -110,11 +110,13 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, Mo
     for (uint64_t k0 = t0; k0 < t1; k0 += round_keys) {
         const uint64_t k1 = k0 + round_keys < t1 ? k0 + round_keys : t1;
         uint32_t pos[KP][KQ];
+        bool valid[KP];
         if constexpr (KFIX > 0) {  // positions stay in registers between counting and placing
 #pragma unroll
             for (int r = 0; r < KP; ++r) {
                 const uint64_t i = k0 + (uint64_t)r * blockDim.x + threadIdx.x;
-                if (i < k1) {
+                valid[r] = i < k1;
+                if (valid[r]) {
                     uint64_t h1, h2;
                     if constexpr (kPre)
                         Src::hash_raw(kv[r], h1, h2);
@@ -153,14 +155,21 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, Mo
         }
         __syncthreads();
         if constexpr (KFIX > 0) {
+            // All slot claims first, then all writes: the atomics are independent and pipeline,
+            // where claim-then-write per position serialises on every atomic's return.
+            uint32_t slot[KP][KQ];
 #pragma unroll
-            for (int r = 0; r < KP; ++r) {
-                const uint64_t i = k0 + (uint64_t)r * blockDim.x + threadIdx.x;
-                if (i < k1) {
+            for (int r = 0; r < KP; ++r)
+                if (valid[r]) {
 #pragma unroll
-                    for (int q = 0; q < KQ; ++q) sorted[atomicAdd(&cursor[pos[r][q] >> kBktShift], 1u)] = pos[r][q];
+                    for (int q = 0; q < KQ; ++q) slot[r][q] = atomicAdd(&cursor[pos[r][q] >> kBktShift], 1u);
                 }
-            }
+#pragma unroll
+            for (int r = 0; r < KP; ++r)
+                if (valid[r]) {
+#pragma unroll
+                    for (int q = 0; q < KQ; ++q) sorted[slot[r][q]] = pos[r][q];
+                }
         } else {
             for (uint64_t i = k0 + threadIdx.x; i < k1; i += blockDim.x) {
                 uint64_t h1, h2;
