@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--bcast", default="packed", choices=["packed", "keys"],
-                    help="c2c3, N > 1: broadcast 8-B packed residues (hashed once on rank 0) or the 16-B keys")
+                    help="c2c3/c5, N > 1: broadcast 8-B packed residues (hashed once on rank 0) or the 16-B keys")
     ap.add_argument("--overlap", type=int, default=0,
                     help="c2c3/c4: build step j+1 (second filter buffer, own stream) while step j probes")
     for o in OPTIONS:
@@ -223,13 +223,32 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
     st.kernel_bytes = {"probe": 16.0 * n + shard.count * ((m + 7) // 8) + st.plane.element_size() * n}
     st.units_per_step = float(n)
     st.scaling = "strong"
-    st.broadcast_bufs = st.pbufs if world > 1 else None
     st.workload = ("C5: 64 SSTable filters (100K keys each, m=958,506, k=7) sharded over the GPUs; a 10M-key "
                    "batch RCCL-broadcast from rank 0, multi-filter probe, u64 masks all-gathered")
+    # N > 1: the 64 filters share (m, k), so the batch travels as 8-B packed residues (80 MB per step
+    # instead of 160 MB of keys): rank 0 packs batch j+2 in step j (seb_dev_pack_residues) and every
+    # rank probes the packed words of batch j (seb_dev_probe_multi_packed).
+    packed = world > 1 and args.bcast == "packed" and k == 7 and m < (1 << 29)
+    if packed:
+        st.bcast_lead = 2
+        st.packed = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(st.bcast_lead + 1)]
+        st.broadcast_bufs = st.packed
+        st.bcast_prologue = lambda b, buf: seb.dev_pack_residues(st.pk[0], m, k, buf)
+        st.kernel_bytes["probe"] = (24.0 * n if rank == 0 else 0.0) + 8.0 * n + shard.count * ((m + 7) // 8) + \
+            st.plane.element_size() * n
+        st.workload += " (batch as 8-B packed residues, hashed once on rank 0)"
+        st.pmc_key = "c5_packed"
+    else:
+        st.broadcast_bufs = st.pbufs if world > 1 else None
     st.parallelism = f"filters sharded {nf}/{world} per gpu, batch broadcast + mask all-gather (RCCL)"
 
     def probe(j, buf, target):
-        if shard.count:
+        if packed:
+            if rank == 0:  # the broadcast form of batch j + 2
+                seb.dev_pack_residues(st.pk[0], m, k, target)
+            if shard.count:
+                seb.dev_probe_multi_packed(buf, n, st.local, st.plane)
+        elif shard.count:
             seb.dev_probe_multi(st.pk[j % 2], st.local, st.plane)
         if world > 1:
             dist.all_gather(st.planes, st.plane)

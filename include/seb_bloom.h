@@ -118,6 +118,10 @@ int seb_dev_pack_residues(const seb_keys *keys, uint64_t num_bits, uint32_t num_
                           void *stream);
 int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, uint64_t num_bits,
                          uint32_t num_hashes, uint8_t *out, void *stream);
+/* Multi-filter probe of packed residues (seb_dev_probe_multi's mask layout); every filter must
+ * have the packed batch's (num_bits, num_hashes). */
+int seb_dev_probe_multi_packed(const uint64_t *packed, uint64_t n, const seb_filter_ref *filters, uint32_t num_filters,
+                               void *mask, uint32_t mask_bytes, void *stream);
 /* seb_dev_probe plus the batch's packed residues in one pass (the broadcast root's probe). */
 int seb_dev_probe_emit_packed(const seb_keys *keys, const uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
                               uint8_t *out, uint64_t *packed, void *stream);

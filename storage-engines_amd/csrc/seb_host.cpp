@@ -452,6 +452,26 @@ extern "C" int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *f
     return SEB_OK;
 }
 
+extern "C" int seb_dev_probe_multi_packed(const uint64_t *packed, uint64_t n, const seb_filter_ref *filters,
+                                          uint32_t nf, void *mask, uint32_t mask_bytes, void *stream) {
+    std::call_once(g_env_once, load_env);
+    int rc;
+    MultiArg ma;
+    if ((rc = fill_multi(filters, nf, mask_bytes, &ma, "seb_dev_probe_multi_packed"))) return rc;
+    for (uint32_t f = 0; f < nf; ++f)
+        if (ma.f[f].md.m != ma.f[0].md.m || ma.f[f].md.k != ma.f[0].md.k)
+            return fail(SEB_ERR_INVALID, "seb_dev_probe_multi_packed: filters must share (num_bits, num_hashes)");
+    if ((rc = check_packed_args(ma.f[0].md.m, ma.f[0].md.k, "seb_dev_probe_multi_packed"))) return rc;
+    if (n && (!packed || !mask)) return fail(SEB_ERR_INVALID, "seb_dev_probe_multi_packed: null pointer");
+    if (n == 0) return SEB_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t tb = ((ma.f[0].md.m + 31) / 32) * 32 * mask_bytes;
+    void *ws = nullptr;
+    if ((rc = cached_workspace(s, (tb + 255) & ~255ull, &ws))) return rc;
+    HIP_OR_FAIL(launch_probe_interleaved_packed(packed, n, ma, mask, mask_bytes, ws, s));
+    return SEB_OK;
+}
+
 static const uint32_t kLdsMax = 160 * 1024;
 
 extern "C" int seb_dev_build_many(const seb_keys *keys, const uint64_t *key_begin, const seb_filter_ref *filters,

@@ -119,6 +119,10 @@ hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s);
 uint64_t interleaved_bytes(const MultiArg &ma, uint32_t mask_bytes);
 hipError_t launch_probe_interleaved(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes, void *ws,
                                     hipStream_t s);
+// The same over packed residues (all filters share (m, k), k == 7, m < 2^kPackBits); `ws` holds
+// the table (interleaved_table_bytes).
+hipError_t launch_probe_interleaved_packed(const uint64_t *packed, uint64_t n, const MultiArg &ma, void *mask,
+                                           uint32_t mask_bytes, void *ws, hipStream_t s);
 hipError_t launch_build_many_lds(const KeyBatch &kb, const ManyArg &ma, uint32_t lds_bytes, hipStream_t s);
 
 // Packed residues (k == 7, m < 2^kPackBits): 8 bytes per key instead of the key itself.

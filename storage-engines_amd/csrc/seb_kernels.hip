@@ -695,6 +695,52 @@ __global__ __launch_bounds__(256) void k_probe_interleaved(Src src, uint64_t n, 
     }
 }
 
+// Interleaved multi-filter probe over packed residues (k_pack_residues' layout): the broadcast
+// form of a batch probed against same-size filters on several GPUs (C5 at N > 1).
+template <typename MaskT>
+__global__ __launch_bounds__(256) void k_probe_interleaved_packed(const uint64_t *__restrict__ packed, uint64_t n,
+                                                                  const MaskT *__restrict__ table, ModArg md,
+                                                                  MaskT *__restrict__ mask, uint32_t slice_shift,
+                                                                  uint32_t nslices) {
+    constexpr int KPT = 2;
+    const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
+    constexpr uint64_t kMask = (1ull << kPackBits) - 1;
+    const uint64_t span = (uint64_t)blockDim.x * KPT;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
+        uint32_t pos[KPT][7];
+        MaskT acc[KPT];
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            const uint64_t v = i < n ? __builtin_nontemporal_load(packed + i) : 0ull;
+            uint32_t x = (uint32_t)(v & kMask);
+            const uint32_t b = (uint32_t)((v >> kPackBits) & kMask), f = (uint32_t)(v >> (2 * kPackBits));
+            const uint32_t nb = m - b, bc = b >= c ? b - c : b + (m - c), nd = m - bc;
+            pos[r][0] = x;
+#pragma unroll
+            for (int q = 1; q < 7; ++q) {
+                const uint32_t d = (f >> (q - 1)) & 1u ? nd : nb;
+                const uint32_t t = x - d;
+                x = x >= d ? t : t + m;
+                pos[r][q] = x;
+            }
+            acc[r] = i < n ? (MaskT)~(MaskT)0 : (MaskT)0;
+        }
+        for (uint32_t sl = 0; sl < nslices; ++sl) {
+#pragma unroll
+            for (int r = 0; r < KPT; ++r)
+#pragma unroll
+                for (int q = 0; q < 7; ++q)
+                    if (acc[r] && (pos[r][q] >> slice_shift) == sl) acc[r] &= table[pos[r][q]];
+        }
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
+            if (i < n) mask[i] = acc[r];
+        }
+    }
+}
+
 // Batched build of independent small filters: one workgroup per filter, the whole filter held
 // in LDS (ds_or_b32 atomics, no global atomics), then OR-merged into HBM with coalesced
 // accesses.  Filters too large for LDS go through k_build.
@@ -896,6 +942,33 @@ static hipError_t interleaved_mask(const KeyBatch &kb, const MultiArg &ma, void 
                            md, (MaskT *)mask, shift, nsl);
         return hipGetLastError();
     });
+}
+
+template <typename MaskT>
+static hipError_t interleaved_mask_packed(const uint64_t *packed, uint64_t n, const MultiArg &ma, void *mask, void *ws,
+                                          hipStream_t s) {
+    const ModArg &md = ma.f[0].md;
+    const uint64_t nwords = (md.m + 31) / 32;
+    MaskT *table = (MaskT *)ws;
+    hipLaunchKernelGGL((k_interleave<MaskT>), dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, ma, nwords, md.m,
+                       table);
+    const uint32_t shift = 21 - (sizeof(MaskT) == 1 ? 0 : sizeof(MaskT) == 2 ? 1 : sizeof(MaskT) == 4 ? 2 : 3);
+    const uint32_t nsl = (uint32_t)((md.m + (1ull << shift) - 1) >> shift);
+    const unsigned g = grid_for((n + 1) / 2, 256, options().grid_cap);
+    hipLaunchKernelGGL((k_probe_interleaved_packed<MaskT>), dim3(g), dim3(256), 0, s, packed, n, (const MaskT *)table, md,
+                       (MaskT *)mask, shift, nsl);
+    return hipGetLastError();
+}
+
+hipError_t launch_probe_interleaved_packed(const uint64_t *packed, uint64_t n, const MultiArg &ma, void *mask,
+                                           uint32_t mask_bytes, void *ws, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    switch (mask_bytes) {
+        case 1: return interleaved_mask_packed<uint8_t>(packed, n, ma, mask, ws, s);
+        case 2: return interleaved_mask_packed<uint16_t>(packed, n, ma, mask, ws, s);
+        case 4: return interleaved_mask_packed<uint32_t>(packed, n, ma, mask, ws, s);
+        default: return interleaved_mask_packed<uint64_t>(packed, n, ma, mask, ws, s);
+    }
 }
 
 uint64_t interleaved_bytes(const MultiArg &ma, uint32_t mask_bytes) {

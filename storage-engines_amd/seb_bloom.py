@@ -107,6 +107,7 @@ _SIGS = {
     "seb_dev_pack_residues": (_i, [C.POINTER(seb_keys), _u64, _u32, _vp, _vp]),
     "seb_dev_probe_packed": (_i, [_vp, _u64, _vp, _u64, _u32, _vp, _vp]),
     "seb_dev_probe_emit_packed": (_i, [C.POINTER(seb_keys), _vp, _u64, _u32, _vp, _vp, _vp]),
+    "seb_dev_probe_multi_packed": (_i, [_vp, _u64, C.POINTER(seb_filter_ref), _u32, _vp, _u32, _vp]),
     "seb_timer_create": (_i, [C.POINTER(_vp)]),
     "seb_timer_record": (_i, [_vp, _vp]),
     "seb_timer_elapsed_ms": (_i, [_vp, _vp, C.POINTER(C.c_float)]),
@@ -457,6 +458,13 @@ def dev_probe_emit_packed(keys: seb_keys, words, m: int, k: int, out, packed, st
     """dev_probe that also writes the batch's packed residues (the broadcast root's probe)."""
     check(lib().seb_dev_probe_emit_packed(C.byref(keys), words.data_ptr(), m, k, out.data_ptr(), packed.data_ptr(),
                                           _stream(stream)))
+
+
+def dev_probe_multi_packed(packed, n: int, filters: list[tuple[object, int, int]], mask, stream=None) -> None:
+    """dev_probe_multi over packed residues (filters of one (m, k); k == 7, m < 2^29)."""
+    refs = (seb_filter_ref * len(filters))(*[seb_filter_ref(w.data_ptr(), m, k, 0) for w, m, k in filters])
+    check(lib().seb_dev_probe_multi_packed(packed.data_ptr(), n, refs, len(filters), mask.data_ptr(),
+                                           mask.element_size(), _stream(stream)))
 
 
 def dev_probe_multi(keys: seb_keys, filters: list[tuple[object, int, int]], mask, stream=None) -> None:

@@ -255,6 +255,47 @@ def test_sliced_probe_gather_orders(seb, golden, torch_cuda):
             assert got[ragged] == 7, (mode, kpt)  # nothing written past the batch
 
 
+def test_multi_packed_matches_multi(seb, golden, torch_cuda):
+    """The C5 multi-filter probe over packed residues equals the probe over the keys (golden C5
+    digest for 64 filters, u64 masks) and the oracle for 8 filters with a ragged batch; mixed
+    filter sizes are rejected."""
+    torch = torch_cuda
+    nf, per, n = 64, 100_000, 10_000_000
+    m, k = seb.params(per, 0.01)
+    fkeys = torch.from_numpy(kg.key16(np.arange(nf * per))).cuda()
+    filters = [(seb.new_words(m), m, k) for _ in range(nf)]
+    seb.dev_build_many(seb.dev_keys(fkeys, n=nf * per, stride=16), [j * per for j in range(nf + 1)], filters)
+    q = np.arange(n, dtype=np.int64)
+    half = q // 2
+    pk = seb.dev_keys(torch.from_numpy(kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf,
+                                                          nf * per + q))).cuda(), n=n, stride=16)
+    packed = torch.zeros(n, dtype=torch.int64, device="cuda")
+    seb.dev_pack_residues(pk, m, k, packed)
+    mask = torch.zeros(n, dtype=torch.int64, device="cuda")
+    seb.dev_probe_multi_packed(packed, n, filters, mask)
+    torch.cuda.synchronize()
+    assert sha(mask.cpu().numpy().view(np.uint64).astype("<u8").tobytes()) == golden["c5"]["mask_sha256"]
+    # 8 filters, u8 masks, ragged batch, against the oracle
+    nn = 100_003
+    sub = filters[:8]
+    keys8 = kg.key16(np.where(q[:nn] % 2 == 0, (half[:nn] % 8) * per + half[:nn] // 8, nf * per + q[:nn]))
+    pk8 = seb.dev_keys(torch.from_numpy(keys8).cuda(), n=nn, stride=16)
+    p8 = torch.zeros(nn, dtype=torch.int64, device="cuda")
+    seb.dev_pack_residues(pk8, m, k, p8)
+    m8 = torch.full((nn + 1,), 7, dtype=torch.uint8, device="cuda")
+    seb.dev_probe_multi_packed(p8, nn, sub, m8)
+    torch.cuda.synchronize()
+    host = [(seb.words_to_bits(w, m), m, k) for w, m, k in sub]
+    ref = oc.probe_multi(host, keys8, nn, stride=16)
+    got = m8.cpu().numpy()
+    assert np.array_equal(got[:nn].astype(np.uint64), ref)
+    assert got[nn] == 7
+    m2, k2 = seb.params(per + 1, 0.01)
+    with pytest.raises(seb.SebError):
+        seb.dev_probe_multi_packed(p8, nn, sub + [(seb.new_words(m2), m2, k2)],
+                                   torch.zeros(nn, dtype=torch.int16, device="cuda"))
+
+
 def unpack_positions(packed: np.ndarray, m: int) -> np.ndarray:
     """Test-side decoding of seb_dev_pack_residues' words into the 7 positions (the recurrence
     of for_positions, in Python integers)."""
