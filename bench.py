@@ -13,8 +13,8 @@ batch travels as 8-byte packed residues that rank 0's own probe emits (--bcast p
 (build + probe keys over all ranks) / max-over-ranks wall time, inputs already resident in HBM.
 c4: the same with variable-length keys (8-256 B, zipf); no broadcast.
 c5: 64 compaction-sized filters (100K keys each) sharded over the ranks, a 10M-key batch
-broadcast from rank 0, multi-filter probe, masks all-gathered (strong scaling; value = batch
-keys / s).
+broadcast from rank 0, multi-filter probe, answer planes gathered to rank 0 (strong scaling;
+value = batch keys / s).
 
 Printed (rank 0): one JSON line with the metric, a `roofline` object for the dominant kernel
 (algorithmic bytes / hipEvent-measured launch time on the launch stream) and a `cpu_baseline`
@@ -224,7 +224,7 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
     st.units_per_step = float(n)
     st.scaling = "strong"
     st.workload = ("C5: 64 SSTable filters (100K keys each, m=958,506, k=7) sharded over the GPUs; a 10M-key "
-                   "batch RCCL-broadcast from rank 0, multi-filter probe, u64 masks all-gathered")
+                   "batch RCCL-broadcast from rank 0, multi-filter probe, answer planes gathered to rank 0")
     # N > 1: the 64 filters share (m, k), so the batch travels as 8-B packed residues (80 MB per step
     # instead of 160 MB of keys): rank 0 packs batch j+2 in step j (seb_dev_pack_residues) and every
     # rank probes the packed words of batch j (seb_dev_probe_multi_packed).
@@ -240,7 +240,7 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
         st.pmc_key = "c5_packed"
     else:
         st.broadcast_bufs = st.pbufs if world > 1 else None
-    st.parallelism = f"filters sharded {nf}/{world} per gpu, batch broadcast + mask all-gather (RCCL)"
+    st.parallelism = f"filters sharded {nf}/{world} per gpu, batch broadcast + plane gather (RCCL)"
 
     def probe(j, buf, target):
         if packed:
@@ -250,8 +250,8 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
                 seb.dev_probe_multi_packed(buf, n, st.local, st.plane)
         elif shard.count:
             seb.dev_probe_multi(st.pk[j % 2], st.local, st.plane)
-        if world > 1:
-            dist.all_gather(st.planes, st.plane)
+        if world > 1:  # only rank 0 assembles masks: gather the answer planes there
+            dist.gather(st.plane, gather_list=st.planes if rank == 0 else None, dst=0)
 
     def parity(j):
         if n != 10_000_000 or rank != 0:
