@@ -82,6 +82,7 @@ int seb_abi_version(void);
  *   "probe_phases"    phased probe (probe_mode 8): phases, 0 = one per 4 MiB of filter
  *   "probe_persistent" sliced probe: persistent 1024-thread workgroups (0 = off)
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
+ *   "multiget_pass_kib" registry MultiGet: filter bytes per pass (0 = one pass over all files)
  *   "scatter_threads", "scatter_kpt"  radix-partitioned build: workgroup size, keys per thread
  *   "stream_nt"       non-temporal loads of 16-B key batches (0/1)
  *   "varlen_prehash_min_keys", "varlen_sort_min_keys"  variable-length batches: LDS pre-hash and

@@ -132,6 +132,7 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     else if (!strcmp(name, "probe_phases") && value >= 0 && value <= 64) o.probe_phases = (int)value;
     else if (!strcmp(name, "probe_phase0_pct") && value >= 0 && value <= 90) o.probe_phase0_pct = (int)value;
     else if (!strcmp(name, "probe_phase0_kpt") && (value == 1 || value == 2 || value == 4)) o.probe_phase0_kpt = (int)value;
+    else if (!strcmp(name, "multiget_pass_kib") && value >= 0 && value <= (1 << 22)) o.multiget_pass_kib = (int)value;
     else if (!strcmp(name, "wal_lds_kib") && (value == 36 || value == 48)) o.wal_lds_kib = (int)value;
     else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
@@ -159,6 +160,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "probe_phases")) *value = o.probe_phases;
     else if (!strcmp(name, "probe_phase0_pct")) *value = o.probe_phase0_pct;
     else if (!strcmp(name, "probe_phase0_kpt")) *value = o.probe_phase0_kpt;
+    else if (!strcmp(name, "multiget_pass_kib")) *value = o.multiget_pass_kib;
     else if (!strcmp(name, "wal_lds_kib")) *value = o.wal_lds_kib;
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;
@@ -1101,6 +1103,8 @@ struct seb_registry {
     DevBuf dslots, dranges;
     uint32_t nslots = 0;
     RegLayout layout{};
+    std::vector<uint32_t> passes;  // MultiGet pass bounds over the lookup-ordered slots
+    int pass_kib = -1;             // multiget_pass_kib the bounds were computed for
     seb_ctx *ctx = nullptr;
 };
 
@@ -1201,8 +1205,32 @@ static std::vector<const RegEntry *> lookup_order(const seb_registry *r) {
     return v;
 }
 
+// Group the lookup-ordered slots into MultiGet passes of at most multiget_pass_kib of filter
+// words each (a larger filter gets a pass of its own); 0 = one pass.
+static void plan_passes(seb_registry *r, const std::vector<uint64_t> &bytes) {
+    const uint64_t budget = (uint64_t)options().multiget_pass_kib * 1024;
+    r->passes.assign(1, 0u);
+    uint64_t acc = 0;
+    for (uint32_t i = 0; i < bytes.size(); ++i) {
+        if (budget && i > r->passes.back() && acc + bytes[i] > budget) {
+            r->passes.push_back(i);
+            acc = 0;
+        }
+        acc += bytes[i];
+    }
+    r->passes.push_back((uint32_t)bytes.size());
+    r->pass_kib = options().multiget_pass_kib;
+}
+
 static int sync_registry_locked(seb_registry *r) {
-    if (!r->dirty) return SEB_OK;
+    if (!r->dirty) {
+        if (r->pass_kib != options().multiget_pass_kib) {  // the knob changed since the last sync
+            std::vector<uint64_t> bytes;
+            for (const RegEntry *e : lookup_order(r)) bytes.push_back(seb_words_bytes(e->m));
+            plan_passes(r, bytes);
+        }
+        return SEB_OK;
+    }
     HIP_OR_FAIL(hipSetDevice(r->device));
     auto order = lookup_order(r);
     std::vector<RegSlot> slots;
@@ -1250,6 +1278,9 @@ static int sync_registry_locked(seb_registry *r) {
     if (!ranges.empty()) HIP_OR_FAIL(hipMemcpy(r->dranges.p, ranges.data(), ranges.size(), hipMemcpyHostToDevice));
     r->nslots = (uint32_t)slots.size();
     r->layout = lay;
+    std::vector<uint64_t> bytes;
+    for (const RegEntry *e : order) bytes.push_back(seb_words_bytes(e->m));
+    plan_passes(r, bytes);
     r->dirty = false;
     return SEB_OK;
 }
@@ -1278,7 +1309,8 @@ extern "C" int seb_registry_multiget_dev(seb_registry *r, const seb_keys *keys, 
     std::lock_guard<std::mutex> g(r->mu);
     if ((rc = sync_registry_locked(r))) return rc;
     HIP_OR_FAIL(launch_multiget(key_batch(keys), (const RegSlot *)r->dslots.p, r->nslots, r->layout,
-                                (const uint8_t *)r->dranges.p, maybe, (hipStream_t)stream));
+                                (const uint8_t *)r->dranges.p, maybe, r->passes.data(),
+                                (uint32_t)r->passes.size() - 1, (hipStream_t)stream));
     return SEB_OK;
 }
 
@@ -1302,7 +1334,8 @@ extern "C" int seb_registry_multiget(seb_registry *r, const seb_keys *kb, uint64
         if ((rc = c->out[b].reserve(dk.n * 8))) return rc;
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));
         HIP_OR_FAIL(launch_multiget(dk, (const RegSlot *)r->dslots.p, r->nslots, r->layout,
-                                    (const uint8_t *)r->dranges.p, (uint64_t *)c->out[b].p, c->s_comp));
+                                    (const uint8_t *)r->dranges.p, (uint64_t *)c->out[b].p, r->passes.data(),
+                                    (uint32_t)r->passes.size() - 1, c->s_comp));
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
         HIP_OR_FAIL(hipMemcpyAsync(maybe + chunks[j].i0, c->out[b].p, dk.n * 8, hipMemcpyDeviceToHost, c->s_d2h));

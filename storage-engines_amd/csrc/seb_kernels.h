@@ -69,15 +69,18 @@ hipError_t launch_route_partition(const KeyBatch &kb, uint32_t bits, uint32_t *p
                                   uint16_t *shard_out, void *ws, uint64_t ws_bytes, hipStream_t s);
 hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mode, uint32_t *crc, uint8_t *ok,
                           hipStream_t s);
+// Passes: slots [pass_bounds[p], pass_bounds[p+1]) per launch (npasses == 0: one pass, all slots).
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
-                           const uint8_t *ranges, uint64_t *maybe, hipStream_t s);
+                           const uint8_t *ranges, uint64_t *maybe, const uint32_t *pass_bounds, uint32_t npasses,
+                           hipStream_t s);
 
 // Process-wide tuning knobs (seb_set_option).
 struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed)
-    int multi_interleave = 1;
+    int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
+    int multiget_pass_kib = 0;    // MultiGet: filter bytes per pass (0 = one pass; passes measured slower)
     uint64_t varlen_sort_min_keys = INT64_MAX;  // length-bucketed order (measured slower; off by default)
-    uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys     // multi-filter probe: interleaved table when filters share (m, k)
+    uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys
     int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)
     int probe_kpt = 2;            // k == 7 probes: keys per thread (1, 2, 4)
     int probe_slice_shift = 19;   // k == 7, m < 2^32: sliced probe with 2^shift-word (2 MiB) slices (0 = off)

@@ -40,19 +40,30 @@ __device__ __forceinline__ int cmp_key(const uint8_t *key, uint32_t klen, uint64
     return (int)klen - (int)blen;
 }
 
+// MayContain of one filter, with the reference's early exit (lsm/bloom.go:86-89): a position is
+// gathered only while every bit so far is set.  Gathering all k unconditionally cost 42 L2
+// requests per key over a MultiGet's 6 filter tests (profiles/r01y_lsm_pmc.csv); the early exit
+// leaves ~1.9 per filter that does not hold the key.
 template <int KFIX, bool M32>
 __device__ __forceinline__ uint32_t test_filter(const RegSlot &sl, uint64_t h1, uint64_t h2) {
     uint32_t acc = 1u;
     for_positions<KFIX, M32>(h1, h2, sl.md, sl.md.k, [&](uint32_t, uint64_t p) {
-        acc &= sl.words[p >> 5] >> (uint32_t)(p & 31);
+        if (acc & 1u) acc &= sl.words[p >> 5] >> (uint32_t)(p & 31);
     });
     return acc & 1u;
 }
 
+// One pass tests only the filters of slots [pass_lo, pass_hi) (lookup order).  With
+// multiget_pass_kib the host groups slots into passes of that many filter bytes, so the filters a
+// pass gathers from stay in each XCD's L2 (the phased probe's idea, seb_kernels.hip).  Every pass
+// re-reads, re-hashes and re-walks every key, which costs more than the L2 misses it saves on the
+// C-LSM layout (1.46 ms in one pass, 2.12 ms in 4 MiB passes): one pass is the default.  Pass 0
+// writes the mask and later passes OR into it.
 template <typename Src, int KFIX, bool M32>
 __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const RegSlot *__restrict__ gslots,
                                                   uint32_t nslots, RegLayout lay, const uint8_t *__restrict__ ranges,
-                                                  uint64_t *__restrict__ maybe) {
+                                                  uint64_t *__restrict__ maybe, uint32_t pass_lo, uint32_t pass_hi,
+                                                  uint32_t accumulate) {
     __shared__ RegSlot slots[kMaxSlots];
     for (uint32_t s = threadIdx.x; s < nslots; s += blockDim.x) slots[s] = gslots[s];
     __syncthreads();
@@ -71,11 +82,13 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         src.hash(i, h1, h2);
         const uint64_t k0 = be64(key, klen), k1 = klen > 8 ? be64(key + 8, klen - 8) : 0ull;
         uint64_t mask = 0;
-        for (uint32_t s = lay.lo[0]; s < lay.hi[0]; ++s)  // every L0 file
+        const uint32_t s0 = lay.lo[0] > pass_lo ? lay.lo[0] : pass_lo;
+        const uint32_t s1 = lay.hi[0] < pass_hi ? lay.hi[0] : pass_hi;
+        for (uint32_t s = s0; s < s1; ++s)  // every L0 file (of this pass)
             mask |= (uint64_t)test_filter<KFIX, M32>(slots[s], h1, h2) << slots[s].slot;
         for (uint32_t L = 1; L < 5; ++L) {
             uint32_t lo = lay.lo[L], hi = lay.hi[L];
-            if (lo == hi) continue;
+            if (lo == hi || hi <= pass_lo || lo >= pass_hi) continue;  // no file of this level in the pass
             int hit = -1;
             if (lay.nonoverlap >> L & 1u) {
                 // last file with MinKey <= key; it is the only one that can cover the key
@@ -100,27 +113,42 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                         hit = (int)s;
                 }
             }
-            if (hit >= 0) mask |= (uint64_t)test_filter<KFIX, M32>(slots[hit], h1, h2) << slots[hit].slot;
+            if (hit >= (int)pass_lo && hit < (int)pass_hi)
+                mask |= (uint64_t)test_filter<KFIX, M32>(slots[hit], h1, h2) << slots[hit].slot;
         }
-        maybe[i] = mask;
+        if (!accumulate)
+            maybe[i] = mask;
+        else if (mask)
+            maybe[i] |= mask;
     }
 }
 
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
-                           const uint8_t *ranges, uint64_t *maybe, hipStream_t s) {
+                           const uint8_t *ranges, uint64_t *maybe, const uint32_t *pass_bounds, uint32_t npasses,
+                           hipStream_t s) {
     if (kb.n == 0) return hipSuccess;
     if (nslots > kMaxSlots) return hipErrorInvalidValue;
     uint64_t g = (kb.n + 255) / 256;
     if (g > 65536) g = 65536;
+    const uint32_t one[2] = {0u, nslots};
+    if (npasses == 0) {
+        pass_bounds = one;
+        npasses = 1;
+    }
     return with_src(kb, [&](auto src) {
         using S = decltype(src);
-        if (lay.all_k7_m32)
-            hipLaunchKernelGGL((k_multiget<S, 7, true>), dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay,
-                               ranges, maybe);
-        else
-            hipLaunchKernelGGL((k_multiget<S, 0, false>), dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots,
-                               lay, ranges, maybe);
-        return hipGetLastError();
+        for (uint32_t p = 0; p < npasses; ++p) {
+            const uint32_t lo = pass_bounds[p], hi = pass_bounds[p + 1], acc = p > 0 ? 1u : 0u;
+            if (lay.all_k7_m32)
+                hipLaunchKernelGGL((k_multiget<S, 7, true>), dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots,
+                                   lay, ranges, maybe, lo, hi, acc);
+            else
+                hipLaunchKernelGGL((k_multiget<S, 0, false>), dim3((unsigned)g), dim3(256), 0, s, src, kb, slots,
+                                   nslots, lay, ranges, maybe, lo, hi, acc);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
     });
 }
 

@@ -744,7 +744,14 @@ def _lsm_get_model(files, key: bytes):
     return mask
 
 
-def test_registry_multiget_matches_lsm_get_walk(seb, torch_cuda):
+@pytest.fixture(params=[0, 4096, 1], ids=["one-pass", "passes-4MiB", "pass-per-file"])
+def multiget_passes(request, seb):
+    """MultiGet split into passes of filter bytes (multiget_pass_kib): the masks never change."""
+    with seb.option("multiget_pass_kib", request.param):
+        yield request.param
+
+
+def test_registry_multiget_matches_lsm_get_walk(seb, torch_cuda, multiget_passes):
     torch = torch_cuda
     rng = np.random.default_rng(17)
     reg = seb.Registry(0)
@@ -801,7 +808,7 @@ def test_registry_multiget_matches_lsm_get_walk(seb, torch_cuda):
     reg.close()
 
 
-def test_registry_multiget_overlap_long_keys_generic_k(seb, torch_cuda):
+def test_registry_multiget_overlap_long_keys_generic_k(seb, torch_cuda, multiget_passes):
     """The branches the LSM bench layout does not reach: an overlapping level (the reference's
     first-cover linear scan, lsm/lsm.go:184-196), range keys longer than the 16-byte LDS prefix
     that tie on it (HBM tail compare), prefix-of relations, and filters with k != 7."""
