@@ -86,8 +86,9 @@ __global__ __launch_bounds__(256) void k_probe(Src src, uint64_t n, const uint32
             uint64_t h1, h2;
             src.hash(i, h1, h2);
             uint32_t acc = 1u;
-            for_positions<0, M32>(h1, h2, md, md.k,
-                                  [&](uint32_t, uint64_t p) { acc &= words[p >> 5] >> (uint32_t)(p & 31); });
+            for_positions<0, M32>(h1, h2, md, md.k, [&](uint32_t, uint64_t p) {
+                if (acc & 1u) acc &= words[p >> 5] >> (uint32_t)(p & 31);  // MayContain's early exit
+            });
             out[src.index(i)] = (uint8_t)(acc & 1u);
         }
     }
@@ -621,7 +622,8 @@ __global__ __launch_bounds__(256) void k_probe_multi(Src src, uint64_t n, MultiA
                     const uint32_t *wd = ma.f[f].words;
                     uint32_t acc = 1u;
 #pragma unroll
-                    for (int q = 0; q < KFIX; ++q) acc &= wd[pos[q] >> 5] >> (uint32_t)(pos[q] & 31);
+                    for (int q = 0; q < KFIX; ++q)  // MayContain's early exit (lsm/bloom.go:86-89)
+                        if (acc & 1u) acc &= wd[pos[q] >> 5] >> (uint32_t)(pos[q] & 31);
                     w |= (MaskT)(acc & 1u) << f;
                 }
             }
@@ -629,8 +631,9 @@ __global__ __launch_bounds__(256) void k_probe_multi(Src src, uint64_t n, MultiA
             for (uint32_t f = 0; f < ma.nf; ++f) {
                 const uint32_t *wd = ma.f[f].words;
                 uint32_t acc = 1u;
-                for_positions<KFIX, M32>(h1, h2, ma.f[f].md, ma.f[f].md.k,
-                                         [&](uint32_t, uint64_t p) { acc &= wd[p >> 5] >> (uint32_t)(p & 31); });
+                for_positions<KFIX, M32>(h1, h2, ma.f[f].md, ma.f[f].md.k, [&](uint32_t, uint64_t p) {
+                    if (acc & 1u) acc &= wd[p >> 5] >> (uint32_t)(p & 31);
+                });
                 w |= (MaskT)(acc & 1u) << f;
             }
         }
