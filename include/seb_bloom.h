@@ -87,6 +87,8 @@ int seb_abi_version(void);
  *   "stream_nt"       non-temporal loads of 16-B key batches (0/1)
  *   "varlen_prehash_min_keys", "varlen_sort_min_keys"  variable-length batches: LDS pre-hash and
  *                     global length-sort thresholds
+ *   "varlen_hash_keys", "varlen_hash_win"  LDS pre-hash: keys per workgroup (256, 512) and window
+ *                     bytes per key (64, 72, 80)
  * Environment variables SEB_<NAME> (upper case) set the initial values. */
 int seb_set_option(const char *name, int64_t value);
 int seb_get_option(const char *name, int64_t *value);

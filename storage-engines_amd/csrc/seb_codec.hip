@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "seb_device.h"
 #include "seb_kernels.h"
 
 namespace seb {
@@ -135,16 +136,6 @@ __global__ __launch_bounds__(1024) void k_route_scan_rows(uint32_t *__restrict__
     if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
-// Lanes of this wave holding the same shard as this lane (live lanes only).
-__device__ __forceinline__ uint64_t shard_peers(bool live, uint32_t s, uint32_t bits) {
-    uint64_t peers = __ballot(live);
-    for (uint32_t b = 0; b < bits; ++b) {
-        const uint64_t on = __ballot(live && ((s >> b) & 1u));
-        peers &= ((s >> b) & 1u) ? on : ~on;
-    }
-    return peers;
-}
-
 // LDS: wrun[kRouteWaves][nbins] | wsum[kRouteWaves]
 __global__ __launch_bounds__(kRouteThreads) void k_route_scatter(const uint16_t *__restrict__ shard, uint64_t n,
                                                                  uint32_t nbins, uint32_t bits, uint32_t ntiles,
@@ -197,7 +188,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route_scatter(const uint16_t 
 #pragma unroll
     for (uint32_t r = 0; r < kRoutePerLane; ++r) {
         const bool live = sv[r] != 0xffffffffu;
-        pk[r] = shard_peers(live, sv[r], bits);
+        pk[r] = wave_peers(live, sv[r], bits);
         if (live && (pk[r] & lt) == 0ull) wrun[wid * nbins + sv[r]] += (uint32_t)__popcll(pk[r]);
     }
     __syncthreads();

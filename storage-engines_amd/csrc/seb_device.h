@@ -230,4 +230,20 @@ static inline hipError_t with_src(const KeyBatch &kb, Fn &&fn) {
     return fn(KeysStrideB{kb.data, kb.stride});
 }
 
+// Lanes of this wave holding the same `bits`-bit value v as this lane (live lanes only): one ballot
+// per bit, so lanes can share one LDS atomic per distinct value instead of one per lane.
+__device__ __forceinline__ uint64_t wave_peers(bool live, uint32_t v, uint32_t bits) {
+    uint64_t peers = __ballot(live);
+    for (uint32_t b = 0; b < bits; ++b) {
+        const uint64_t on = __ballot(live && ((v >> b) & 1u));
+        peers &= ((v >> b) & 1u) ? on : ~on;
+    }
+    return peers;
+}
+
+// Number of lanes of `mask` below this lane.
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
 }  // namespace seb

@@ -133,6 +133,10 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     else if (!strcmp(name, "probe_phase0_pct") && value >= 0 && value <= 90) o.probe_phase0_pct = (int)value;
     else if (!strcmp(name, "probe_phase0_kpt") && (value == 1 || value == 2 || value == 4)) o.probe_phase0_kpt = (int)value;
     else if (!strcmp(name, "multiget_pass_kib") && value >= 0 && value <= (1 << 22)) o.multiget_pass_kib = (int)value;
+    else if (!strcmp(name, "varlen_hash_keys") && (value == 256 || value == 512))
+        o.varlen_hash_keys = (uint32_t)value;
+    else if (!strcmp(name, "varlen_hash_win") && (value == 64 || value == 72 || value == 80))
+        o.varlen_hash_win = (uint32_t)value;
     else if (!strcmp(name, "wal_lds_kib") && (value == 36 || value == 48)) o.wal_lds_kib = (int)value;
     else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
@@ -161,6 +165,8 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "probe_phase0_pct")) *value = o.probe_phase0_pct;
     else if (!strcmp(name, "probe_phase0_kpt")) *value = o.probe_phase0_kpt;
     else if (!strcmp(name, "multiget_pass_kib")) *value = o.multiget_pass_kib;
+    else if (!strcmp(name, "varlen_hash_keys")) *value = o.varlen_hash_keys;
+    else if (!strcmp(name, "varlen_hash_win")) *value = o.varlen_hash_win;
     else if (!strcmp(name, "wal_lds_kib")) *value = o.wal_lds_kib;
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;

@@ -92,81 +92,125 @@ __global__ __launch_bounds__(kPermThreads) void k_len_scatter(const uint64_t *__
 // read is an LDS access instead of an L2/fabric round trip.  A span larger than the LDS window
 // is hashed straight from HBM in input order.  Build and probe then read 16 B per key
 // (KeysHashed), exactly like the fixed 16-B path.
-constexpr uint32_t kHashKeys = 512;
-constexpr uint32_t kHashLds = 40 * 1024;
+// Funnel walk of one key staged in LDS: every 4 key bytes come from two aligned LDS dwords
+// (v_alignbyte), so all full words take the same path whatever the key's alignment.
+struct Funnel {
+    uint32_t wi, cur, sh, len;
+    uint64_t h1, h2;
+    __device__ __forceinline__ void init(const uint32_t *lds, uint32_t b, uint32_t n) {
+        wi = b >> 2;
+        sh = b & 3u;
+        len = n;
+        cur = lds[wi];
+        h1 = kFnvOffset;
+        h2 = kFnvOffset;
+    }
+    __device__ __forceinline__ void step(const uint32_t *lds) {  // the next 4 bytes
+        const uint32_t nxt = lds[++wi];
+        fnv_word(__builtin_amdgcn_alignbyte(nxt, cur, sh), h1, h2);
+        cur = nxt;
+    }
+    __device__ __forceinline__ void tail(const uint32_t *lds) {  // the last len % 4 bytes
+        const uint32_t r = len & 3u;
+        if (r) fnv_word_part(__builtin_amdgcn_alignbyte(lds[wi + 1], cur, sh), 0u, r, h1, h2);
+    }
+};
 
-__global__ __launch_bounds__(kHashKeys) void k_hash_varlen(const uint8_t *__restrict__ data,
-                                                           const uint64_t *__restrict__ off, uint64_t n,
-                                                           uint4 *__restrict__ hashes) {
+// A workgroup owns KEYS consecutive keys and an LDS window of WIN bytes per key (C4 keys average
+// 40 B).  It copies the keys' byte span into LDS, counting-sorts the keys by dword length so each
+// wave walks keys of about one length, and lane t hashes sorted key t with the funnel walk.  The
+// work per workgroup is short, so its time is mostly the chain of dependent memory round trips:
+// each thread loads its own key's offsets up front (with the span bounds), then the span; the
+// sorted slots carry (start, length, key) in LDS so the hash phase touches HBM only to store.
+template <uint32_t KEYS, uint32_t WIN>
+__global__ __launch_bounds__(KEYS) void k_hash_varlen(const uint8_t *__restrict__ data,
+                                                      const uint64_t *__restrict__ off, uint64_t n,
+                                                      uint4 *__restrict__ hashes) {
+    constexpr uint32_t kHashLds = KEYS * WIN;
+    static_assert(kHashLds % 16 == 0 && kHashLds + 16 < 65536, "window offsets are 16-bit");
     __shared__ uint4 stage[kHashLds / 16 + 1];  // +16 B: the funnel walk reads one dword past a key
     __shared__ uint32_t cur[kLenBuckets];
-    __shared__ uint16_t order[kHashKeys];
-    const uint64_t k0 = (uint64_t)blockIdx.x * kHashKeys;
-    const uint64_t k1 = k0 + kHashKeys < n ? k0 + kHashKeys : n;
+    __shared__ uint32_t slot_key[KEYS];  // sorted slot -> start byte in the window << 16 | length
+    __shared__ uint16_t slot_idx[KEYS];  // sorted slot -> key within the workgroup
+    const uint32_t t = threadIdx.x;
+    const uint64_t k0 = (uint64_t)blockIdx.x * KEYS;
+    const uint64_t k1 = k0 + KEYS < n ? k0 + KEYS : n;
     const uint32_t cnt = (uint32_t)(k1 - k0);
+    const bool mine = t < cnt;
+    const uint64_t ks = mine ? off[k0 + t] : 0, ke = mine ? off[k0 + t + 1] : 0;
     const uintptr_t s0 = (uintptr_t)(data + off[k0]);
     const uintptr_t s1 = (uintptr_t)(data + off[k1]);
     const uintptr_t base = s0 & ~(uintptr_t)15;
     const uint64_t chunks = (s1 - base + 15) >> 4;
-    const bool staged = chunks * 16 <= kHashLds;  // block-uniform
-    uint64_t i = k0 + threadIdx.x;
-    if (staged) {
-        if (threadIdx.x < kLenBuckets) cur[threadIdx.x] = 0u;
-        for (uint64_t c = threadIdx.x; c < chunks; c += blockDim.x) stage[c] = ((const uint4 *)base)[c];
-        __syncthreads();
-        const uint32_t bk = threadIdx.x < cnt ? len_bucket(off, k0 + threadIdx.x) : 0u;
-        if (threadIdx.x < cnt) atomicAdd(&cur[bk], 1u);
-        __syncthreads();
-        if (threadIdx.x < 64) {  // exclusive scan of the 65 bucket counts by one wave
-            const uint32_t lane = threadIdx.x;
-            uint32_t c = cur[lane] + (lane == 63 ? cur[64] : 0u);
-            uint32_t v = c;
+    if (chunks * 16 > kHashLds) {  // block-uniform: a span larger than the window, straight from HBM
+        if (mine) {
+            uint64_t h1, h2;
+            fnv_range(data, ks, ke, h1, h2);
+            hashes[k0 + t] = make_uint4((uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32));
+        }
+        return;
+    }
+    if (t < kLenBuckets) cur[t] = 0u;
+    for (uint32_t c = t; c < (uint32_t)chunks; c += KEYS) stage[c] = ((const uint4 *)base)[c];
+    const uint32_t len = (uint32_t)(ke - ks);
+    const uint32_t dw = (len + 3) >> 2;
+    const uint32_t bk = dw > 64 ? 64u : dw;
+    // a wave whose keys all fall in one length bucket (uniform-length batches) takes its slots with
+    // one LDS atomic instead of 64 serialised on one counter; mixed waves (C4's zipf lengths) stay
+    // per lane, where full peer grouping (7 ballots) cost more than the contention it saved
+    const uint64_t live = __ballot(mine);
+    const uint64_t same = __ballot(mine && bk == __builtin_amdgcn_readfirstlane(bk));
+    const uint64_t peers = same == live ? live : 1ull << (t & 63);
+    const uint32_t below = lanes_below(peers);
+    const bool leader = mine && below == 0;
+    __syncthreads();
+    if (leader) atomicAdd(&cur[bk], (uint32_t)__popcll(peers));
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the 65 bucket counts by one wave
+        uint32_t c = cur[t] + (t == 63 ? cur[64] : 0u);
+        uint32_t v = c;
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                uint32_t y = __shfl_up(v, d, 64);
-                if (lane >= (uint32_t)d) v += y;
-            }
-            const uint32_t last63 = cur[63];
-            cur[lane] = v - c;
-            if (lane == 63) cur[64] = v - c + last63;
+        for (int d = 1; d < 64; d <<= 1) {
+            uint32_t y = __shfl_up(v, d, 64);
+            if (t >= (uint32_t)d) v += y;
         }
-        __syncthreads();
-        if (threadIdx.x < cnt) order[atomicAdd(&cur[bk], 1u)] = (uint16_t)threadIdx.x;
-        __syncthreads();
-        if (threadIdx.x < cnt) i = k0 + order[threadIdx.x];
+        const uint32_t last63 = cur[63];
+        cur[t] = v - c;
+        if (t == 63) cur[64] = v - c + last63;
     }
-    if (i >= k1) return;
-    uint64_t h1, h2;
-    const uint64_t s = off[i], e = off[i + 1];
-    if (staged) {
-        // Funnel walk: every 4 key bytes come from two aligned LDS dwords (v_alignbyte), so all
-        // full words take the same path whatever the key's alignment; the < 4-byte tail last.
-        const uint32_t *lds = (const uint32_t *)stage;
-        const uint32_t b = (uint32_t)((uintptr_t)(data + s) - base);
-        const uint32_t len = (uint32_t)(e - s);
-        const uint32_t sh = (b & 3u) * 8u;
-        uint32_t wi = b >> 2;
-        uint32_t cur = lds[wi];
-        h1 = kFnvOffset;
-        h2 = kFnvOffset;
-        for (uint32_t j = 0; j + 4 <= len; j += 4) {
-            const uint32_t nxt = lds[++wi];
-            fnv_word(__builtin_amdgcn_alignbyte(nxt, cur, sh >> 3), h1, h2);
-            cur = nxt;
-        }
-        const uint32_t r = len & 3u;
-        if (r) fnv_word_part(__builtin_amdgcn_alignbyte(lds[wi + 1], cur, sh >> 3), 0u, r, h1, h2);
-    } else {
-        fnv_range(data, s, e, h1, h2);
+    __syncthreads();
+    uint32_t q = leader ? atomicAdd(&cur[bk], (uint32_t)__popcll(peers)) : 0u;
+    q = __shfl(q, mine ? __ffsll((unsigned long long)peers) - 1 : (int)(t & 63), 64) + below;
+    if (mine) {
+        slot_key[q] = (uint32_t)((uintptr_t)(data + ks) - base) << 16 | len;
+        slot_idx[q] = (uint16_t)t;
     }
-    hashes[i] = make_uint4((uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32));
+    __syncthreads();
+    if (!mine) return;  // cnt lanes hash the cnt sorted slots
+    const uint32_t sk = slot_key[t];
+    const uint32_t *lds = (const uint32_t *)stage;
+    Funnel f;
+    f.init(lds, sk >> 16, sk & 0xffffu);
+    for (uint32_t j = 0; j < f.len >> 2; ++j) f.step(lds);
+    f.tail(lds);
+    hashes[k0 + slot_idx[t]] = make_uint4((uint32_t)f.h1, (uint32_t)(f.h1 >> 32), (uint32_t)f.h2, (uint32_t)(f.h2 >> 32));
+}
+
+template <uint32_t KEYS>
+static hipError_t launch_hash_varlen_keys(const KeyBatch &kb, uint4 *hashes, uint32_t win, hipStream_t s) {
+    auto k = win == 64 ? k_hash_varlen<KEYS, 64> : win == 72 ? k_hash_varlen<KEYS, 72> : k_hash_varlen<KEYS, 80>;
+    hipLaunchKernelGGL(k, dim3((unsigned)((kb.n + KEYS - 1) / KEYS)), dim3(KEYS), 0, s, kb.data, kb.offsets, kb.n,
+                       hashes);
+    return hipGetLastError();
 }
 
 hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s) {
     if (!kb.offsets || kb.n == 0) return hipSuccess;
-    const uint64_t blocks = (kb.n + kHashKeys - 1) / kHashKeys;
-    hipLaunchKernelGGL(k_hash_varlen, dim3((unsigned)blocks), dim3(kHashKeys), 0, s, kb.data, kb.offsets, kb.n, hashes);
-    return hipGetLastError();
+    const Options &o = options();
+    switch (o.varlen_hash_keys) {
+        case 256: return launch_hash_varlen_keys<256>(kb, hashes, o.varlen_hash_win, s);
+        default: return launch_hash_varlen_keys<512>(kb, hashes, o.varlen_hash_win, s);
+    }
 }
 
 uint64_t len_perm_workspace_bytes(uint64_t n) {

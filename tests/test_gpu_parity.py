@@ -405,6 +405,38 @@ def test_varlen_processing_order_invisible(seb, torch_cuda, mode, build_algo):
         assert np.array_equal(out.cpu().numpy(), oc.probe(ref, m, k, pd, n, offsets=off))
 
 
+@pytest.mark.parametrize("keys,win", [(256, 64), (256, 80), (512, 64), (512, 72), (512, 80)])
+def test_varlen_prehash_geometries(seb, torch_cuda, keys, win):
+    """Every pre-hash workgroup size and LDS window hashes like the oracle, over
+    lengths that mix empty, sub-word, bucket-edge and window-overflowing keys, and a ragged
+    last workgroup."""
+    torch = torch_cuda
+    rng = np.random.default_rng(keys + win)
+    n = 40000 + 77
+    w = np.array([4, 4, 4, 4, 4, 4, 4, 8, 4, 8, 4, 8, 8, 4, 4, 4, 4, 4, 4, 3, 1], float)
+    lens = rng.choice([0, 1, 2, 3, 4, 5, 7, 8, 9, 16, 31, 39, 40, 41, 63, 64, 65, 255, 256, 300, 2000], size=n,
+                      p=w / w.sum())
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    data = rng.integers(0, 256, int(off[-1]) + 1, dtype=np.uint8)[1:]  # odd base offset in the host copy
+    m, k = oc.params(n, 0.01)
+    ref = oc.build(m, k, data, n, offsets=off)
+    with seb.option("varlen_hash_keys", keys), seb.option("varlen_hash_win", win), \
+            seb.option("varlen_prehash_min_keys", 0):
+        dd = torch.zeros(int(off[-1]) + 64, dtype=torch.uint8, device="cuda")
+        offd = to_dev(torch, off)
+        for shift in (0, 3):  # key bytes at an unaligned device address too
+            view = dd[shift: shift + int(off[-1])]
+            view.copy_(torch.from_numpy(data).cuda())
+            kd = seb.dev_keys(view, offd)
+            words, bits = dev_build_bits(seb, torch, kd, m, k)
+            assert np.array_equal(bits, ref), shift
+            out = torch.empty(n, dtype=torch.uint8, device="cuda")
+            seb.dev_probe(kd, words, m, k, out)
+            torch.cuda.synchronize()
+            assert bool(out.all()), shift
+
+
 def test_c4_varlen_10m_properties(seb, torch_cuda):
     """Full C4 size: no false negatives, and the bit array equals the oracle's."""
     torch = torch_cuda
