@@ -117,12 +117,19 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, Mo
                 const uint64_t i = k0 + (uint64_t)r * blockDim.x + threadIdx.x;
                 valid[r] = i < k1;
                 if (valid[r]) {
-                    uint64_t h1, h2;
-                    if constexpr (kPre)
-                        Src::hash_raw(kv[r], h1, h2);
-                    else
-                        src.hash(i, h1, h2);
-                    for_positions<KFIX, true>(h1, h2, md, KFIX, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
+                    if constexpr (IsPacked<Src>::value) {
+                        static_assert(KFIX == 7, "packed residues are k == 7");
+                        packed_positions((uint64_t)kv[r].x | (uint64_t)kv[r].y << 32, (uint32_t)md.m, (uint32_t)md.c,
+                                         pos[r]);
+                    } else {
+                        uint64_t h1, h2;
+                        if constexpr (kPre)
+                            Src::hash_raw(kv[r], h1, h2);
+                        else
+                            src.hash(i, h1, h2);
+                        for_positions<KFIX, true>(h1, h2, md, KFIX,
+                                                  [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
+                    }
 #pragma unroll
                     for (int q = 0; q < KQ; ++q) atomicAdd(&cursor[pos[r][q] >> kBktShift], 1u);
                 }
@@ -314,18 +321,15 @@ uint64_t bucketed_workspace_bytes(uint64_t n, uint64_t m, uint32_t k) {
     return plan_bucketed(n < cap ? n : cap, m, k).bytes;
 }
 
-hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModArg &md, void *ws, uint64_t ws_bytes,
-                                 hipStream_t s) {
-    if (kb.n == 0 || md.k == 0) return hipSuccess;
+// One launch pair (scatter + apply) per chunk of at most bucketed_max_keys keys; `chunk(k0, n)`
+// calls fn with the key source of keys [k0, k0 + n).
+template <typename Chunk>
+static hipError_t run_bucketed(uint64_t n, const ModArg &md, uint32_t *words, void *ws, uint64_t ws_bytes,
+                               hipStream_t s, Chunk &&chunk) {
     const uint64_t maxk = bucketed_max_keys(md.k);
-    for (uint64_t k0 = 0; k0 < kb.n; k0 += maxk) {  // OR-accumulative: split large batches
-        KeyBatch sub = kb;
-        sub.n = kb.n - k0 < maxk ? kb.n - k0 : maxk;
-        if (kb.offsets)
-            sub.offsets = kb.offsets + k0;
-        else
-            sub.data = kb.data + k0 * (uint64_t)kb.stride;
-        const BktPlan p = plan_bucketed(sub.n, md.m, md.k);
+    for (uint64_t k0 = 0; k0 < n; k0 += maxk) {  // OR-accumulative: split large batches
+        const uint64_t sn = n - k0 < maxk ? n - k0 : maxk;
+        const BktPlan p = plan_bucketed(sn, md.m, md.k);
         if (p.bytes > ws_bytes || p.ntiles > kMaxTiles) return hipErrorInvalidValue;
         if ((uint64_t)p.nb * p.ntiles * p.cap >= (1ull << 31)) return hipErrorInvalidValue;  // u32 region index
         uint8_t *w = (uint8_t *)ws;
@@ -335,21 +339,48 @@ hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModA
         const uint32_t thr = scatter_threads();
         const uint32_t kpt = scatter_kpt(p.nb);
         const size_t lds = ((size_t)thr * kpt * 7 + 2 * p.nb + 17) * sizeof(uint32_t);
-        hipError_t e = with_src(sub, [&](auto src) -> hipError_t {
+        hipError_t e = chunk(k0, sn, [&](auto src) -> hipError_t {
             using S = decltype(src);
-            auto scat = thr == 512 ? (md.k == 7 ? k_bkt_scatter<S, 7, 512, 4> : k_bkt_scatter<S, 0, 512, 4>)
-                        : kpt == 5 ? (md.k == 7 ? k_bkt_scatter<S, 7, 1024, 5> : k_bkt_scatter<S, 0, 1024, 5>)
-                                   : (md.k == 7 ? k_bkt_scatter<S, 7, 1024, 4> : k_bkt_scatter<S, 0, 1024, 4>);
+            constexpr int K0 = IsPacked<S>::value ? 7 : 0;  // packed sources have no generic-k kernel
+            auto scat = thr == 512 ? (md.k == 7 ? k_bkt_scatter<S, 7, 512, 4> : k_bkt_scatter<S, K0, 512, 4>)
+                        : kpt == 5 ? (md.k == 7 ? k_bkt_scatter<S, 7, 1024, 5> : k_bkt_scatter<S, K0, 1024, 5>)
+                                   : (md.k == 7 ? k_bkt_scatter<S, 7, 1024, 4> : k_bkt_scatter<S, K0, 1024, 4>);
             hipError_t a = hipFuncSetAttribute((const void *)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (a != hipSuccess) return a;
-            hipLaunchKernelGGL(scat, dim3(p.ntiles), dim3(thr), lds, s, src, sub.n, md, p.nb, p.tile_keys,
-                               p.ntiles, p.cap, regions, counts, words);
+            hipLaunchKernelGGL(scat, dim3(p.ntiles), dim3(thr), lds, s, src, sn, md, p.nb, p.tile_keys, p.ntiles,
+                               p.cap, regions, counts, words);
             hipLaunchKernelGGL(k_bkt_apply, dim3(p.nb), dim3(256), 0, s, regions, counts, p.ntiles, p.cap, words, nwords);
             return hipGetLastError();
         });
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModArg &md, void *ws, uint64_t ws_bytes,
+                                 hipStream_t s) {
+    if (kb.n == 0 || md.k == 0) return hipSuccess;
+    return run_bucketed(kb.n, md, words, ws, ws_bytes, s, [&](uint64_t k0, uint64_t sn, auto &&fn) {
+        KeyBatch sub = kb;
+        sub.n = sn;
+        if (kb.hashes)
+            sub.hashes = kb.hashes + k0;
+        else if (kb.perm)
+            sub.perm = kb.perm + k0;  // perm holds batch-wide key indices into the same offsets
+        else if (kb.offsets)
+            sub.offsets = kb.offsets + k0;
+        else
+            sub.data = kb.data + k0 * (uint64_t)kb.stride;
+        return with_src(sub, fn);
+    });
+}
+
+hipError_t launch_build_bucketed_packed(const uint64_t *packed, uint64_t n, uint32_t *words, const ModArg &md,
+                                        void *ws, uint64_t ws_bytes, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (md.k != 7 || md.m >= (1ull << kPackBits)) return hipErrorInvalidValue;
+    return run_bucketed(n, md, words, ws, ws_bytes, s,
+                        [&](uint64_t k0, uint64_t, auto &&fn) { return fn(KeysPacked{packed + k0}); });
 }
 
 }  // namespace seb

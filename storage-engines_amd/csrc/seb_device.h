@@ -230,6 +230,55 @@ static inline hipError_t with_src(const KeyBatch &kb, Fn &&fn) {
     return fn(KeysStrideB{kb.data, kb.stride});
 }
 
+// ---- packed residues (k == 7, m < 2^kPackBits): bits 0-28 r0 = h1 mod m, 29-57 b = h2 mod m,
+// 58-63 bit q-1 = "the u64 sum h1 + q*h2 wrapped at step q" for q = 1..6.  The positions follow
+// for_positions' recurrence, so they are exactly (h1 + q*h2 mod 2^64) mod m of lsm/bloom.go:64.
+__device__ __forceinline__ uint64_t pack_residue(uint64_t h1, uint64_t h2, const ModArg &md) {
+    const uint64_t r0 = mod64(h1, md.m, md.mu), b = mod64(h2, md.m, md.mu);
+    uint64_t f = 0, x = h1;
+#pragma unroll
+    for (uint32_t q = 1; q < 7; ++q) {
+        const uint64_t xn = x + h2;
+        f |= (uint64_t)(xn < x) << (q - 1);
+        x = xn;
+    }
+    return r0 | (b << kPackBits) | (f << (2 * kPackBits));
+}
+
+// The 7 positions of packed word v (m, c = 2^64 mod m as u32: m < 2^29).
+__device__ __forceinline__ void packed_positions(uint64_t v, uint32_t m, uint32_t c, uint32_t pos[7]) {
+    constexpr uint64_t kMask = (1ull << kPackBits) - 1;
+    uint32_t x = (uint32_t)(v & kMask);
+    const uint32_t b = (uint32_t)((v >> kPackBits) & kMask), f = (uint32_t)(v >> (2 * kPackBits));
+    const uint32_t nb = m - b, bc = b >= c ? b - c : b + (m - c), nd = m - bc;
+    pos[0] = x;
+#pragma unroll
+    for (int q = 1; q < 7; ++q) {
+        const uint32_t na = (f >> (q - 1)) & 1u ? nd : nb;
+        const uint32_t t = x - na;
+        x = x >= na ? t : t + m;
+        pos[q] = x;
+    }
+}
+
+// A batch given as packed residues (the variable-length pre-hash writes these when the filter
+// allows): load(i) carries the 8-byte word in .x/.y; kernels take the positions from it directly.
+struct KeysPacked {
+    static constexpr bool kSplit = true;
+    static constexpr bool kPacked = true;
+    const uint64_t *p;
+    __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
+    __device__ __forceinline__ uint4 load(uint64_t i) const {
+        const uint64_t v = __builtin_nontemporal_load(p + i);
+        return make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u);
+    }
+};
+
+template <typename S, typename = void>
+struct IsPacked { static constexpr bool value = false; };
+template <typename S>
+struct IsPacked<S, std::void_t<decltype(S::kPacked)>> { static constexpr bool value = S::kPacked; };
+
 // Lanes of this wave holding the same `bits`-bit value v as this lane (live lanes only): one ballot
 // per bit, so lanes can share one LDS atomic per distinct value instead of one per lane.
 __device__ __forceinline__ uint64_t wave_peers(bool live, uint32_t v, uint32_t bits) {

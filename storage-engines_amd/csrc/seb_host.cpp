@@ -137,6 +137,8 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
         o.varlen_hash_keys = (uint32_t)value;
     else if (!strcmp(name, "varlen_hash_win") && (value == 64 || value == 72 || value == 80))
         o.varlen_hash_win = (uint32_t)value;
+    else if (!strcmp(name, "varlen_prehash_packed") && (value == 0 || value == 1))
+        o.varlen_prehash_packed = (int)value;
     else if (!strcmp(name, "wal_lds_kib") && (value == 36 || value == 48)) o.wal_lds_kib = (int)value;
     else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
@@ -167,6 +169,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "multiget_pass_kib")) *value = o.multiget_pass_kib;
     else if (!strcmp(name, "varlen_hash_keys")) *value = o.varlen_hash_keys;
     else if (!strcmp(name, "varlen_hash_win")) *value = o.varlen_hash_win;
+    else if (!strcmp(name, "varlen_prehash_packed")) *value = o.varlen_prehash_packed;
     else if (!strcmp(name, "wal_lds_kib")) *value = o.wal_lds_kib;
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;
@@ -250,6 +253,12 @@ static bool want_len_perm(const KeyBatch &kb) {
            kb.n <= 0xffffffffull;
 }
 static uint64_t prehash_bytes(const KeyBatch &kb) { return want_prehash(kb) ? ((kb.n * 16 + 255) & ~255ull) : 0; }
+// Pre-hash straight to packed residues (8 B per key) when the filter allows them (k == 7,
+// m < 2^29): the bucketed build and the phased probe then read half the bytes per key and skip
+// re-deriving the residues.
+static bool want_prehash_packed(const KeyBatch &kb, const ModArg &md) {
+    return want_prehash(kb) && options().varlen_prehash_packed && md.k == 7 && md.m < (1ull << kPackBits);
+}
 
 // Build dispatcher: bucketed (LDS, no global atomics) or device-scope atomics; variable-length
 // batches are first put in length-bucketed order.  Scratch layout: [perm | bucketed].  `ws` /
@@ -259,6 +268,19 @@ static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStr
                           Grow &&grow) {
     if (kb.n == 0 || md.k == 0) return SEB_OK;
     const bool bucketed = choose_build_algo(kb.n, md.m, md.k) == 2;
+    if (bucketed && want_prehash_packed(kb, md)) {  // scratch: [packed residues | bucketed]
+        const uint64_t pack_b = (kb.n * 8 + 255) & ~255ull;
+        const uint64_t need = pack_b + bucketed_workspace_bytes(kb.n, md.m, md.k);
+        if (need > ws_bytes) {
+            int rc = grow(need, &ws);
+            if (rc) return rc;
+            ws_bytes = need;
+        }
+        HIP_OR_FAIL(launch_hash_varlen_packed(kb, md, (uint64_t *)ws, s));
+        HIP_OR_FAIL(launch_build_bucketed_packed((const uint64_t *)ws, kb.n, words, md, (uint8_t *)ws + pack_b,
+                                                 ws_bytes - pack_b, s));
+        return SEB_OK;
+    }
     const uint64_t pre_b = prehash_bytes(kb);
     const uint64_t perm_b = want_len_perm(kb) ? len_perm_workspace_bytes(kb.n) : 0;
     const uint64_t head = pre_b + perm_b;
@@ -310,8 +332,15 @@ static bool want_phased(uint64_t n, const ModArg &md, const uint8_t *out) {
 
 static int probe_dispatch(KeyBatch kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s) {
     void *ws;
-    int rc = prepare_probe_keys(kb, s, 0, &ws);
-    if (rc) return rc;
+    int rc;
+    if (want_phased(kb.n, md, out) && want_prehash_packed(kb, md)) {  // pre-hash to packed, all phases from it
+        void *packed;
+        if ((rc = cached_workspace(s, kb.n * 8, &packed, 1))) return rc;
+        HIP_OR_FAIL(launch_hash_varlen_packed(kb, md, (uint64_t *)packed, s));
+        HIP_OR_FAIL(launch_probe_phased(nullptr, kb.n, words, md, out, (uint64_t *)packed, s));
+        return SEB_OK;
+    }
+    if ((rc = prepare_probe_keys(kb, s, 0, &ws))) return rc;
     if (want_phased(kb.n, md, out)) {  // packed residues in their own scratch (tag 1)
         void *packed;
         if ((rc = cached_workspace(s, kb.n * 8, &packed, 1))) return rc;
@@ -381,6 +410,10 @@ extern "C" int seb_dev_pack_residues(const seb_keys *keys, uint64_t m, uint32_t 
         return rc;
     if (!packed && keys->n) return fail(SEB_ERR_INVALID, "seb_dev_pack_residues: null packed");
     KeyBatch kb = key_batch(keys);
+    if (want_prehash_packed(kb, mod_arg(m, k))) {
+        HIP_OR_FAIL(launch_hash_varlen_packed(kb, mod_arg(m, k), packed, (hipStream_t)stream));
+        return SEB_OK;
+    }
     void *ws;
     if ((rc = prepare_probe_keys(kb, (hipStream_t)stream, 0, &ws))) return rc;
     HIP_OR_FAIL(launch_pack_residues(kb, mod_arg(m, k), packed, (hipStream_t)stream));
@@ -410,9 +443,14 @@ extern "C" int seb_dev_probe_emit_packed(const seb_keys *keys, const uint32_t *w
         return rc;
     if (keys->n && (!words || !out || !packed)) return fail(SEB_ERR_INVALID, "seb_dev_probe_emit_packed: null pointer");
     KeyBatch kb = key_batch(keys);
+    const ModArg md = mod_arg(m, k);
+    if (want_phased(kb.n, md, out) && want_prehash_packed(kb, md)) {
+        HIP_OR_FAIL(launch_hash_varlen_packed(kb, md, packed, (hipStream_t)stream));
+        HIP_OR_FAIL(launch_probe_phased(nullptr, kb.n, words, md, out, packed, (hipStream_t)stream));
+        return SEB_OK;
+    }
     void *ws;
     if ((rc = prepare_probe_keys(kb, (hipStream_t)stream, 0, &ws))) return rc;
-    const ModArg md = mod_arg(m, k);
     if (want_phased(kb.n, md, out))  // phase 0 writes the packed residues anyway
         HIP_OR_FAIL(launch_probe_phased(&kb, kb.n, words, md, out, packed, (hipStream_t)stream));
     else

@@ -83,6 +83,7 @@ struct Options {
     uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys
     uint32_t varlen_hash_keys = 512;  // keys per pre-hash workgroup (256, 512)
     uint32_t varlen_hash_win = 72;    // pre-hash LDS window bytes per key (64, 72, 80)
+    int varlen_prehash_packed = 1;    // pre-hash to packed residues where k == 7, m < 2^29 (0/1)
     int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)
     int probe_kpt = 2;            // k == 7 probes: keys per thread (1, 2, 4)
     int probe_slice_shift = 19;   // k == 7, m < 2^32: sliced probe with 2^shift-word (2 MiB) slices (0 = off)
@@ -104,6 +105,9 @@ Options &options();
 hipError_t launch_build(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s);
 bool bucketed_supported(uint64_t m, uint32_t k);
 uint64_t bucketed_workspace_bytes(uint64_t n, uint64_t m, uint32_t k);
+// Build from packed residues (k == 7, m < 2^kPackBits); same workspace as launch_build_bucketed.
+hipError_t launch_build_bucketed_packed(const uint64_t *packed, uint64_t n, uint32_t *words, const ModArg &md,
+                                        void *ws, uint64_t ws_bytes, hipStream_t s);
 hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModArg &md, void *ws, uint64_t ws_bytes,
                                  hipStream_t s);
 // 1 = atomic, 2 = bucketed, for a batch of n keys into an m-bit filter.
@@ -118,6 +122,8 @@ hipError_t launch_len_perm(const KeyBatch &kb, void *ws, uint64_t ws_bytes, hipS
 
 // Pre-hash a variable-length batch into one uint4 (h1, h2) per key (LDS-staged byte walk).
 hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s);
+// The same pre-hash writing packed residues for filter md (k == 7, m < 2^kPackBits) instead.
+hipError_t launch_hash_varlen_packed(const KeyBatch &kb, const ModArg &md, uint64_t *packed, hipStream_t s);
 
 // Interleaved multi-filter probe (all filters share (m, k), k == 7, m < 2^32): scratch bytes
 // needed for the per-call table (0 = not applicable), and the launch (table in `ws`).

@@ -311,15 +311,7 @@ __global__ __launch_bounds__(256) void k_pack_residues(Src src, uint64_t n, ModA
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint64_t h1, h2;
         src.hash(i, h1, h2);
-        const uint64_t r0 = mod64(h1, md.m, md.mu), b = mod64(h2, md.m, md.mu);
-        uint64_t f = 0, x = h1;
-#pragma unroll
-        for (uint32_t q = 1; q < 7; ++q) {
-            const uint64_t xn = x + h2;
-            f |= (uint64_t)(xn < x) << (q - 1);
-            x = xn;
-        }
-        out[src.index(i)] = r0 | (b << kPackBits) | (f << (2 * kPackBits));
+        out[src.index(i)] = pack_residue(h1, h2, md);
     }
 }
 

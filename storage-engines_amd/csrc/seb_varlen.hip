@@ -122,10 +122,20 @@ struct Funnel {
 // work per workgroup is short, so its time is mostly the chain of dependent memory round trips:
 // each thread loads its own key's offsets up front (with the span bounds), then the span; the
 // sorted slots carry (start, length, key) in LDS so the hash phase touches HBM only to store.
-template <uint32_t KEYS, uint32_t WIN>
+// Output: (h1, h2) as a uint4 per key, or with PACK the key's packed residues for filter md
+// (8 B instead of 16; the build and the phased probe take positions straight from them).
+template <bool PACK>
+__device__ __forceinline__ void put_hash(void *out, uint64_t i, uint64_t h1, uint64_t h2, const ModArg &md) {
+    if constexpr (PACK)
+        ((uint64_t *)out)[i] = pack_residue(h1, h2, md);
+    else
+        ((uint4 *)out)[i] = make_uint4((uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32));
+}
+
+template <uint32_t KEYS, uint32_t WIN, bool PACK>
 __global__ __launch_bounds__(KEYS) void k_hash_varlen(const uint8_t *__restrict__ data,
                                                       const uint64_t *__restrict__ off, uint64_t n,
-                                                      uint4 *__restrict__ hashes) {
+                                                      void *__restrict__ hashes, ModArg md) {
     constexpr uint32_t kHashLds = KEYS * WIN;
     static_assert(kHashLds % 16 == 0 && kHashLds + 16 < 65536, "window offsets are 16-bit");
     __shared__ uint4 stage[kHashLds / 16 + 1];  // +16 B: the funnel walk reads one dword past a key
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(KEYS) void k_hash_varlen(const uint8_t *__restrict_
         if (mine) {
             uint64_t h1, h2;
             fnv_range(data, ks, ke, h1, h2);
-            hashes[k0 + t] = make_uint4((uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32));
+            put_hash<PACK>(hashes, k0 + t, h1, h2, md);
         }
         return;
     }
@@ -193,24 +203,35 @@ __global__ __launch_bounds__(KEYS) void k_hash_varlen(const uint8_t *__restrict_
     f.init(lds, sk >> 16, sk & 0xffffu);
     for (uint32_t j = 0; j < f.len >> 2; ++j) f.step(lds);
     f.tail(lds);
-    hashes[k0 + slot_idx[t]] = make_uint4((uint32_t)f.h1, (uint32_t)(f.h1 >> 32), (uint32_t)f.h2, (uint32_t)(f.h2 >> 32));
+    put_hash<PACK>(hashes, k0 + slot_idx[t], f.h1, f.h2, md);
 }
 
-template <uint32_t KEYS>
-static hipError_t launch_hash_varlen_keys(const KeyBatch &kb, uint4 *hashes, uint32_t win, hipStream_t s) {
-    auto k = win == 64 ? k_hash_varlen<KEYS, 64> : win == 72 ? k_hash_varlen<KEYS, 72> : k_hash_varlen<KEYS, 80>;
-    hipLaunchKernelGGL(k, dim3((unsigned)((kb.n + KEYS - 1) / KEYS)), dim3(KEYS), 0, s, kb.data, kb.offsets, kb.n,
-                       hashes);
+template <uint32_t KEYS, bool PACK>
+static hipError_t launch_hash_varlen_keys(const KeyBatch &kb, void *out, const ModArg &md, uint32_t win,
+                                          hipStream_t s) {
+    auto k = win == 64   ? k_hash_varlen<KEYS, 64, PACK>
+             : win == 72 ? k_hash_varlen<KEYS, 72, PACK>
+                         : k_hash_varlen<KEYS, 80, PACK>;
+    hipLaunchKernelGGL(k, dim3((unsigned)((kb.n + KEYS - 1) / KEYS)), dim3(KEYS), 0, s, kb.data, kb.offsets, kb.n, out,
+                       md);
     return hipGetLastError();
 }
 
-hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s) {
+template <bool PACK>
+static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const ModArg &md, hipStream_t s) {
     if (!kb.offsets || kb.n == 0) return hipSuccess;
     const Options &o = options();
-    switch (o.varlen_hash_keys) {
-        case 256: return launch_hash_varlen_keys<256>(kb, hashes, o.varlen_hash_win, s);
-        default: return launch_hash_varlen_keys<512>(kb, hashes, o.varlen_hash_win, s);
-    }
+    if (o.varlen_hash_keys == 256) return launch_hash_varlen_keys<256, PACK>(kb, out, md, o.varlen_hash_win, s);
+    return launch_hash_varlen_keys<512, PACK>(kb, out, md, o.varlen_hash_win, s);
+}
+
+hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s) {
+    return launch_hash_varlen_any<false>(kb, hashes, ModArg{}, s);
+}
+
+hipError_t launch_hash_varlen_packed(const KeyBatch &kb, const ModArg &md, uint64_t *packed, hipStream_t s) {
+    if (md.k != 7 || md.m >= (1ull << kPackBits)) return hipErrorInvalidValue;
+    return launch_hash_varlen_any<true>(kb, packed, md, s);
 }
 
 uint64_t len_perm_workspace_bytes(uint64_t n) {

@@ -437,6 +437,65 @@ def test_varlen_prehash_geometries(seb, torch_cuda, keys, win):
             assert bool(out.all()), shift
 
 
+@pytest.mark.parametrize("packed", [0, 1])
+@pytest.mark.parametrize("algo", [1, 2])
+def test_varlen_prehash_packed_paths(seb, torch_cuda, packed, algo):
+    """Pre-hash to packed residues (bucketed build from KeysPacked, phased probe from packed
+    words, pack_residues / emit_packed over variable-length keys) against the oracle, and the
+    same with the 16-B hash path; a 2-range filter so the probe runs phased."""
+    torch = torch_cuda
+    rng = np.random.default_rng(11 + packed)
+    n = 600_001
+    w = np.array([20, 10, 10, 10, 5, 3, 1, 1], float)
+    lens = rng.choice([8, 9, 15, 16, 40, 100, 256, 3000], size=n, p=w / w.sum())
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    data = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    m, k = 40_000_003, 7
+    ref = oc.build(m, k, data, n, offsets=off, threads=16)
+    pd = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    pd[: int(off[n // 2])] = data[: int(off[n // 2])]  # first half present
+    want = oc.probe(ref, m, k, pd, n, offsets=off)
+    with seb.option("varlen_prehash_packed", packed), seb.option("build_algo", algo):
+        kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
+        words, bits = dev_build_bits(seb, torch, kd, m, k)
+        assert np.array_equal(bits, ref)
+        pkd = seb.dev_keys(to_dev(torch, pd), to_dev(torch, off))
+        out = torch.empty(n, dtype=torch.uint8, device="cuda")
+        seb.dev_probe(pkd, words, m, k, out)
+        pk = torch.zeros(n, dtype=torch.int64, device="cuda")
+        seb.dev_pack_residues(pkd, m, k, pk)
+        out2 = torch.empty(n, dtype=torch.uint8, device="cuda")
+        seb.dev_probe_packed(pk, n, words, m, k, out2)
+        pk3 = torch.zeros(n, dtype=torch.int64, device="cuda")
+        out3 = torch.empty(n, dtype=torch.uint8, device="cuda")
+        seb.dev_probe_emit_packed(pkd, words, m, k, out3, pk3)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want)
+        assert np.array_equal(out2.cpu().numpy(), want)
+        assert np.array_equal(out3.cpu().numpy(), want)
+        assert torch.equal(pk, pk3)
+
+
+@pytest.mark.parametrize("packed", [0, 1])
+def test_varlen_bucketed_build_chunks(seb, torch_cuda, packed):
+    """A pre-hashed variable-length build larger than one bucketed launch (16.7M keys at k = 7)
+    runs in chunks; every chunk must take its own slice of the hashes / packed residues."""
+    torch = torch_cuda
+    rng = np.random.default_rng(21)
+    n = (1 << 24) + 123_457
+    lens = rng.integers(8, 13, n)
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    data = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    m, k = 160_000_001, 7
+    ref = oc.build(m, k, data, n, offsets=off, threads=16)
+    with seb.option("varlen_prehash_packed", packed), seb.option("build_algo", 2):
+        kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
+        words, bits = dev_build_bits(seb, torch, kd, m, k)
+        assert np.array_equal(bits, ref)
+
+
 def test_c4_varlen_10m_properties(seb, torch_cuda):
     """Full C4 size: no false negatives, and the bit array equals the oracle's."""
     torch = torch_cuda
