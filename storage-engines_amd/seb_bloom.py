@@ -21,7 +21,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libseb_bloom.so")
+LIB_PATH = os.environ.get("SEB_LIB_PATH") or os.path.join(_HERE, "lib", "libseb_bloom.so")  # override: A/B builds
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "seb_bloom.h")
 
 SEB_OK = 0

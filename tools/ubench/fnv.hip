@@ -4,6 +4,9 @@
 //   0  plain C: (h ^ b) * P  /  (h * P) ^ b   (compiler: v_mad_u64_u32 + v_mul_lo_u32 + v_add3)
 //   1  P = 2^40 + 435, 435 = (3*9)*16 + 3: three v_lshl_add_u64 + one v_lshl_add_u32 per step
 //   2  lo/hi split with v_mul_hi_u32 / v_mul_lo_u32 (three 32-bit multiplies per step)
+//   3  16-B keys only: the low word runs the chain alone (lo' = low32((lo ^ b) * 435)), and the
+//      high word, linear in the per-step terms d_j = carry_j + (x_j << 8), is summed with
+//      constant weights 435^(15-j) mod 2^32 off the critical path (one v_mad_u64_u32 each)
 // Build: hipcc --offload-arch=gfx950 -O3 fnv.hip -o fnv
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -48,6 +51,40 @@ __device__ __forceinline__ void step(uint32_t b, uint64_t &h1, uint64_t &h2) {
     }
 }
 
+// 435^e mod 2^32
+__host__ __device__ constexpr uint32_t pw435(int e) {
+    uint32_t r = 1;
+    for (int i = 0; i < e; ++i) r *= 435u;
+    return r;
+}
+
+// acc + a * b as one v_mad_u64_u32 (the compiler narrows a mad whose high half is unused into
+// v_mul_lo_u32 + v_add3_u32, two instructions)
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t acc) {
+    uint64_t r;
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(acc) : "vcc");
+    return r;
+}
+
+__device__ __forceinline__ void fnv16_v3(const uint32_t w[4], uint64_t &h1, uint64_t &h2) {
+    uint32_t lo1 = (uint32_t)kOff, lo2 = (uint32_t)kOff;
+    uint64_t acc1 = (uint64_t)((uint32_t)(kOff >> 32) * pw435(16)), acc2 = acc1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
+        const uint32_t cj = pw435(15 - j);
+        const uint32_t x = lo1 ^ b;  // FNV-1a: xor, then multiply
+        const uint64_t p = (uint64_t)x * 435u;
+        lo1 = (uint32_t)p;
+        acc1 = mad64((uint32_t)(p >> 32) + (x << 8), cj, acc1);
+        const uint64_t q = (uint64_t)lo2 * 435u;  // FNV-1: multiply, then xor
+        acc2 = mad64((uint32_t)(q >> 32) + (lo2 << 8), cj, acc2);
+        lo2 = (uint32_t)q ^ b;
+    }
+    h1 = (acc1 << 32) | lo1;
+    h2 = (acc2 << 32) | lo2;
+}
+
 // R > 1: hash R variants of the key (first word xor r) and xor the results: compute-bound form.
 template <int V, int R = 1>
 __global__ __launch_bounds__(256) void k_hash(const uint4 *__restrict__ keys, uint64_t n, uint4 *__restrict__ out) {
@@ -58,10 +95,14 @@ __global__ __launch_bounds__(256) void k_hash(const uint4 *__restrict__ keys, ui
     for (int r = 0; r < R; ++r) {
         uint64_t h1 = kOff, h2 = kOff;
         const uint32_t w[4] = {v.x ^ (uint32_t)r, v.y, v.z, v.w};
+        if constexpr (V == 3) {
+            fnv16_v3(w, h1, h2);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int s = 0; s < 4; ++s) step<V>((w[j] >> (8 * s)) & 0xffu, h1, h2);
+                for (int s = 0; s < 4; ++s) step<V>((w[j] >> (8 * s)) & 0xffu, h1, h2);
+        }
         a1 ^= h1;
         a2 ^= h2;
     }
@@ -156,11 +197,16 @@ int main() {
     hipMemcpy(got.data(), out, n * 16, hipMemcpyDeviceToHost);
     printf("{\"kernel\": \"fnv_v2_split\", \"ms\": %.4f, \"equal\": %d}\n", t2,
            (int)(memcmp(ref.data(), got.data(), n * 16) == 0));
-    for (int v = 0; v < 3; ++v) {
+    float t3 = timeit([&] { hipLaunchKernelGGL(k_hash<3>, g, b, 0, 0, keys, n, out); });
+    hipMemcpy(got.data(), out, n * 16, hipMemcpyDeviceToHost);
+    printf("{\"kernel\": \"fnv_v3_lochain\", \"ms\": %.4f, \"equal\": %d}\n", t3,
+           (int)(memcmp(ref.data(), got.data(), n * 16) == 0));
+    for (int v = 0; v < 4; ++v) {
         float t = timeit([&] {
             if (v == 0) hipLaunchKernelGGL((k_hash<0, 16>), g, b, 0, 0, keys, n, out);
             if (v == 1) hipLaunchKernelGGL((k_hash<1, 16>), g, b, 0, 0, keys, n, out);
             if (v == 2) hipLaunchKernelGGL((k_hash<2, 16>), g, b, 0, 0, keys, n, out);
+            if (v == 3) hipLaunchKernelGGL((k_hash<3, 16>), g, b, 0, 0, keys, n, out);
         });
         hipMemcpy(got.data(), out, n * 16, hipMemcpyDeviceToHost);
         if (v == 0) ref = got;
