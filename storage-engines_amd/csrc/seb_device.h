@@ -84,6 +84,37 @@ __device__ __forceinline__ void fnv_key16(const uint4 v, uint64_t &h1, uint64_t 
     h2 = (acc2 << 32) | lo2;
 }
 
+// Both chains in the split form of fnv_key16, for walks of unknown length: the high words are
+// kept as u64 accumulators whose low 32 bits are the hash's high word, and each 4-byte word
+// folds its four d_j into them with constant weights (3 mads), then one mad scales the old value
+// by 435^4: 17 VALU instructions per word and hash instead of 20.
+struct FnvSplit {
+    uint32_t lo1 = (uint32_t)kFnvOffset, lo2 = (uint32_t)kFnvOffset;
+    uint64_t a1 = kFnvOffset >> 32, a2 = kFnvOffset >> 32;
+    __device__ __forceinline__ void word(uint32_t w) {
+        uint32_t d1[4], d2[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t b = (w >> (8 * j)) & 0xffu;
+            const uint32_t x = lo1 ^ b;  // FNV-1a
+            const uint64_t p = (uint64_t)x * 435u;
+            lo1 = (uint32_t)p;
+            d1[j] = (uint32_t)(p >> 32) + (x << 8);
+            const uint64_t q = (uint64_t)lo2 * 435u;  // FNV-1
+            d2[j] = (uint32_t)(q >> 32) + (lo2 << 8);
+            lo2 = (uint32_t)q ^ b;
+        }
+        const uint64_t t1 = mad_lo(d1[0], pow435(3), mad_lo(d1[1], pow435(2), mad_lo(d1[2], 435u, d1[3])));
+        const uint64_t t2 = mad_lo(d2[0], pow435(3), mad_lo(d2[1], pow435(2), mad_lo(d2[2], 435u, d2[3])));
+        a1 = mad_lo((uint32_t)a1, pow435(4), t1);
+        a2 = mad_lo((uint32_t)a2, pow435(4), t2);
+    }
+    __device__ __forceinline__ void get(uint64_t &h1, uint64_t &h2) const {
+        h1 = (a1 << 32) | lo1;
+        h2 = (a2 << 32) | lo2;
+    }
+};
+
 // Sources with kSplit = true also expose load(i) -> uint4 and hash_raw(raw, h1, h2), so a kernel
 // can issue the loads of its next batch of keys before it hashes them (software prefetch).
 struct Keys16 {  // fixed 16-B keys, 16-B aligned: one dwordx4 per lane, 1 KiB per wave, coalesced

@@ -96,21 +96,21 @@ __global__ __launch_bounds__(kPermThreads) void k_len_scatter(const uint64_t *__
 // (v_alignbyte), so all full words take the same path whatever the key's alignment.
 struct Funnel {
     uint32_t wi, cur, sh, len;
-    uint64_t h1, h2;
+    FnvSplit f;
     __device__ __forceinline__ void init(const uint32_t *lds, uint32_t b, uint32_t n) {
         wi = b >> 2;
         sh = b & 3u;
         len = n;
         cur = lds[wi];
-        h1 = kFnvOffset;
-        h2 = kFnvOffset;
     }
     __device__ __forceinline__ void step(const uint32_t *lds) {  // the next 4 bytes
         const uint32_t nxt = lds[++wi];
-        fnv_word(__builtin_amdgcn_alignbyte(nxt, cur, sh), h1, h2);
+        f.word(__builtin_amdgcn_alignbyte(nxt, cur, sh));
         cur = nxt;
     }
-    __device__ __forceinline__ void tail(const uint32_t *lds) {  // the last len % 4 bytes
+    // the last len % 4 bytes; returns the key's (h1, h2)
+    __device__ __forceinline__ void finish(const uint32_t *lds, uint64_t &h1, uint64_t &h2) {
+        f.get(h1, h2);
         const uint32_t r = len & 3u;
         if (r) fnv_word_part(__builtin_amdgcn_alignbyte(lds[wi + 1], cur, sh), 0u, r, h1, h2);
     }
@@ -202,8 +202,9 @@ __global__ __launch_bounds__(KEYS) void k_hash_varlen(const uint8_t *__restrict_
     Funnel f;
     f.init(lds, sk >> 16, sk & 0xffffu);
     for (uint32_t j = 0; j < f.len >> 2; ++j) f.step(lds);
-    f.tail(lds);
-    put_hash<PACK>(hashes, k0 + slot_idx[t], f.h1, f.h2, md);
+    uint64_t h1, h2;
+    f.finish(lds, h1, h2);
+    put_hash<PACK>(hashes, k0 + slot_idx[t], h1, h2, md);
 }
 
 template <uint32_t KEYS, bool PACK>
