@@ -84,6 +84,7 @@ int seb_abi_version(void);
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
  *   "multiget_pass_kib" registry MultiGet: filter bytes per pass (0 = one pass over all files)
  *   "scatter_threads", "scatter_kpt"  radix-partitioned build: workgroup size, keys per thread
+ *   "apply_threads"   radix-partitioned build: apply workgroup size (256, 512, 1024)
  *   "stream_nt"       non-temporal loads of 16-B key batches (0/1)
  *   "varlen_prehash_min_keys", "varlen_sort_min_keys"  variable-length batches: LDS pre-hash and
  *                     global length-sort thresholds

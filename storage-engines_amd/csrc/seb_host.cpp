@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -91,33 +92,8 @@ static bool env_flag(const char *name, long *out) {
     return true;
 }
 
-static std::once_flag g_env_once;
-static void load_env() {
-    long v;
-    Options &o = options();
-    if (env_flag("SEB_GRID_CAP", &v) && v > 0) o.grid_cap = (unsigned)v;
-    if (env_flag("SEB_BUILD_ALGO", &v)) o.build_algo = (int)v;
-    if (env_flag("SEB_PROBE_SPLIT", &v)) o.probe_split = (int)v;
-    if (env_flag("SEB_PROBE_KPT", &v)) o.probe_kpt = (int)v;
-    if (env_flag("SEB_PROBE_PHASES", &v) && v >= 0 && v <= 64) o.probe_phases = (int)v;
-    if (env_flag("SEB_MULTI_INTERLEAVE", &v)) o.multi_interleave = (int)v;
-    if (env_flag("SEB_SCATTER_THREADS", &v)) o.scatter_threads = (int)v;
-    if (env_flag("SEB_STREAM_NT", &v)) o.stream_nt = (int)v;
-    if (env_flag("SEB_SCATTER_KPT", &v)) o.scatter_kpt = (int)v;
-    if (env_flag("SEB_PROBE_PERSISTENT", &v)) o.probe_persistent = (int)v;
-    if (env_flag("SEB_PROBE_MODE", &v) && v >= 0 && v <= 8) o.probe_mode = (int)v;
-    if (env_flag("SEB_WAL_LDS_KIB", &v) && (v == 36 || v == 48)) o.wal_lds_kib = (int)v;
-    if (env_flag("SEB_VARLEN_SORT_MIN_KEYS", &v) && v >= 0) o.varlen_sort_min_keys = (uint64_t)v;
-    if (env_flag("SEB_VARLEN_PREHASH_MIN_KEYS", &v) && v >= 0) o.varlen_prehash_min_keys = (uint64_t)v;
-    if (env_flag("SEB_PROBE_SLICE_SHIFT", &v)) o.probe_slice_shift = (int)v;
-    if (env_flag("SEB_PROBE_SLICE_GRID", &v)) o.probe_slice_grid = (unsigned)v;
-    if (env_flag("SEB_BUCKET_MIN_KEYS", &v) && v >= 0) o.bucket_min_keys = (uint64_t)v;
-}
-
-extern "C" int seb_set_option(const char *name, int64_t value) {
-    std::call_once(g_env_once, load_env);
-    if (!name) return fail(SEB_ERR_INVALID, "seb_set_option: null name");
-    Options &o = options();
+// Validated assignment of one knob; false for an unknown name or an out-of-range value.
+static bool set_opt(Options &o, const char *name, int64_t value) {
     if (!strcmp(name, "build_algo") && value >= 0 && value <= 2) o.build_algo = (int)value;
     else if (!strcmp(name, "probe_split") && (value == 0 || value == 2 || value == 3)) o.probe_split = (int)value;
     else if (!strcmp(name, "probe_kpt") && (value == 1 || value == 2 || value == 4 || value == 6 || value == 8)) o.probe_kpt = (int)value;
@@ -137,6 +113,8 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
         o.varlen_hash_keys = (uint32_t)value;
     else if (!strcmp(name, "varlen_hash_win") && (value == 64 || value == 72 || value == 80))
         o.varlen_hash_win = (uint32_t)value;
+    else if (!strcmp(name, "apply_threads") && (value == 256 || value == 512 || value == 1024))
+        o.apply_threads = (uint32_t)value;
     else if (!strcmp(name, "varlen_prehash_packed") && (value == 0 || value == 1))
         o.varlen_prehash_packed = (int)value;
     else if (!strcmp(name, "wal_lds_kib") && (value == 36 || value == 48)) o.wal_lds_kib = (int)value;
@@ -144,7 +122,36 @@ extern "C" int seb_set_option(const char *name, int64_t value) {
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
     else if (!strcmp(name, "grid_cap") && value > 0 && value <= (1 << 30)) o.grid_cap = (unsigned)value;
     else if (!strcmp(name, "bucket_min_keys") && value >= 0) o.bucket_min_keys = (uint64_t)value;
-    else return fail(SEB_ERR_INVALID, "seb_set_option: bad option %s=%lld", name, (long long)value);
+    else return false;
+    return true;
+}
+
+// Every knob of seb_set_option; SEB_<NAME> in the environment sets its initial value.
+static const char *const kOptionNames[] = {
+    "build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "multi_interleave",
+    "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases",
+    "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
+    "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
+    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys"};
+
+static std::once_flag g_env_once;
+static void load_env() {
+    Options &o = options();
+    for (const char *name : kOptionNames) {
+        char var[64] = "SEB_";
+        size_t j = 4;
+        for (const char *c = name; *c && j + 1 < sizeof var; ++c) var[j++] = (char)toupper((unsigned char)*c);
+        var[j] = 0;
+        long v;
+        if (env_flag(var, &v)) set_opt(o, name, v);
+    }
+}
+
+extern "C" int seb_set_option(const char *name, int64_t value) {
+    std::call_once(g_env_once, load_env);
+    if (!name) return fail(SEB_ERR_INVALID, "seb_set_option: null name");
+    if (!set_opt(options(), name, value))
+        return fail(SEB_ERR_INVALID, "seb_set_option: bad option %s=%lld", name, (long long)value);
     return SEB_OK;
 }
 
@@ -170,6 +177,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "varlen_hash_keys")) *value = o.varlen_hash_keys;
     else if (!strcmp(name, "varlen_hash_win")) *value = o.varlen_hash_win;
     else if (!strcmp(name, "varlen_prehash_packed")) *value = o.varlen_prehash_packed;
+    else if (!strcmp(name, "apply_threads")) *value = o.apply_threads;
     else if (!strcmp(name, "wal_lds_kib")) *value = o.wal_lds_kib;
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;

@@ -83,6 +83,7 @@ struct Options {
     uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys
     uint32_t varlen_hash_keys = 512;  // keys per pre-hash workgroup (256, 512)
     uint32_t varlen_hash_win = 72;    // pre-hash LDS window bytes per key (64, 72, 80)
+    uint32_t apply_threads = 1024;    // radix-partitioned build: apply workgroup size (256, 512, 1024)
     int varlen_prehash_packed = 1;    // pre-hash to packed residues where k == 7, m < 2^29 (0/1)
     int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)
     int probe_kpt = 2;            // k == 7 probes: keys per thread (1, 2, 4)

@@ -165,12 +165,13 @@ def test_host_api_chunked_pipeline(seb, monkeypatch, torch_cuda):
 
 # --------------------------------------------------------- device-resident API --------------
 
-@pytest.fixture(params=[(1, 1024, 4), (2, 1024, 4), (2, 512, 4), (2, 1024, 5)],
+@pytest.fixture(params=[(1, 1024, 4, 1024), (2, 1024, 4, 256), (2, 512, 4, 512), (2, 1024, 5, 1024)],
                 ids=["atomic", "bucketed", "bucketed512", "bucketed-kpt5"])
 def build_algo(request, seb):
-    with seb.option("build_algo", request.param[0]), seb.option("scatter_threads", request.param[1]), \
-            seb.option("scatter_kpt", request.param[2]):
-        yield request.param[0]
+    algo, thr, kpt, apply = request.param
+    with seb.option("build_algo", algo), seb.option("scatter_threads", thr), seb.option("scatter_kpt", kpt), \
+            seb.option("apply_threads", apply):
+        yield algo
 
 
 @pytest.fixture(params=[(0, 1, 0, 0, 0), (2, 2, 0, 0, 0), (3, 1, 0, 0, 1), (3, 2, 0, 0, 0), (3, 4, 0, 0, 0),
