@@ -80,6 +80,9 @@ int seb_abi_version(void);
  *   "probe_slice_grid"  sliced probe: workgroup cap (0 = grid_cap)
  *   "probe_mode"      k == 7 probe: 8 = phased, one launch per filter range (default); 0-7 sliced gather orders (k_probe_sliced)
  *   "probe_phases"    phased probe (probe_mode 8): phases, 0 = one per 4 MiB of filter
+ *   "probe_phase0_pct", "probe_phase0_kpt"  phased probe: range 0's share of the filter (0 = even),
+ *                     keys per thread in phase 0 (1, 2, 4)
+ *   "probe_pack_first" phased probe: a streaming pack pass, then every range from packed words (0/1)
  *   "probe_persistent" sliced probe: persistent 1024-thread workgroups (0 = off)
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
  *   "multiget_pass_kib" registry MultiGet: filter bytes per pass (0 = one pass over all files)

@@ -96,7 +96,8 @@ struct Options {
     int probe_persistent = 0;     // sliced probe: persistent 1024-thread workgroups, barrier per slice (0 = off)
     int wal_lds_kib = 36;         // WAL CRC: LDS staging window per 256-record workgroup (36 or 48)
     int probe_phase0_pct = 0;     // phased probe: share of the filter in range 0 (0 = even split)
-    int probe_phase0_kpt = 2;     // phased probe: keys per thread in phase 0 (1, 2, 4)
+    int probe_phase0_kpt = 1;     // phased probe: keys per thread in phase 0 (1, 2, 4)
+    int probe_pack_first = 0;     // phased probe: pack residues in a streaming pass instead of in phase 0
     int probe_phases = 0;         // phased probe: number of phases (0 = one per 4 MiB of filter)
     int probe_mode = 8;           // k == 7 probe: 8 = phased (one launch per filter range, default); 0-6 k_probe_sliced MODE, 7 k_probe_compact
     unsigned grid_cap = 1u << 20;

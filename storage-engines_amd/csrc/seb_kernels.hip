@@ -1092,6 +1092,10 @@ hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *w
     };
     hipError_t e = hipSuccess;
     uint64_t p0 = 0;
+    if (kb && o.probe_pack_first) {  // a streaming pack pass, then every range from the packed words
+        if ((e = launch_pack_residues(*kb, md, packed, s)) != hipSuccess) return e;
+        kb = nullptr;
+    }
     if (kb) {
         const uint32_t kpt0 = o.probe_phase0_kpt == 1 || o.probe_phase0_kpt == 4 ? (uint32_t)o.probe_phase0_kpt : 2u;
         const unsigned g0 = grid_for((n + kpt0 - 1) / kpt0, 256, o.grid_cap);
