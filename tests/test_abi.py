@@ -108,3 +108,39 @@ def test_no_silent_fallback_without_library(seb, monkeypatch, tmp_path):
     monkeypatch.setattr(mod, "LIB_PATH", str(tmp_path / "missing.so"))
     with pytest.raises(mod.SebError):
         mod.params(10, 0.01)
+
+
+OPTION_NAMES = ["build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "multi_interleave",
+                "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases",
+                "probe_pack_first", "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys",
+                "varlen_hash_win", "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
+                "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys"]
+
+
+def test_options_round_trip_and_reject_bad_values(seb):
+    """Every knob reads back what was set, bad values are refused and leave the knob unchanged."""
+    for name in OPTION_NAMES:
+        old = seb.get_option(name)
+        seb.set_option(name, old)
+        assert seb.get_option(name) == old
+    with seb.option("apply_threads", 512):
+        assert seb.get_option("apply_threads") == 512
+    for name, bad in (("apply_threads", 300), ("varlen_hash_win", 50), ("probe_mode", 9), ("nonexistent", 1)):
+        before = seb.get_option(name) if name != "nonexistent" else None
+        with pytest.raises(seb.SebError):
+            seb.set_option(name, bad)
+        if before is not None:
+            assert seb.get_option(name) == before
+
+
+def test_options_from_environment(seb):
+    """SEB_<NAME> sets a knob's initial value in a fresh process; an out-of-range value is ignored."""
+    code = ("import sys; sys.path.insert(0, 'storage-engines_amd'); import seb_bloom as s; "
+            "print(s.get_option('apply_threads'), s.get_option('varlen_hash_win'), s.get_option('probe_phases'))")
+    import os
+    env = dict(os.environ, SEB_APPLY_THREADS="512", SEB_VARLEN_HASH_WIN="13", SEB_PROBE_PHASES="5")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run(["python", "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
+    apply, win, phases = map(int, out.stdout.split())
+    assert apply == 512 and phases == 5
+    assert win == 72  # 13 is not a valid window: the default stays
