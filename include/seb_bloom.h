@@ -85,6 +85,8 @@ int seb_abi_version(void);
  *   "probe_pack_first" phased probe: a streaming pack pass, then every range from packed words (0/1)
  *   "probe_persistent" sliced probe: persistent 1024-thread workgroups (0 = off)
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
+ *   "multi_phases"    interleaved multi-filter probe: 1 = in-kernel slices (default), 0 = one launch
+ *                     per 4 MiB of table, n > 1 = n launches (phased, k == 7, m < 2^29)
  *   "multiget_pass_kib" registry MultiGet: filter bytes per pass (0 = one pass over all files)
  *   "scatter_threads", "scatter_kpt"  radix-partitioned build: workgroup size, keys per thread
  *   "apply_threads"   radix-partitioned build: apply workgroup size (256, 512, 1024)

@@ -107,6 +107,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "probe_mode") && value >= 0 && value <= 8) o.probe_mode = (int)value;
     else if (!strcmp(name, "probe_phases") && value >= 0 && value <= 64) o.probe_phases = (int)value;
     else if (!strcmp(name, "probe_pack_first") && (value == 0 || value == 1)) o.probe_pack_first = (int)value;
+    else if (!strcmp(name, "multi_phases") && value >= 0 && value <= 64) o.multi_phases = (int)value;
     else if (!strcmp(name, "probe_phase0_pct") && value >= 0 && value <= 90) o.probe_phase0_pct = (int)value;
     else if (!strcmp(name, "probe_phase0_kpt") && (value == 1 || value == 2 || value == 4)) o.probe_phase0_kpt = (int)value;
     else if (!strcmp(name, "multiget_pass_kib") && value >= 0 && value <= (1 << 22)) o.multiget_pass_kib = (int)value;
@@ -130,7 +131,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
 // Every knob of seb_set_option; SEB_<NAME> in the environment sets its initial value.
 static const char *const kOptionNames[] = {
     "build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "multi_interleave",
-    "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases", "probe_pack_first",
+    "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases", "probe_pack_first", "multi_phases",
     "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
     "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
     "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys"};
@@ -173,6 +174,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "probe_mode")) *value = o.probe_mode;
     else if (!strcmp(name, "probe_phases")) *value = o.probe_phases;
     else if (!strcmp(name, "probe_pack_first")) *value = o.probe_pack_first;
+    else if (!strcmp(name, "multi_phases")) *value = o.multi_phases;
     else if (!strcmp(name, "probe_phase0_pct")) *value = o.probe_phase0_pct;
     else if (!strcmp(name, "probe_phase0_kpt")) *value = o.probe_phase0_kpt;
     else if (!strcmp(name, "multiget_pass_kib")) *value = o.multiget_pass_kib;
@@ -501,7 +503,12 @@ extern "C" int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *f
     void *ws = nullptr;
     if ((rc = prepare_probe_keys(kb, s, (tb + 255) & ~255ull, &ws))) return rc;
     if (tb) {
-        HIP_OR_FAIL(launch_probe_interleaved(kb, ma, mask, mask_bytes, ws, s));
+        const ModArg &md = ma.f[0].md;
+        void *packed = nullptr;  // phased: packed residues in their own scratch (tag 1)
+        if (md.m < (1ull << kPackBits) && multi_phase_count(md.m, mask_bytes) > 1 &&
+            (rc = cached_workspace(s, kb.n * 8, &packed, 1)))
+            return rc;
+        HIP_OR_FAIL(launch_probe_interleaved(kb, ma, mask, mask_bytes, ws, (uint64_t *)packed, s));
         return SEB_OK;
     }
     HIP_OR_FAIL(launch_probe_multi(kb, ma, mask, mask_bytes, s));

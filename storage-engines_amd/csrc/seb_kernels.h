@@ -97,6 +97,8 @@ struct Options {
     int wal_lds_kib = 36;         // WAL CRC: LDS staging window per 256-record workgroup (36 or 48)
     int probe_phase0_pct = 0;     // phased probe: share of the filter in range 0 (0 = even split)
     int probe_phase0_kpt = 1;     // phased probe: keys per thread in phase 0 (1, 2, 4)
+    int multi_phases = 1;         // phased interleaved multi-filter probe: ranges (1 = off, the default: measured slower
+                                  // on C5; 0 = one per 4 MiB of table; n > 1 = n ranges)
     int probe_pack_first = 0;     // phased probe: pack residues in a streaming pass instead of in phase 0
     int probe_phases = 0;         // phased probe: number of phases (0 = one per 4 MiB of filter)
     int probe_mode = 8;           // k == 7 probe: 8 = phased (one launch per filter range, default); 0-6 k_probe_sliced MODE, 7 k_probe_compact
@@ -130,8 +132,11 @@ hipError_t launch_hash_varlen_packed(const KeyBatch &kb, const ModArg &md, uint6
 // Interleaved multi-filter probe (all filters share (m, k), k == 7, m < 2^32): scratch bytes
 // needed for the per-call table (0 = not applicable), and the launch (table in `ws`).
 uint64_t interleaved_bytes(const MultiArg &ma, uint32_t mask_bytes);
+// packed != nullptr: phased (multi_phase_count > 1), with n * 8 bytes of packed-residue scratch.
 hipError_t launch_probe_interleaved(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes, void *ws,
-                                    hipStream_t s);
+                                    uint64_t *packed, hipStream_t s);
+// Table ranges of the phased interleaved probe for filters of m bits (0: not phased).
+uint32_t multi_phase_count(uint64_t m, uint32_t mask_bytes);
 // The same over packed residues (all filters share (m, k), k == 7, m < 2^kPackBits); `ws` holds
 // the table (interleaved_table_bytes).
 hipError_t launch_probe_interleaved_packed(const uint64_t *packed, uint64_t n, const MultiArg &ma, void *mask,

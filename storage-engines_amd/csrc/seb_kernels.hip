@@ -736,6 +736,50 @@ __global__ __launch_bounds__(256) void k_probe_interleaved_packed(const uint64_t
     }
 }
 
+// Phased form of the interleaved probe (the bloom probe's phased gather, §5.3 of DESIGN.md): one
+// launch per table range, so every XCD gathers from the same range while it sits in L2.  The
+// mask array carries liveness between phases (0 = every filter already said no).  Phase 0
+// hashes the keys, writes their packed residues and gathers range 0; phase p > 0 regenerates the
+// positions from the packed words of keys whose mask is still non-zero.  `first`: phase 0 run
+// from packed words (the broadcast batch of C5 at N > 1), every key starting with all bits set.
+template <typename Src, typename MaskT>
+__global__ __launch_bounds__(256) void k_probe_interleaved_phase0(Src src, uint64_t n, const MaskT *__restrict__ table,
+                                                                  ModArg md, MaskT *__restrict__ mask,
+                                                                  uint64_t *__restrict__ packed, uint32_t hi) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t h1, h2;
+        src.hash(i, h1, h2);
+        uint32_t pos[7];
+        for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[q] = (uint32_t)p; });
+        __builtin_nontemporal_store(pack_residue(h1, h2, md), packed + i);
+        MaskT acc = (MaskT)~(MaskT)0;
+#pragma unroll
+        for (int q = 0; q < 7; ++q)
+            if (acc && pos[q] < hi) acc &= table[pos[q]];
+        mask[src.index(i)] = acc;
+    }
+}
+
+template <typename MaskT>
+__global__ __launch_bounds__(256) void k_probe_interleaved_phase(const uint64_t *__restrict__ packed, uint64_t n,
+                                                                 const MaskT *__restrict__ table, ModArg md,
+                                                                 MaskT *__restrict__ mask, uint32_t lo, uint32_t hi,
+                                                                 uint32_t first) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        MaskT acc = first ? (MaskT)~(MaskT)0 : mask[i];
+        if (!acc) continue;
+        uint32_t pos[7];
+        packed_positions(__builtin_nontemporal_load(packed + i), (uint32_t)md.m, (uint32_t)md.c, pos);
+        const MaskT in = acc;
+#pragma unroll
+        for (int q = 0; q < 7; ++q)
+            if (acc && pos[q] - lo < hi - lo) acc &= table[pos[q]];
+        if (acc != in || first) mask[i] = acc;
+    }
+}
+
 // Batched build of independent small filters: one workgroup per filter, the whole filter held
 // in LDS (ds_or_b32 atomics, no global atomics), then OR-merged into HBM with coalesced
 // accesses.  Filters too large for LDS go through k_build.
@@ -768,6 +812,42 @@ static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
     if (g < 1) g = 1;
     return (unsigned)(g > cap ? cap : g);
 }
+
+// Table ranges of the phased interleaved probe: one per 4 MiB of table (0 = not phased).
+uint32_t multi_phase_count(uint64_t m, uint32_t mask_bytes) {
+    const int o = options().multi_phases;
+    if (o == 1) return 0;
+    if (o > 1) return (uint32_t)o;
+    const uint64_t bytes = m * mask_bytes;
+    const uint64_t np = (bytes + (4u << 20) - 1) >> 22;
+    return np > 1 ? (uint32_t)np : 0;
+}
+
+template <typename MaskT>
+static hipError_t interleaved_phased(const KeyBatch *kb, uint64_t n, const MaskT *table, const ModArg &md, MaskT *mask,
+                                     uint64_t *packed, uint32_t np, hipStream_t s) {
+    auto bound = [&](uint32_t p) { return (uint32_t)(md.m * p / np); };
+    uint32_t p0 = 0;
+    const unsigned g = grid_for(n, 256, options().grid_cap);
+    if (kb) {
+        hipError_t e = with_src(*kb, [&](auto src) {
+            using S = decltype(src);
+            hipLaunchKernelGGL((k_probe_interleaved_phase0<S, MaskT>), dim3(g), dim3(256), 0, s, src, n, table, md, mask,
+                               packed, bound(1));
+            return hipGetLastError();
+        });
+        if (e != hipSuccess) return e;
+        p0 = 1;
+    }
+    for (uint32_t p = p0; p < np; ++p) {
+        hipLaunchKernelGGL((k_probe_interleaved_phase<MaskT>), dim3(g), dim3(256), 0, s, packed, n, table, md, mask,
+                           bound(p), bound(p + 1), p == 0 ? 1u : 0u);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 
 Options &options() {
     static Options o;
@@ -920,13 +1000,16 @@ static hipError_t launch_multi_t(const Src &src, uint64_t n, const MultiArg &ma,
 }
 
 template <typename MaskT>
-static hipError_t interleaved_mask(const KeyBatch &kb, const MultiArg &ma, void *mask, void *ws, hipStream_t s) {
+static hipError_t interleaved_mask(const KeyBatch &kb, const MultiArg &ma, void *mask, void *ws, uint64_t *packed,
+                                   hipStream_t s) {
     const ModArg &md = ma.f[0].md;
     const uint64_t nwords = (md.m + 31) / 32;
     MaskT *table = (MaskT *)ws;
     // valid-bit mask: filters beyond nf must read 0, which the zero-initialised entries give
     hipLaunchKernelGGL((k_interleave<MaskT>), dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, ma, nwords, md.m,
                        table);
+    if (packed) return interleaved_phased<MaskT>(&kb, kb.n, table, md, (MaskT *)mask, packed,
+                                                 multi_phase_count(md.m, sizeof(MaskT)), s);
     const uint64_t entries_per_slice_shift = 21 - (sizeof(MaskT) == 1 ? 0 : sizeof(MaskT) == 2 ? 1 : sizeof(MaskT) == 4 ? 2 : 3);
     const uint32_t shift = (uint32_t)entries_per_slice_shift;  // 2 MiB of table per slice
     const uint32_t nsl = (uint32_t)((md.m + (1ull << shift) - 1) >> shift);
@@ -947,6 +1030,8 @@ static hipError_t interleaved_mask_packed(const uint64_t *packed, uint64_t n, co
     MaskT *table = (MaskT *)ws;
     hipLaunchKernelGGL((k_interleave<MaskT>), dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, ma, nwords, md.m,
                        table);
+    if (const uint32_t np = multi_phase_count(md.m, sizeof(MaskT)))
+        return interleaved_phased<MaskT>(nullptr, n, table, md, (MaskT *)mask, const_cast<uint64_t *>(packed), np, s);
     const uint32_t shift = 21 - (sizeof(MaskT) == 1 ? 0 : sizeof(MaskT) == 2 ? 1 : sizeof(MaskT) == 4 ? 2 : 3);
     const uint32_t nsl = (uint32_t)((md.m + (1ull << shift) - 1) >> shift);
     const unsigned g = grid_for((n + 1) / 2, 256, options().grid_cap);
@@ -975,13 +1060,13 @@ uint64_t interleaved_bytes(const MultiArg &ma, uint32_t mask_bytes) {
 }
 
 hipError_t launch_probe_interleaved(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes, void *ws,
-                                    hipStream_t s) {
+                                    uint64_t *packed, hipStream_t s) {
     if (kb.n == 0) return hipSuccess;
     switch (mask_bytes) {
-        case 1: return interleaved_mask<uint8_t>(kb, ma, mask, ws, s);
-        case 2: return interleaved_mask<uint16_t>(kb, ma, mask, ws, s);
-        case 4: return interleaved_mask<uint32_t>(kb, ma, mask, ws, s);
-        default: return interleaved_mask<uint64_t>(kb, ma, mask, ws, s);
+        case 1: return interleaved_mask<uint8_t>(kb, ma, mask, ws, packed, s);
+        case 2: return interleaved_mask<uint16_t>(kb, ma, mask, ws, packed, s);
+        case 4: return interleaved_mask<uint32_t>(kb, ma, mask, ws, packed, s);
+        default: return interleaved_mask<uint64_t>(kb, ma, mask, ws, packed, s);
     }
 }
 

@@ -283,14 +283,16 @@ def test_multi_packed_matches_multi(seb, golden, torch_cuda):
     pk8 = seb.dev_keys(torch.from_numpy(keys8).cuda(), n=nn, stride=16)
     p8 = torch.zeros(nn, dtype=torch.int64, device="cuda")
     seb.dev_pack_residues(pk8, m, k, p8)
-    m8 = torch.full((nn + 1,), 7, dtype=torch.uint8, device="cuda")
-    seb.dev_probe_multi_packed(p8, nn, sub, m8)
-    torch.cuda.synchronize()
     host = [(seb.words_to_bits(w, m), m, k) for w, m, k in sub]
     ref = oc.probe_multi(host, keys8, nn, stride=16)
-    got = m8.cpu().numpy()
-    assert np.array_equal(got[:nn].astype(np.uint64), ref)
-    assert got[nn] == 7
+    for phases in (0, 1, 3):  # auto (one range: sliced), sliced, phased
+        with seb.option("multi_phases", phases):
+            m8 = torch.full((nn + 1,), 7, dtype=torch.uint8, device="cuda")
+            seb.dev_probe_multi_packed(p8, nn, sub, m8)
+            torch.cuda.synchronize()
+        got = m8.cpu().numpy()
+        assert np.array_equal(got[:nn].astype(np.uint64), ref), phases
+        assert got[nn] == 7
     m2, k2 = seb.params(per + 1, 0.01)
     with pytest.raises(seb.SebError):
         seb.dev_probe_multi_packed(p8, nn, sub + [(seb.new_words(m2), m2, k2)],
@@ -716,9 +718,10 @@ def test_multi_filter_probe(seb, golden, torch_cuda, which):
     assert np.array_equal(mm.cpu().numpy(), ref.astype(np.uint8))
 
 
-@pytest.mark.parametrize("interleave", [0, 1])
-def test_multi_filter_interleaved_vs_direct(seb, golden, torch_cuda, interleave):
-    """The interleaved (bit-transposed) table path and the per-filter path give identical masks."""
+@pytest.mark.parametrize("interleave,phases", [(0, 0), (1, 0), (1, 1), (1, 2), (1, 3), (1, 5)])
+def test_multi_filter_interleaved_vs_direct(seb, golden, torch_cuda, interleave, phases):
+    """The interleaved (bit-transposed) table path and the per-filter path give identical masks;
+    phases > 1 forces the phased interleaved probe (one launch per table range) on a small table."""
     torch = torch_cuda
     row = golden["multi"][1]  # 64 filters x 2000 keys
     nf, per, npr, m, k = row["filters"], row["keys_per_filter"], row["probes"], row["m"], row["k"]
@@ -729,7 +732,7 @@ def test_multi_filter_interleaved_vs_direct(seb, golden, torch_cuda, interleave)
     half = q // 2
     kd = seb.dev_keys(to_dev(torch, kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q))),
                       n=npr, stride=16)
-    with seb.option("multi_interleave", interleave):
+    with seb.option("multi_interleave", interleave), seb.option("multi_phases", phases):
         for dt, nsub in ((torch.int64, 64), (torch.int32, 32), (torch.int16, 16), (torch.uint8, 8)):
             mask = torch.zeros(npr, dtype=dt, device="cuda")
             seb.dev_probe_multi(kd, filters[:nsub], mask)
