@@ -43,10 +43,11 @@ GOLDEN_C5 = "0668715db8804f529bc6795461a1cbd9905bbaab44b18b88a3b29881cd29f375"  
 GOLDEN_LSM = "caf8282a71e15e15141639089e86e2ae5adabdfc91f69ea47e28fe5d71a941f9"  # sha256(MultiGet masks)
 GOLDEN_ROUTE = "d4ba568830284e7cac12e54c58ea3b6e35b5acd0fbe1cafe90269f177f778ff0"  # sha256(u32 perm), 10M, 8 bits
 GOLDEN_ROUTE_BEGIN = "0afec9b77141e0845ef7750736ed4667d1d1adf3df91c0ab47e85c09302ba1ff"  # sha256(u64 shard_begin)
+GOLDEN_MANY = "18f390ebd4082f2282f8f6352c2e02f946e855b57078fcd4f21e81956050baa7"  # sha256 of the 64 C5 filter digests
 GOLDEN_WAL = "7d661e321c2804cebf541abd9c1a34463b70fe27fce3c5459a71408ac91b3e01"  # sha256(u32 CRCs), 2M records
 OPTIONS = ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "bucket_min_keys",
            "multi_interleave", "varlen_prehash_min_keys", "varlen_sort_min_keys", "scatter_threads",
-           "stream_nt", "probe_persistent", "scatter_kpt", "probe_mode", "wal_lds_kib", "probe_phases", "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win", "varlen_prehash_packed", "apply_threads", "probe_pack_first", "multi_phases")
+           "stream_nt", "probe_persistent", "scatter_kpt", "probe_mode", "wal_lds_kib", "probe_phases", "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win", "varlen_prehash_packed", "apply_threads", "probe_pack_first", "multi_phases", "many_splits")
 
 
 def sha(b) -> str:
@@ -58,7 +59,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "lsm", "route", "wal"])
+    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "lsm", "route", "wal", "many"])
     ap.add_argument("--keys", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
@@ -336,6 +337,46 @@ def setup_route(args, seb, kg, torch, dev, rank, world, dist):
     return st
 
 
+def setup_many(args, seb, kg, torch, dev, rank, world, dist):
+    """one compaction's output filters built in one launch
+    (lsm/compaction.go:226-333, NewBloomFilter(100000, 0.01) per output file): 64 filters of 100K
+    keys each (the C5 filter set), cleared and rebuilt every step from 6.4M device-resident keys
+    (seb_dev_build_many).  Every GPU builds its own compaction's filters: weak scaling."""
+    st = Setup()
+    nf, per = 64, 100_000
+    m, k = seb.params(per, 0.01)
+    st.m, st.k, st.n = m, k, nf * per
+    keys = torch.from_numpy(kg.key16(np.arange(nf * per))).to(dev)
+    st.kd = seb.dev_keys(keys, n=nf * per, stride=16)
+    st.table = torch.zeros((nf, seb.words_bytes(m) // 4), dtype=torch.int32, device=dev)
+    st.filters = [(st.table[f], m, k) for f in range(nf)]
+    begin = [f * per for f in range(nf + 1)]
+    nb = (m + 7) // 8
+    st.kernel_bytes = {"build_many": 16.0 * nf * per + 2.0 * nf * nb}  # keys + clear + filter writes
+    st.units_per_step = float(nf * per) * world
+    st.probe_name = "build_many"
+    st.workload = ("compaction output filters (SURVEY 8(f) row 3): clear + build 64 filters of 100K x 16-B keys "
+                   "@1% FPR (m=958,506, k=7) in one batched launch")
+    st.parallelism = f"independent compaction per gpu x{world}"
+
+    def build_many(j, buf, target):
+        st.table.zero_()
+        seb.dev_build_many(st.kd, begin, st.filters)
+
+    def parity(j):
+        if rank != 0:
+            return None
+        import struct
+        head = struct.pack("<QI", m, k)
+        fsha = [sha(head + seb.words_to_bits(w, m).tobytes()) for w, _, _ in st.filters]
+        ok = sha("".join(fsha).encode()) == GOLDEN_MANY
+        return "bit-exact (sha256 of the 64 filters' Encode() digests matches tests/golden c5)" if ok \
+            else "MISMATCH filters"
+
+    st.probe, st.parity = build_many, parity
+    return st
+
+
 def setup_wal(args, seb, kg, torch, dev, rank, world, dist):
     """ReadAll's integrity check of a WAL image (lsm/wal.go:98-133) on the GPU:
     CRC32-IEEE of every record's [4:] against its stored field, plus framing.  2M records of
@@ -401,7 +442,7 @@ def main():
         if v is not None:
             seb.set_option(o, v)
 
-    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "lsm": setup_lsm, "route": setup_route,
+    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "lsm": setup_lsm, "route": setup_route, "many": setup_many,
              "wal": setup_wal}[args.config]
     st = setup(args, seb, kg, torch, dev, rank, world, dist)
     torch.cuda.synchronize()

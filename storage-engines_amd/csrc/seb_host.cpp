@@ -108,6 +108,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "probe_phases") && value >= 0 && value <= 64) o.probe_phases = (int)value;
     else if (!strcmp(name, "probe_pack_first") && (value == 0 || value == 1)) o.probe_pack_first = (int)value;
     else if (!strcmp(name, "multi_phases") && value >= 0 && value <= 64) o.multi_phases = (int)value;
+    else if (!strcmp(name, "many_splits") && value >= 0 && value <= 64) o.many_splits = (uint32_t)value;
     else if (!strcmp(name, "probe_phase0_pct") && value >= 0 && value <= 90) o.probe_phase0_pct = (int)value;
     else if (!strcmp(name, "probe_phase0_kpt") && (value == 1 || value == 2 || value == 4)) o.probe_phase0_kpt = (int)value;
     else if (!strcmp(name, "multiget_pass_kib") && value >= 0 && value <= (1 << 22)) o.multiget_pass_kib = (int)value;
@@ -131,7 +132,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
 // Every knob of seb_set_option; SEB_<NAME> in the environment sets its initial value.
 static const char *const kOptionNames[] = {
     "build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "multi_interleave",
-    "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases", "probe_pack_first", "multi_phases",
+    "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases", "probe_pack_first", "multi_phases", "many_splits",
     "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
     "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
     "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys"};
@@ -175,6 +176,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "probe_phases")) *value = o.probe_phases;
     else if (!strcmp(name, "probe_pack_first")) *value = o.probe_pack_first;
     else if (!strcmp(name, "multi_phases")) *value = o.multi_phases;
+    else if (!strcmp(name, "many_splits")) *value = o.many_splits;
     else if (!strcmp(name, "probe_phase0_pct")) *value = o.probe_phase0_pct;
     else if (!strcmp(name, "probe_phase0_kpt")) *value = o.probe_phase0_kpt;
     else if (!strcmp(name, "multiget_pass_kib")) *value = o.multiget_pass_kib;

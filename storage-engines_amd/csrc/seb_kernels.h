@@ -97,6 +97,7 @@ struct Options {
     int wal_lds_kib = 36;         // WAL CRC: LDS staging window per 256-record workgroup (36 or 48)
     int probe_phase0_pct = 0;     // phased probe: share of the filter in range 0 (0 = even split)
     int probe_phase0_kpt = 1;     // phased probe: keys per thread in phase 0 (1, 2, 4)
+    uint32_t many_splits = 0;     // batched small-filter build: workgroups per filter (0 = auto, one per CU)
     int multi_phases = 1;         // phased interleaved multi-filter probe: ranges (1 = off, the default: measured slower
                                   // on C5; 0 = one per 4 MiB of table; n > 1 = n ranges)
     int probe_pack_first = 0;     // phased probe: pack residues in a streaming pass instead of in phase 0

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include <type_traits>
 
 #include "seb_device.h"
@@ -784,17 +786,23 @@ __global__ __launch_bounds__(256) void k_probe_interleaved_phase(const uint64_t 
     }
 }
 
-// Batched build of independent small filters: one workgroup per filter, the whole filter held
-// in LDS (ds_or_b32 atomics, no global atomics), then OR-merged into HBM with coalesced
-// accesses.  Filters too large for LDS go through k_build.
+// Batched build of independent small filters (compaction outputs, lsm/compaction.go:226-333): each
+// filter's keys are split over `splits` workgroups, each holding the whole filter in LDS
+// (ds_or_b32, no global atomics while hashing), then OR-merging its image into HBM: a plain
+// read-modify-write when one workgroup owns the filter, device-scope atomic ORs of the non-zero
+// words when several do.  One workgroup per filter left 32 of the 256 CUs busy for a 32-filter
+// launch.  Filters too large for LDS go through k_build.
 template <typename Src, int KFIX, bool M32>
-__global__ __launch_bounds__(1024) void k_build_many_lds(Src src, ManyArg ma) {
+__global__ __launch_bounds__(1024) void k_build_many_lds(Src src, ManyArg ma, uint32_t splits) {
     extern __shared__ uint32_t lds[];
-    const ManyFilter &F = ma.f[blockIdx.x];
+    const ManyFilter &F = ma.f[blockIdx.x / splits];
+    const uint32_t part = blockIdx.x % splits;
     const uint32_t nw = (uint32_t)F.nwords;
+    const uint64_t nk = F.key_end - F.key_begin;
+    const uint64_t k0 = F.key_begin + nk * part / splits, k1 = F.key_begin + nk * (part + 1) / splits;
     for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) lds[j] = 0u;
     __syncthreads();
-    for (uint64_t i = F.key_begin + threadIdx.x; i < F.key_end; i += blockDim.x) {
+    for (uint64_t i = k0 + threadIdx.x; i < k1; i += blockDim.x) {
         uint64_t h1, h2;
         src.hash(i, h1, h2);
         for_positions<KFIX, M32>(h1, h2, F.md, F.md.k, [&](uint32_t, uint64_t p) {
@@ -803,9 +811,16 @@ __global__ __launch_bounds__(1024) void k_build_many_lds(Src src, ManyArg ma) {
         });
     }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) {
-        uint32_t v = lds[j];
-        if (v) F.words[j] |= v;
+    if (splits == 1) {
+        for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) {
+            const uint32_t v = lds[j];
+            if (v) F.words[j] |= v;
+        }
+    } else {
+        for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) {
+            const uint32_t v = lds[j];
+            if (v) __hip_atomic_fetch_or(F.words + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -1111,10 +1126,18 @@ hipError_t launch_build_many_lds(const KeyBatch &kb, const ManyArg &ma, uint32_t
     }
     return with_src(kb, [&](auto src) {
         using S = decltype(src);
+        // splits: enough workgroups for one per CU (256), at least 8K keys each
+        uint64_t most = 0;
+        for (uint32_t f = 0; f < ma.nf; ++f) most = std::max<uint64_t>(most, ma.f[f].key_end - ma.f[f].key_begin);
+        uint32_t splits = options().many_splits;
+        if (splits == 0) {
+            splits = (256 + ma.nf - 1) / ma.nf;
+            while (splits > 1 && most / splits < 8192) --splits;
+        }
         auto go = [&](auto kern) {
             hipError_t e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(kern, dim3(ma.nf), dim3(1024), lds_bytes, s, src, ma);
+            hipLaunchKernelGGL(kern, dim3(ma.nf * splits), dim3(1024), lds_bytes, s, src, ma, splits);
             return hipGetLastError();
         };
         if (m32) return k7 ? go(k_build_many_lds<S, 7, true>) : go(k_build_many_lds<S, 0, true>);

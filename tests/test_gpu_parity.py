@@ -760,6 +760,30 @@ def test_multi_filter_host_api(seb, golden, ctx):
     assert sha(got.astype("<u8").tobytes()) == row["mask_sha256"]
 
 
+@pytest.mark.parametrize("splits", [0, 1, 3, 8])
+def test_build_many_splits(seb, torch_cuda, splits):
+    """Compaction filters whose keys are split over several workgroups (atomic OR merge) equal the
+    oracle; ragged key counts, an empty filter, and filters that already hold bits (OR-accumulate)."""
+    torch = torch_cuda
+    counts = [100_000, 33_333, 0, 65_537, 100_000, 1]
+    begin = np.concatenate([[0], np.cumsum(counts)]).tolist()
+    n = begin[-1]
+    keys = kg.key16(np.arange(n) * 3 + 7)
+    m, k = oc.params(100_000, 0.01)
+    pre = kg.key16(np.arange(5000) * 5 + 1)  # bits already set in every filter
+    filters = []
+    for _ in counts:
+        w = seb.new_words(m)
+        seb.dev_build(seb.dev_keys(to_dev(torch, pre), n=5000, stride=16), w, m, k)
+        filters.append((w, m, k))
+    with seb.option("many_splits", splits):
+        seb.dev_build_many(seb.dev_keys(to_dev(torch, keys), n=n, stride=16), begin, filters)
+    torch.cuda.synchronize()
+    for f, c in enumerate(counts):
+        ref = oc.build(m, k, np.concatenate([pre, keys[begin[f]:begin[f + 1]]]), 5000 + c, stride=16)
+        assert np.array_equal(seb.words_to_bits(filters[f][0], m), ref), f
+
+
 def test_build_many_compaction_batch(seb, golden, torch_cuda):
     """Batched compaction-output build (lsm/compaction.go:286, 100K-key filters) in one launch:
     small filters built in LDS, one filter larger than LDS through the global path."""

@@ -35,7 +35,12 @@ STEP_KERNELS = {  # per config: timed step name -> kernels launched by that step
     "lsm": {"probe": ("k_multiget",)},
     "route": {"route": ("k_route_tile", "k_route_scan_rows", "k_route_scatter")},
     "wal": {"wal_verify": ("k_wal_crc",)},
+    "many": {"build_many": ("k_build_many",)},
 }
+
+
+# kernels launched more than once per timed step (besides the phased probe's, weighted above)
+LAUNCHES_PER_STEP = {"many": {"k_build_many": 2}}  # 64 filters = two 32-filter launches
 
 
 def main():
@@ -75,6 +80,7 @@ def main():
             v = mean[(k, c)]
             if "k_probe_phase<" in k and p0:
                 v *= max(1, round(count[(k, c)] / p0[0]))
+            v *= LAUNCHES_PER_STEP.get(a.config, {}).get(next((p for p in pats if p in k), ""), 1)
             if c == "FETCH_SIZE":
                 fetch += v
                 kernels.append(k)
