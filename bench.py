@@ -41,6 +41,7 @@ GOLDEN_C2 = "a86f3c69041ea0caac1dc559cfb36b06d5d5513d4ee203d22878715f612a0c3a"  
 GOLDEN_C3 = "aba77536fae51d566de525f519cd4c573799880d63000d88a2ce3052d0b90f95"  # sha256(answers)
 GOLDEN_C5 = "0668715db8804f529bc6795461a1cbd9905bbaab44b18b88a3b29881cd29f375"  # sha256(u64 masks)
 GOLDEN_LSM = "caf8282a71e15e15141639089e86e2ae5adabdfc91f69ea47e28fe5d71a941f9"  # sha256(MultiGet masks)
+GOLDEN_LSM_WIDE = "0f50077ccda60050f48634839339b470a5ab0dd5454a277b17c296f0a0dc65b6"  # sha256(candidate rows)
 GOLDEN_ROUTE = "d4ba568830284e7cac12e54c58ea3b6e35b5acd0fbe1cafe90269f177f778ff0"  # sha256(u32 perm), 10M, 8 bits
 GOLDEN_ROUTE_BEGIN = "0afec9b77141e0845ef7750736ed4667d1d1adf3df91c0ab47e85c09302ba1ff"  # sha256(u64 shard_begin)
 GOLDEN_MANY = "18f390ebd4082f2282f8f6352c2e02f946e855b57078fcd4f21e81956050baa7"  # sha256 of the 64 C5 filter digests
@@ -59,7 +60,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "lsm", "route", "wal", "many"])
+    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "lsm", "lsm_wide", "route", "wal",
+                                                           "many"])
     ap.add_argument("--keys", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
@@ -268,9 +270,13 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
 def setup_lsm(args, seb, kg, torch, dev, rank, world, dist):
     """a device-resident filter registry for a 3-level LSM (4 overlapping
     L0 files of 250K keys, 8 L1 files of 1M, 16 L2 files of 500K; keygen.lsm_files) and one batched
-    MultiGet of 10M keys (half present) that resolves LSM.Get's file walk + bloom checks on the GPU."""
+    MultiGet of 10M keys (half present) that resolves LSM.Get's file walk + bloom checks on the GPU.
+    lsm_wide: the same key span in 244 compaction-sized files (4 L0 x 250K, 80 L1 x 100K, 160 L2 x
+    50K; lsm/compaction.go:253), past the u64 mask form: the candidate-list form (6 u16 per key)
+    with the slot table read from HBM/L2."""
     st = Setup()
-    lay = kg.LSM_LAYOUT
+    wide = args.config == "lsm_wide"
+    lay = kg.LSM_WIDE_LAYOUT if wide else kg.LSM_LAYOUT
     files = kg.lsm_files(lay)
     st.reg = seb.Registry(dev.index)
     for level, file_num, idx in files:
@@ -285,18 +291,31 @@ def setup_lsm(args, seb, kg, torch, dev, rank, world, dist):
     st.m, st.k, st.n = 0, 7, n
     pk = torch.from_numpy(kg.key16(kg.lsm_probe_indices(lay))).to(dev)
     st.pk = seb.dev_keys(pk, n=n, stride=16)
-    st.mask = torch.zeros(n, dtype=torch.int64, device=dev)
     filt_bytes = sum((seb.params(len(i), 0.01)[0] + 7) // 8 for _, _, i in files)
-    st.kernel_bytes = {"probe": 16.0 * n + filt_bytes + 8.0 * n}
     st.units_per_step = float(n) * world
-    st.workload = ("LSM MultiGet (SURVEY 8(f)): registry of 28 SSTable filters (L0 4x250K overlapping, L1 8x1M, "
-                   "L2 16x500K keys); one 10M-key batch resolved per LSM.Get's file walk + bloom checks")
     st.parallelism = f"registry-per-gpu x{world}"
-    st.probe = lambda j, buf, target: st.reg.multiget_dev(st.pk, st.mask)
+    if wide:
+        cap = st.reg.max_candidates()
+        st.rows = torch.zeros((n, cap), dtype=torch.int16, device=dev)
+        st.kernel_bytes = {"probe": 16.0 * n + filt_bytes + 2.0 * cap * n}
+        st.workload = (f"LSM MultiGet (SURVEY 8(f)), list form: registry of {len(files)} SSTable filters (L0 4x250K "
+                       "overlapping, L1 80x100K, L2 160x50K keys); one 10M-key batch resolved per LSM.Get's file walk "
+                       f"+ bloom checks into {cap} u16 candidate slots per key")
+        st.probe = lambda j, buf, target: st.reg.multiget_list_dev(st.pk, st.rows, cap)
+    else:
+        st.mask = torch.zeros(n, dtype=torch.int64, device=dev)
+        st.kernel_bytes = {"probe": 16.0 * n + filt_bytes + 8.0 * n}
+        st.workload = ("LSM MultiGet (SURVEY 8(f)): registry of 28 SSTable filters (L0 4x250K overlapping, L1 8x1M, "
+                       "L2 16x500K keys); one 10M-key batch resolved per LSM.Get's file walk + bloom checks")
+        st.probe = lambda j, buf, target: st.reg.multiget_dev(st.pk, st.mask)
 
     def parity(j):
         if rank != 0:
             return None
+        if wide:
+            ok = sha(st.rows.cpu().numpy().view(np.uint16).astype("<u2").tobytes()) == GOLDEN_LSM_WIDE
+            return ("bit-exact (sha256 of the 10M x 6 candidate rows matches tests/golden lsm_wide)" if ok
+                    else "MISMATCH candidate rows")
         ok = sha(st.mask.cpu().numpy().view(np.uint64).astype("<u8").tobytes()) == GOLDEN_LSM
         return "bit-exact (sha256 of the 10M MultiGet masks matches tests/golden lsm)" if ok else "MISMATCH masks"
 
@@ -442,7 +461,7 @@ def main():
         if v is not None:
             seb.set_option(o, v)
 
-    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "lsm": setup_lsm, "route": setup_route, "many": setup_many,
+    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "lsm": setup_lsm, "lsm_wide": setup_lsm, "route": setup_route, "many": setup_many,
              "wal": setup_wal}[args.config]
     st = setup(args, seb, kg, torch, dev, rank, world, dist)
     torch.cuda.synchronize()
@@ -548,7 +567,7 @@ def main():
                 traffic = json.load(f).get(st.pmc_key or args.config, {}).get(dom, {}).get("hbm_bytes_per_launch")
         ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
         result = {
-            "metric": METRIC if args.config in ("c2c3", "c4", "c5", "lsm") else f"{args.config} {st.unit}",
+            "metric": METRIC if args.config in ("c2c3", "c4", "c5", "lsm", "lsm_wide") else f"{args.config} {st.unit}",
             "value": round(value, 2), "unit": st.unit, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),
             "higher_is_better": True, "scaling": st.scaling, "vs_baseline": None, "dtype": st.dtype,

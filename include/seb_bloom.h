@@ -216,7 +216,11 @@ int seb_filter_flush(seb_filter *f);
  * lsm/levels.go:45-63 keeps them.  seb_registry_remove frees it (compaction, lsm/compaction.go).
  * seb_registry_multiget: for each key, bit s of maybe[i] is set when registry slot s is a file
  * LSM.Get would consult for the key (every L0 file; per level 1..4 the first file whose range
- * covers it, lsm/lsm.go:168-198) AND its filter may contain the key.  At most 64 files. */
+ * covers it, lsm/lsm.go:168-198) AND its filter may contain the key; the mask form needs every slot
+ * < 64 (a registry that never held more than 64 files).  The list form takes any registry (up to
+ * 4096 files, u16 slot ids): row i of cand (cap u16 per key) lists the slots of those files in the
+ * order Get visits them (L0 in insertion order, then levels 1..4), padded with 0xFFFF; cap must be
+ * >= seb_registry_max_candidates (the L0 file count + the number of non-empty levels 1..4). */
 typedef struct seb_registry seb_registry;
 seb_registry *seb_registry_new(int device);
 void seb_registry_free(seb_registry *reg);
@@ -228,6 +232,10 @@ int seb_registry_remove(seb_registry *reg, uint64_t file_num);
 int seb_registry_slots(seb_registry *reg, uint64_t *file_nums, int32_t *levels, uint32_t cap);
 int seb_registry_multiget(seb_registry *reg, const seb_keys *keys, uint64_t *maybe);          /* host keys */
 int seb_registry_multiget_dev(seb_registry *reg, const seb_keys *keys, uint64_t *maybe, void *stream);
+int seb_registry_max_candidates(seb_registry *reg); /* >= 0, or < 0 on error */
+int seb_registry_multiget_list(seb_registry *reg, const seb_keys *keys, uint16_t *cand, uint32_t cap); /* host */
+int seb_registry_multiget_list_dev(seb_registry *reg, const seb_keys *keys, uint16_t *cand, uint32_t cap,
+                                   void *stream);
 
 /* ---------- hash-index shard routing + WAL record checksums (off the bloom path) ---- */
 /* shard[i] = FNV-1a32(key i) & ((1 << shard_bits) - 1), the reference's getShard

@@ -1165,6 +1165,8 @@ struct seb_registry {
     bool dirty = true;
     DevBuf dslots, dranges;
     uint32_t nslots = 0;
+    uint32_t max_cand = 0;         // longest Get walk: every L0 file + one file per non-empty level 1..4
+    uint32_t max_slot = 0;         // 1 + the largest slot id in use (the mask form needs <= 64)
     RegLayout layout{};
     std::vector<uint32_t> passes;  // MultiGet pass bounds over the lookup-ordered slots
     int pass_kib = -1;             // multiget_pass_kib the bounds were computed for
@@ -1216,11 +1218,12 @@ extern "C" int seb_registry_put(seb_registry *r, uint64_t file_num, int level, c
     for (auto &e : r->entries)
         if (e.file_num == file_num) return fail(SEB_ERR_INVALID, "seb_registry_put: file %llu already registered",
                                                 (unsigned long long)file_num);
-    if (r->entries.size() >= 64) return fail(SEB_ERR_INVALID, "seb_registry_put: registry holds at most 64 files");
-    uint64_t used = 0;
-    for (auto &e : r->entries) used |= 1ull << e.slot;
-    uint32_t slot = 0;
-    while (used >> slot & 1) ++slot;
+    if (r->entries.size() >= kRegMaxFiles)
+        return fail(SEB_ERR_INVALID, "seb_registry_put: registry holds at most %u files", kRegMaxFiles);
+    std::vector<char> used(kRegMaxFiles, 0);
+    for (auto &e : r->entries) used[e.slot] = 1;
+    uint32_t slot = 0;  // lowest free slot: a registry of <= 64 files keeps every slot < 64 (mask form)
+    while (used[slot]) ++slot;
     HIP_OR_FAIL(hipSetDevice(r->device));
     RegEntry e;
     e.file_num = file_num;
@@ -1341,6 +1344,10 @@ static int sync_registry_locked(seb_registry *r) {
     if (!ranges.empty()) HIP_OR_FAIL(hipMemcpy(r->dranges.p, ranges.data(), ranges.size(), hipMemcpyHostToDevice));
     r->nslots = (uint32_t)slots.size();
     r->layout = lay;
+    r->max_cand = lay.hi[0] - lay.lo[0];
+    for (int L = 1; L < 5; ++L) r->max_cand += lay.hi[L] > lay.lo[L] ? 1u : 0u;
+    r->max_slot = 0;
+    for (const RegEntry *e : order) r->max_slot = std::max(r->max_slot, e->slot + 1);
     std::vector<uint64_t> bytes;
     for (const RegEntry *e : order) bytes.push_back(seb_words_bytes(e->m));
     plan_passes(r, bytes);
@@ -1363,49 +1370,93 @@ extern "C" int seb_registry_slots(seb_registry *r, uint64_t *file_nums, int32_t 
     return (int)r->entries.size();
 }
 
-extern "C" int seb_registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t *maybe, void *stream) {
+// Mask form (maybe != null) or list form (cand, cap u16 per key); called with r->mu held and the
+// registry synced.
+static int check_multiget_out(seb_registry *r, uint64_t *maybe, uint16_t *cand, uint32_t cap, uint64_t n,
+                              const char *who) {
+    if (!maybe && !cand && n) return fail(SEB_ERR_INVALID, "%s: null output", who);
+    if (maybe && r->max_slot > 64)
+        return fail(SEB_ERR_INVALID, "%s: slot %u >= 64 does not fit a u64 mask; use seb_registry_multiget_list",
+                    who, r->max_slot - 1);
+    if (cand && cap < r->max_cand)
+        return fail(SEB_ERR_INVALID, "%s: cap %u < %u candidates a key can have", who, cap, r->max_cand);
+    return SEB_OK;
+}
+
+static int registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t *maybe, uint16_t *cand, uint32_t cap,
+                                 void *stream, const char *who) {
     std::call_once(g_env_once, load_env);
     int rc;
-    if (!r) return fail(SEB_ERR_INVALID, "seb_registry_multiget: null registry");
-    if ((rc = check_keys(keys, "seb_registry_multiget"))) return rc;
-    if (!maybe && keys->n) return fail(SEB_ERR_INVALID, "seb_registry_multiget: null output");
+    if (!r) return fail(SEB_ERR_INVALID, "%s: null registry", who);
+    if ((rc = check_keys(keys, who))) return rc;
     std::lock_guard<std::mutex> g(r->mu);
-    if ((rc = sync_registry_locked(r))) return rc;
+    if ((rc = sync_registry_locked(r)) || (rc = check_multiget_out(r, maybe, cand, cap, keys->n, who))) return rc;
     HIP_OR_FAIL(launch_multiget(key_batch(keys), (const RegSlot *)r->dslots.p, r->nslots, r->layout,
-                                (const uint8_t *)r->dranges.p, maybe, r->passes.data(),
+                                (const uint8_t *)r->dranges.p, maybe, cand, cap, r->passes.data(),
                                 (uint32_t)r->passes.size() - 1, (hipStream_t)stream));
     return SEB_OK;
 }
 
-extern "C" int seb_registry_multiget(seb_registry *r, const seb_keys *kb, uint64_t *maybe) {
+static int registry_multiget_host(seb_registry *r, const seb_keys *kb, uint64_t *maybe, uint16_t *cand, uint32_t cap,
+                                  const char *who) {
     int rc;
-    if (!r) return fail(SEB_ERR_INVALID, "seb_registry_multiget: null registry");
-    if ((rc = check_keys(kb, "seb_registry_multiget")) || (rc = validate_offsets(kb, "seb_registry_multiget"))) return rc;
-    if (!maybe && kb->n) return fail(SEB_ERR_INVALID, "seb_registry_multiget: null output");
+    if (!r) return fail(SEB_ERR_INVALID, "%s: null registry", who);
+    if ((rc = check_keys(kb, who)) || (rc = validate_offsets(kb, who))) return rc;
     std::lock_guard<std::mutex> g(r->mu);
-    if ((rc = sync_registry_locked(r))) return rc;
+    if ((rc = sync_registry_locked(r)) || (rc = check_multiget_out(r, maybe, cand, cap, kb->n, who))) return rc;
     if (!r->ctx && (rc = seb_ctx_create(r->device, &r->ctx))) return rc;
     seb_ctx *c = r->ctx;
     std::lock_guard<std::mutex> g2(c->mu);
     HIP_OR_FAIL(hipSetDevice(c->device));
+    const uint64_t per_key = maybe ? 8 : 2ull * cap;
     std::vector<Chunk> chunks;
     plan_chunks(kb, c->chunk_bytes, chunks);
     for (size_t j = 0; j < chunks.size(); ++j) {
         const int b = (int)(j & 1);
         KeyBatch dk{};
         if ((rc = stage_chunk(c, kb, chunks[j], b, &dk))) return rc;
-        if ((rc = c->out[b].reserve(dk.n * 8))) return rc;
+        if ((rc = c->out[b].reserve(dk.n * per_key))) return rc;
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));
         HIP_OR_FAIL(launch_multiget(dk, (const RegSlot *)r->dslots.p, r->nslots, r->layout,
-                                    (const uint8_t *)r->dranges.p, (uint64_t *)c->out[b].p, r->passes.data(),
+                                    (const uint8_t *)r->dranges.p, maybe ? (uint64_t *)c->out[b].p : nullptr,
+                                    maybe ? nullptr : (uint16_t *)c->out[b].p, cap, r->passes.data(),
                                     (uint32_t)r->passes.size() - 1, c->s_comp));
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
-        HIP_OR_FAIL(hipMemcpyAsync(maybe + chunks[j].i0, c->out[b].p, dk.n * 8, hipMemcpyDeviceToHost, c->s_d2h));
+        uint8_t *dst = maybe ? (uint8_t *)(maybe + chunks[j].i0) : (uint8_t *)(cand + chunks[j].i0 * cap);
+        HIP_OR_FAIL(hipMemcpyAsync(dst, c->out[b].p, dk.n * per_key, hipMemcpyDeviceToHost, c->s_d2h));
         HIP_OR_FAIL(hipEventRecord(c->ev_d2h[b], c->s_d2h));
     }
     HIP_OR_FAIL(hipStreamSynchronize(c->s_d2h));
     return SEB_OK;
+}
+
+extern "C" int seb_registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t *maybe, void *stream) {
+    if (!maybe && keys && keys->n) return fail(SEB_ERR_INVALID, "seb_registry_multiget: null output");
+    return registry_multiget_dev(r, keys, maybe, nullptr, 0, stream, "seb_registry_multiget");
+}
+
+extern "C" int seb_registry_multiget(seb_registry *r, const seb_keys *kb, uint64_t *maybe) {
+    if (!maybe && kb && kb->n) return fail(SEB_ERR_INVALID, "seb_registry_multiget: null output");
+    return registry_multiget_host(r, kb, maybe, nullptr, 0, "seb_registry_multiget");
+}
+
+extern "C" int seb_registry_max_candidates(seb_registry *r) {
+    if (!r) return fail(SEB_ERR_INVALID, "seb_registry_max_candidates: null registry");
+    std::lock_guard<std::mutex> g(r->mu);
+    int rc = sync_registry_locked(r);
+    return rc ? rc : (int)r->max_cand;
+}
+
+extern "C" int seb_registry_multiget_list(seb_registry *r, const seb_keys *kb, uint16_t *cand, uint32_t cap) {
+    if (!cand && kb && kb->n) return fail(SEB_ERR_INVALID, "seb_registry_multiget_list: null output");
+    return registry_multiget_host(r, kb, nullptr, cand, cap, "seb_registry_multiget_list");
+}
+
+extern "C" int seb_registry_multiget_list_dev(seb_registry *r, const seb_keys *keys, uint16_t *cand, uint32_t cap,
+                                              void *stream) {
+    if (!cand && keys && keys->n) return fail(SEB_ERR_INVALID, "seb_registry_multiget_list: null output");
+    return registry_multiget_dev(r, keys, nullptr, cand, cap, stream, "seb_registry_multiget_list");
 }
 
 // ------------------------------------------------ shard routing + WAL checksums (§8(f) row 4)

@@ -70,9 +70,11 @@ hipError_t launch_route_partition(const KeyBatch &kb, uint32_t bits, uint32_t *p
 hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mode, uint32_t *crc, uint8_t *ok,
                           hipStream_t s);
 // Passes: slots [pass_bounds[p], pass_bounds[p+1]) per launch (npasses == 0: one pass, all slots).
+// cand != null: the list form (cap u16 slots per key, one pass, any nslots) instead of masks.
+constexpr uint32_t kRegMaxFiles = 4096;  // registry capacity (u16 slot ids, 0xFFFF = none)
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
-                           const uint8_t *ranges, uint64_t *maybe, const uint32_t *pass_bounds, uint32_t npasses,
-                           hipStream_t s);
+                           const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap,
+                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s);
 
 // Process-wide tuning knobs (seb_set_option).
 struct Options {

@@ -8,7 +8,9 @@
 // for a whole key batch in one launch: per key it hashes once, tests every L0 filter, and per
 // level 1..4 finds the covering file (bisection over the MinKey-ordered files when the registry
 // verified the level is disjoint, else the reference's linear scan), then tests that one filter.
-// Bit s of the key's mask = slot s is visited AND its filter may contain the key.  Key ranges are
+// Bit s of the key's mask = slot s is visited AND its filter may contain the key (registries whose
+// slots are all < 64), or, in the list form, the key's row of `cap` u16 slots lists those files in
+// the order Get visits them, padded with 0xFFFF (any registry size).  Key ranges are
 // compared in Go string order: bytewise, a proper prefix first; the first 16 bytes come from LDS
 // as big-endian words, longer ties fall back to the bytes in HBM.
 #include <hip/hip_runtime.h>
@@ -19,7 +21,7 @@
 
 namespace seb {
 
-constexpr uint32_t kMaxSlots = 64;
+constexpr uint32_t kMaxSlots = 64;  // slot tables up to this size are staged in LDS
 
 __device__ __forceinline__ uint64_t be64(const uint8_t *p, uint32_t len) {  // first min(len,8) bytes, big-endian
     uint64_t v = 0;
@@ -59,14 +61,24 @@ __device__ __forceinline__ uint32_t test_filter(const RegSlot &sl, uint64_t h1, 
 // re-reads, re-hashes and re-walks every key, which costs more than the L2 misses it saves on the
 // C-LSM layout (1.46 ms in one pass, 2.12 ms in 4 MiB passes): one pass is the default.  Pass 0
 // writes the mask and later passes OR into it.
-template <typename Src, int KFIX, bool M32>
+//
+// MODE 0: u64 mask, slot table in LDS.  MODE 1: candidate list, slot table in LDS.  MODE 2:
+// candidate list, slot table read from HBM/L2 (more than kMaxSlots files: an LSM past L1 holds
+// hundreds, lsm/levels.go:10-14 with ~4 MB files, lsm/compaction.go:253).  The list form always
+// runs as one pass.
+template <typename Src, int KFIX, bool M32, int MODE>
 __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const RegSlot *__restrict__ gslots,
                                                   uint32_t nslots, RegLayout lay, const uint8_t *__restrict__ ranges,
-                                                  uint64_t *__restrict__ maybe, uint32_t pass_lo, uint32_t pass_hi,
+                                                  uint64_t *__restrict__ maybe, uint16_t *__restrict__ cand,
+                                                  uint32_t cap, uint32_t pass_lo, uint32_t pass_hi,
                                                   uint32_t accumulate) {
-    __shared__ RegSlot slots[kMaxSlots];
-    for (uint32_t s = threadIdx.x; s < nslots; s += blockDim.x) slots[s] = gslots[s];
-    __syncthreads();
+    constexpr bool kLds = MODE < 2, kList = MODE > 0;
+    __shared__ RegSlot lslots[kLds ? kMaxSlots : 1];
+    if constexpr (kLds) {
+        for (uint32_t s = threadIdx.x; s < nslots; s += blockDim.x) lslots[s] = gslots[s];
+        __syncthreads();
+    }
+    const RegSlot *slots = kLds ? lslots : gslots;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kb.n; i += stride) {
         const uint8_t *key;
@@ -82,10 +94,20 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         src.hash(i, h1, h2);
         const uint64_t k0 = be64(key, klen), k1 = klen > 8 ? be64(key + 8, klen - 8) : 0ull;
         uint64_t mask = 0;
+        uint16_t *row = kList ? cand + i * (uint64_t)cap : nullptr;
+        uint32_t nc = 0;
+        auto take = [&](const RegSlot &sl) {
+            if (test_filter<KFIX, M32>(sl, h1, h2)) {
+                if constexpr (kList) {
+                    if (nc < cap) row[nc++] = (uint16_t)sl.slot;  // the host checks cap >= the walk's length
+                } else {
+                    mask |= 1ull << sl.slot;
+                }
+            }
+        };
         const uint32_t s0 = lay.lo[0] > pass_lo ? lay.lo[0] : pass_lo;
         const uint32_t s1 = lay.hi[0] < pass_hi ? lay.hi[0] : pass_hi;
-        for (uint32_t s = s0; s < s1; ++s)  // every L0 file (of this pass)
-            mask |= (uint64_t)test_filter<KFIX, M32>(slots[s], h1, h2) << slots[s].slot;
+        for (uint32_t s = s0; s < s1; ++s) take(slots[s]);  // every L0 file (of this pass)
         for (uint32_t L = 1; L < 5; ++L) {
             uint32_t lo = lay.lo[L], hi = lay.hi[L];
             if (lo == hi || hi <= pass_lo || lo >= pass_hi) continue;  // no file of this level in the pass
@@ -113,38 +135,48 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                         hit = (int)s;
                 }
             }
-            if (hit >= (int)pass_lo && hit < (int)pass_hi)
-                mask |= (uint64_t)test_filter<KFIX, M32>(slots[hit], h1, h2) << slots[hit].slot;
+            if (hit >= (int)pass_lo && hit < (int)pass_hi) take(slots[hit]);
         }
-        if (!accumulate)
+        if constexpr (kList) {
+            for (uint32_t j = nc; j < cap; ++j) row[j] = 0xFFFFu;
+        } else if (!accumulate) {
             maybe[i] = mask;
-        else if (mask)
+        } else if (mask) {
             maybe[i] |= mask;
+        }
     }
 }
 
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
-                           const uint8_t *ranges, uint64_t *maybe, const uint32_t *pass_bounds, uint32_t npasses,
-                           hipStream_t s) {
+                           const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap,
+                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s) {
     if (kb.n == 0) return hipSuccess;
-    if (nslots > kMaxSlots) return hipErrorInvalidValue;
+    if (!cand && nslots > kMaxSlots) return hipErrorInvalidValue;  // the mask form stages slots in LDS
     uint64_t g = (kb.n + 255) / 256;
     if (g > 65536) g = 65536;
     const uint32_t one[2] = {0u, nslots};
-    if (npasses == 0) {
+    if (npasses == 0 || cand) {
         pass_bounds = one;
         npasses = 1;
     }
+    const int mode = !cand ? 0 : nslots <= kMaxSlots ? 1 : 2;
     return with_src(kb, [&](auto src) {
         using S = decltype(src);
         for (uint32_t p = 0; p < npasses; ++p) {
             const uint32_t lo = pass_bounds[p], hi = pass_bounds[p + 1], acc = p > 0 ? 1u : 0u;
-            if (lay.all_k7_m32)
-                hipLaunchKernelGGL((k_multiget<S, 7, true>), dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots,
-                                   lay, ranges, maybe, lo, hi, acc);
-            else
-                hipLaunchKernelGGL((k_multiget<S, 0, false>), dim3((unsigned)g), dim3(256), 0, s, src, kb, slots,
-                                   nslots, lay, ranges, maybe, lo, hi, acc);
+            auto go = [&](auto kern) {
+                hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe,
+                                   cand, cap, lo, hi, acc);
+            };
+            if (lay.all_k7_m32) {
+                if (mode == 0) go(k_multiget<S, 7, true, 0>);
+                else if (mode == 1) go(k_multiget<S, 7, true, 1>);
+                else go(k_multiget<S, 7, true, 2>);
+            } else {
+                if (mode == 0) go(k_multiget<S, 0, false, 0>);
+                else if (mode == 1) go(k_multiget<S, 0, false, 1>);
+                else go(k_multiget<S, 0, false, 2>);
+            }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

@@ -110,6 +110,11 @@ def varlen_keys(idx: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
 LSM_LAYOUT = {"l0_files": 4, "l0_keys": 250_000, "l1_files": 8, "l1_keys": 1_000_000, "l2_files": 16,
               "l2_keys": 500_000, "probes": 10_000_000, "seed": 12345}
 
+# The same key span cut into compaction-sized files (lsm/compaction.go:253, 100K entries per output
+# file): 244 files, beyond the u64 mask form, answered in the candidate-list form.
+LSM_WIDE_LAYOUT = {"l0_files": 4, "l0_keys": 250_000, "l1_files": 80, "l1_keys": 100_000, "l2_files": 160,
+                   "l2_keys": 50_000, "probes": 10_000_000, "seed": 12345}
+
 
 def lsm_files(lay=LSM_LAYOUT):
     """Synthetic LSM for the registry/MultiGet config: keys key16(2i).  L1 file j holds

@@ -99,6 +99,9 @@ _SIGS = {
     "seb_registry_slots": (_i, [_vp, C.POINTER(_u64), C.POINTER(C.c_int32), _u32]),
     "seb_registry_multiget": (_i, [_vp, C.POINTER(seb_keys), _vp]),
     "seb_registry_multiget_dev": (_i, [_vp, C.POINTER(seb_keys), _vp, _vp]),
+    "seb_registry_max_candidates": (_i, [_vp]),
+    "seb_registry_multiget_list": (_i, [_vp, C.POINTER(seb_keys), _vp, _u32]),
+    "seb_registry_multiget_list_dev": (_i, [_vp, C.POINTER(seb_keys), _vp, _u32, _vp]),
     "seb_dev_shard_route": (_i, [C.POINTER(seb_keys), _u32, _vp, _vp, _vp]),
     "seb_dev_shard_partition_workspace_size": (_u64, [_u64, _u32]),
     "seb_dev_shard_partition": (_i, [C.POINTER(seb_keys), _u32, _vp, _vp, _vp, _vp, _u64, _vp]),
@@ -366,11 +369,30 @@ class Registry:
     def remove(self, file_num: int) -> None:
         check(lib().seb_registry_remove(self._h, file_num))
 
+    MAX_FILES = 4096  # kRegMaxFiles (u16 slot ids)
+
     def slots(self) -> dict[int, tuple[int, int]]:
-        fn = (_u64 * 64)()
-        lv = (C.c_int32 * 64)()
-        check(lib().seb_registry_slots(self._h, fn, lv, 64))
-        return {s: (fn[s], lv[s]) for s in range(64) if lv[s] >= 0}
+        cap = self.MAX_FILES
+        fn = (_u64 * cap)()
+        lv = (C.c_int32 * cap)()
+        check(lib().seb_registry_slots(self._h, fn, lv, cap))
+        return {s: (fn[s], lv[s]) for s in range(cap) if lv[s] >= 0}
+
+    def max_candidates(self) -> int:
+        """Longest Get walk: every L0 file plus one file per non-empty level 1..4."""
+        return check(lib().seb_registry_max_candidates(self._h))
+
+    def multiget_list(self, keys, cap: int | None = None) -> np.ndarray:
+        """Per key, the slots of the files Get would consult whose filter may contain it, in
+        visiting order, padded with 0xFFFF: an (n, cap) u16 array.  Any registry size."""
+        kb = as_keys(keys)
+        cap = max(self.max_candidates(), 1) if cap is None else cap
+        out = np.zeros((max(kb.n, 1), cap), dtype=np.uint16)
+        check(lib().seb_registry_multiget_list(self._h, kb.ref, out.ctypes.data, cap))
+        return out[: kb.n]
+
+    def multiget_list_dev(self, keys: "seb_keys", out, cap: int, stream=None) -> None:
+        check(lib().seb_registry_multiget_list_dev(self._h, C.byref(keys), out.data_ptr(), cap, _stream(stream)))
 
     def multiget(self, keys) -> np.ndarray:
         kb = as_keys(keys)

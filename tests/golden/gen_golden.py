@@ -165,6 +165,34 @@ def lsm_case(lay=kg.LSM_LAYOUT) -> dict:
             "mask_popcount": int(np.unpackbits(mask.astype("<u8").view(np.uint8)).sum())}
 
 
+def lsm_wide_case(lay=kg.LSM_WIDE_LAYOUT) -> dict:
+    """bench.py --config lsm_wide: the list form.  Row i (cap = L0 files + 2 u16) holds the slots of
+    the files LSM.Get visits for key i whose filter may contain it, in visiting order (L0 in
+    registration order, then L1 and L2 by MinKey; lsm/lsm.go:168-198), padded with 0xFFFF."""
+    files = kg.lsm_files(lay)
+    pidx = kg.lsm_probe_indices(lay)
+    pk = kg.key16(pidx)
+    n = pk.shape[0]
+    slots = {fn: s for s, (_l, fn, _i) in enumerate(files)}  # registration order = slot order
+    order = sorted(files, key=lambda f: (f[0], 0 if f[0] == 0 else int(f[2][0]), slots[f[1]]))
+    cap = lay["l0_files"] + 2
+    rows = np.full((n, cap), 0xFFFF, dtype=np.uint16)
+    cnt = np.zeros(n, dtype=np.int64)
+    for level, fn, idx in order:
+        m, k = oc.params(len(idx), 0.01)
+        bits = oc.build(m, k, kg.key16(2 * idx), len(idx), stride=16, threads=8)
+        if level == 0:
+            sel = np.arange(n)
+        else:
+            sel = np.nonzero((pidx >= 2 * idx[0]) & (pidx <= 2 * idx[-1]))[0]
+        ans = oc.probe(bits, m, k, pk[sel], len(sel), stride=16, threads=8).astype(bool)
+        hit = sel[ans]
+        rows[hit, cnt[hit]] = slots[fn]
+        cnt[hit] += 1
+    return {"layout": lay, "files": len(files), "cap": cap, "rows_sha256": sha(rows.astype("<u2").tobytes()),
+            "candidates": int(cnt.sum())}
+
+
 def _fnv32a_np(keys: np.ndarray) -> np.ndarray:
     """Vectorised FNV-1a 32 over fixed-width keys (second restatement, checks codec_oracle.c)."""
     h = np.full(keys.shape[0], 0x811C9DC5, np.uint32)
@@ -200,7 +228,8 @@ def main():
         with open(OUT) as f:
             out = json.load(f)
         for name in sys.argv[2].split(","):
-            out[name] = {"route": route_case, "wal": wal_case, "lsm": lsm_case, "c5": c5_case}[name]()
+            out[name] = {"route": route_case, "wal": wal_case, "lsm": lsm_case, "c5": c5_case,
+                         "lsm_wide": lsm_wide_case}[name]()
             print(name, out[name], flush=True)
         with open(OUT, "w") as f:
             json.dump(out, f, indent=1)
@@ -254,6 +283,7 @@ def main():
     out["multi"] = [multi_case(8, 10000, 160000, 0.01), multi_case(64, 2000, 256000, 0.01)]
     out["c5"] = c5_case()
     out["lsm"] = lsm_case()
+    out["lsm_wide"] = lsm_wide_case()
     out["route"] = route_case()
     out["wal"] = wal_case()
     with open(OUT, "w") as f:

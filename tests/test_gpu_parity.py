@@ -846,7 +846,15 @@ def test_c_harness_replays_sstable_sequence(seb, golden, n, expected):
 def _lsm_get_model(files, key: bytes):
     """lsm/lsm.go:168-198 candidate walk over (slot, level, min, max, bits, m, k, seq) records:
     every L0 file in insertion order, then per level 1..4 the first file (by MinKey) whose range
-    covers the key.  Returns the slots visited whose filter may contain the key."""
+    covers the key.  Returns the slots visited whose filter may contain the key, as a mask."""
+    mask = 0
+    for s in _lsm_get_walk(files, key):
+        mask |= 1 << s
+    return mask
+
+
+def _lsm_get_walk(files, key: bytes):
+    """The same walk as _lsm_get_model; the slots in visiting order (the list form)."""
     visited = []
     l0 = sorted((f for f in files if f["level"] == 0), key=lambda f: f["seq"])
     visited += l0
@@ -855,12 +863,12 @@ def _lsm_get_model(files, key: bytes):
             if f["min"] <= key <= f["max"]:
                 visited.append(f)
                 break
-    mask = 0
+    out = []
     for f in visited:
         kb = np.frombuffer(key, np.uint8).reshape(1, -1) if key else np.zeros((1, 0), np.uint8)
         if oc.probe(f["bits"], f["m"], f["k"], kb, 1, stride=len(key))[0]:
-            mask |= 1 << f["slot"]
-    return mask
+            out.append(f["slot"])
+    return out
 
 
 @pytest.fixture(params=[0, 4096, 1], ids=["one-pass", "passes-4MiB", "pass-per-file"])
@@ -965,6 +973,87 @@ def test_registry_multiget_overlap_long_keys_generic_k(seb, torch_cuda, multiget
     got = reg.multiget(probes)
     want = np.array([_lsm_get_model(files, p) for p in probes], dtype=np.uint64)
     assert np.array_equal(got, want)
+    reg.close()
+
+
+def _walk_rows(files, probes, cap):
+    want = np.full((len(probes), cap), 0xFFFF, dtype=np.uint16)
+    for i, p in enumerate(probes):
+        w = _lsm_get_walk(files, p)
+        want[i, : len(w)] = w
+    return want
+
+
+def test_registry_multiget_list_beyond_64_files(seb, torch_cuda):
+    """A registry past 64 files (an LSM with populated L1/L2: 400 MB / ~4 MB files,
+    lsm/levels.go:10-14, lsm/compaction.go:253): the slot table is read from HBM instead of LDS
+    and the answer is the list form, the slots Get would consult whose filter may contain the key
+    in visiting order.  The u64 mask form refuses slots >= 64; cap below the longest walk is
+    refused; the list form at <= 64 files (LDS table) agrees with the mask form."""
+    torch = torch_cuda
+    rng = np.random.default_rng(41)
+    reg = seb.Registry(0)
+    files = []
+    seq = 0
+
+    def add(file_num, level, keys):
+        nonlocal seq
+        m, k = oc.params(max(len(keys), 1), 0.01)
+        arr = np.frombuffer(b"".join(keys), np.uint8)
+        bits = oc.build(m, k, arr, len(keys), stride=16)
+        slot = reg.put(file_num, level, bn.encode(bits, m, k), min(keys), max(keys))
+        files.append(dict(file=file_num, level=level, min=min(keys), max=max(keys), bits=bits, m=m, k=k, seq=seq,
+                          slot=slot))
+        seq += 1
+
+    universe = sorted({kg.key16_bytes(int(i)) for i in rng.integers(0, 400000, 40000)})
+    for f in range(3):
+        add(100 + f, 0, sorted(rng.choice(universe, 1500, replace=False).tolist()))
+    for lvl, parts in ((1, 20), (2, 90), (3, 7)):
+        chunks = np.array_split(np.array(universe, dtype=object), parts)
+        for j in rng.permutation(parts):
+            add(1000 * lvl + int(j), lvl, list(chunks[j]))
+    assert len(files) == 120 and max(f["slot"] for f in files) == 119
+    assert reg.max_candidates() == 3 + 3
+    probes = list(rng.choice(universe, 3000).tolist()) + [kg.key16_bytes(int(i)) for i in rng.integers(400000, 800000, 2000)]
+    probes += [universe[0], universe[-1], b"\x00" * 16, b"\xff" * 16]
+    got = reg.multiget_list(probes)
+    assert got.shape == (len(probes), 6)
+    assert np.array_equal(got, _walk_rows(files, probes, 6))
+    # a wider row pads with 0xFFFF
+    got8 = reg.multiget_list(probes[:500], cap=8)
+    assert np.array_equal(got8, _walk_rows(files, probes[:500], 8))
+    with pytest.raises(seb.SebError):
+        reg.multiget(probes[:10])
+    with pytest.raises(seb.SebError):
+        reg.multiget_list(probes[:10], cap=5)
+    # device-resident form on fixed 16-B keys (rng.choice's bytes array drops trailing NULs)
+    fixed = [p for p in probes if len(p) == 16]
+    dk = seb.dev_keys(to_dev(torch, np.frombuffer(b"".join(fixed), np.uint8)), n=len(fixed), stride=16)
+    out = torch.zeros((len(fixed), 6), dtype=torch.int16, device="cuda")
+    reg.multiget_list_dev(dk, out, 6)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), _walk_rows(files, fixed, 6))
+    # L2 compacted away: 30 files (LDS slot table), but L3 keeps slots 113..119, beyond a u64 mask
+    for f in [f for f in files if f["level"] == 2]:
+        reg.remove(f["file"])
+    files = [f for f in files if f["level"] != 2]
+    assert reg.max_candidates() == 5
+    assert np.array_equal(reg.multiget_list(probes), _walk_rows(files, probes, 5))
+    with pytest.raises(seb.SebError):
+        reg.multiget(probes[:10])
+    # L3 gone too: every slot < 64, and the mask form agrees with the list form
+    for f in [f for f in files if f["level"] == 3]:
+        reg.remove(f["file"])
+    files = [f for f in files if f["level"] < 2]
+    assert reg.max_candidates() == 4
+    assert np.array_equal(reg.multiget_list(probes), _walk_rows(files, probes, 4))
+    mask = reg.multiget(probes)  # every remaining slot is < 64: the mask form works again
+    want = np.zeros(len(probes), np.uint64)
+    for i, row in enumerate(_walk_rows(files, probes, 4)):
+        for s in row[row != 0xFFFF]:
+            want[i] |= np.uint64(1) << np.uint64(s)
+    assert np.array_equal(mask, want)
     reg.close()
 
 

@@ -146,3 +146,18 @@ def test_decode_roundtrip_and_nil():
     mm, kk, bb = bn.decode(enc)
     assert (mm, kk) == (m, k) and np.array_equal(bb, bits)
     assert bn.decode(enc[:11]) is None  # lsm/bloom.go:106-108
+
+
+def test_bench_golden_digests_match_fixtures():
+    """bench.py checks its runs against digests it carries inline (the GPU box has no generator);
+    they must be the ones tests/golden/gen_golden.py wrote."""
+    import json
+    import os
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "bench.py")).read()
+    gold = json.load(open(os.path.join(root, "tests", "golden", "golden.json")))
+    consts = dict(re.findall(r'^(GOLDEN_[A-Z_0-9]+) = "([0-9a-f]{64})"', src, re.M))
+    assert consts["GOLDEN_LSM"] == gold["lsm"]["mask_sha256"]
+    assert consts["GOLDEN_LSM_WIDE"] == gold["lsm_wide"]["rows_sha256"]
