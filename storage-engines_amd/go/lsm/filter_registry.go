@@ -1,0 +1,125 @@
+// Filter registry + batched Get filter step (SURVEY.md §8(f) rows 1-2) — additive API beside the
+// drop-in bloom.go.  The reference's callers do not use it; a batched MultiGet would:
+//
+//	OpenSSTable (lsm/sstable.go:121-129)        -> reg.Put(fileNum, level, bloomBlock, minKey, maxKey)
+//	compaction removes inputs (compaction.go:335-343) -> reg.Remove(fileNum)
+//	LSM.Get's walk + MayContain (lsm/lsm.go:168-198) -> reg.Candidates(keys)
+//
+// Not compiled in this repository's pipeline (no Go toolchain in the image); the C ABI it calls is
+// tested through the Python binding (tests/test_gpu_parity.py, test_registry_*).
+package lsm
+
+/*
+#include <stdint.h>
+#include "seb_bloom.h"
+*/
+import "C"
+
+import (
+	"runtime"
+	"unsafe"
+)
+
+// FilterRegistry holds the bloom filters of the open SSTables in HBM (one per LSM instance).
+type FilterRegistry struct {
+	h *C.seb_registry
+}
+
+func regPanic(op string) {
+	panic("lsm: FilterRegistry." + op + ": " + C.GoString(C.seb_last_error()))
+}
+
+// NewFilterRegistry creates an empty registry on GPU `device`.
+func NewFilterRegistry(device int) *FilterRegistry {
+	h := C.seb_registry_new(C.int(device))
+	if h == nil {
+		regPanic("New")
+	}
+	r := &FilterRegistry{h: h}
+	runtime.SetFinalizer(r, func(r *FilterRegistry) { C.seb_registry_free(r.h) })
+	return r
+}
+
+func bytesPtr(b []byte) *C.uint8_t {
+	if len(b) == 0 {
+		return nil
+	}
+	return (*C.uint8_t)(unsafe.Pointer(&b[0]))
+}
+
+// Put registers an SSTable's bloom block (its Encode() bytes) with the file's level and key
+// range; levels 1..4 are kept by MinKey as lsm/levels.go:45-63 keeps them.  Returns the slot.
+func (r *FilterRegistry) Put(fileNum uint64, level int, bloomBlock []byte, minKey, maxKey string) int {
+	mn, mx := []byte(minKey), []byte(maxKey)
+	rc := C.seb_registry_put(r.h, C.uint64_t(fileNum), C.int(level), bytesPtr(bloomBlock), C.uint64_t(len(bloomBlock)),
+		bytesPtr(mn), C.uint64_t(len(mn)), bytesPtr(mx), C.uint64_t(len(mx)))
+	if rc < 0 {
+		regPanic("Put")
+	}
+	runtime.KeepAlive(bloomBlock)
+	return int(rc)
+}
+
+// Remove frees a file's filter (compaction deleted the file).
+func (r *FilterRegistry) Remove(fileNum uint64) {
+	if C.seb_registry_remove(r.h, C.uint64_t(fileNum)) != 0 {
+		regPanic("Remove")
+	}
+}
+
+// Candidates returns, per key, the file numbers Get would read for it — every L0 file and the
+// covering file of each level 1..4 whose bloom filter may contain the key — in Get's visiting
+// order.  One GPU launch for the whole batch, any number of registered files.
+func (r *FilterRegistry) Candidates(keys []string) [][]uint64 {
+	out := make([][]uint64, len(keys))
+	if len(keys) == 0 {
+		return out
+	}
+	data, offs := packKeys(keys)
+	ks := C.seb_keys{data: (*C.uint8_t)(unsafe.Pointer(&data[0])), offsets: (*C.uint64_t)(unsafe.Pointer(&offs[0])),
+		n: C.uint64_t(len(keys))}
+	capRow := int(C.seb_registry_max_candidates(r.h))
+	if capRow < 0 {
+		regPanic("Candidates")
+	}
+	if capRow == 0 {
+		capRow = 1
+	}
+	cand := make([]uint16, len(keys)*capRow)
+	if C.seb_registry_multiget_list(r.h, &ks, (*C.uint16_t)(unsafe.Pointer(&cand[0])), C.uint32_t(capRow)) != 0 {
+		regPanic("Candidates")
+	}
+	runtime.KeepAlive(data)
+	runtime.KeepAlive(offs)
+	const maxFiles = 4096 // kRegMaxFiles
+	fileNums := make([]uint64, maxFiles)
+	if C.seb_registry_slots(r.h, (*C.uint64_t)(unsafe.Pointer(&fileNums[0])), nil, C.uint32_t(maxFiles)) < 0 {
+		regPanic("Candidates")
+	}
+	for i := range keys {
+		for _, s := range cand[i*capRow : (i+1)*capRow] {
+			if s == 0xFFFF {
+				break
+			}
+			out[i] = append(out[i], fileNums[s])
+		}
+	}
+	return out
+}
+
+// packKeys lays keys out as one byte buffer + len(keys)+1 offsets (the seb_keys var-length form).
+func packKeys(keys []string) ([]byte, []uint64) {
+	total := 0
+	for _, k := range keys {
+		total += len(k)
+	}
+	data := make([]byte, total+1)
+	offs := make([]uint64, len(keys)+1)
+	pos := 0
+	for i, k := range keys {
+		offs[i] = uint64(pos)
+		pos += copy(data[pos:], k)
+	}
+	offs[len(keys)] = uint64(pos)
+	return data, offs
+}

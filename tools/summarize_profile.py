@@ -33,6 +33,7 @@ STEP_KERNELS = {  # per config: timed step name -> kernels launched by that step
            "probe": ("k_probe", "k_hash_varlen")},
     "c5": {"probe": ("k_probe_interleaved", "k_interleave", "k_probe_multi")},
     "lsm": {"probe": ("k_multiget",)},
+    "lsm_wide": {"probe": ("k_multiget",)},
     "route": {"route": ("k_route_tile", "k_route_scan_rows", "k_route_scatter")},
     "wal": {"wal_verify": ("k_wal_crc",)},
     "many": {"build_many": ("k_build_many",)},
