@@ -1022,7 +1022,6 @@ template <typename MaskT>
 static hipError_t interleaved_mask(const KeyBatch &kb, const MultiArg &ma, void *mask, void *ws, uint64_t *packed,
                                    hipStream_t s) {
     const ModArg &md = ma.f[0].md;
-    const uint64_t nwords = (md.m + 31) / 32;
     MaskT *table = (MaskT *)ws;
     // valid-bit mask: filters beyond nf must read 0, which the zero-initialised entries give
     hipLaunchKernelGGL((k_interleave<MaskT>), dim3((unsigned)((md.m + 255) / 256)), dim3(256), 0, s, ma, md.m, table);
@@ -1044,7 +1043,6 @@ template <typename MaskT>
 static hipError_t interleaved_mask_packed(const uint64_t *packed, uint64_t n, const MultiArg &ma, void *mask, void *ws,
                                           hipStream_t s) {
     const ModArg &md = ma.f[0].md;
-    const uint64_t nwords = (md.m + 31) / 32;
     MaskT *table = (MaskT *)ws;
     hipLaunchKernelGGL((k_interleave<MaskT>), dim3((unsigned)((md.m + 255) / 256)), dim3(256), 0, s, ma, md.m, table);
     if (const uint32_t np = multi_phase_count(md.m, sizeof(MaskT)))
