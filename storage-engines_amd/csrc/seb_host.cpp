@@ -120,6 +120,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
         o.apply_threads = (uint32_t)value;
     else if (!strcmp(name, "varlen_prehash_packed") && (value == 0 || value == 1))
         o.varlen_prehash_packed = (int)value;
+    else if (!strcmp(name, "build_prepack") && (value == 0 || value == 1)) o.build_prepack = (int)value;
     else if (!strcmp(name, "wal_lds_kib") && (value == 36 || value == 48)) o.wal_lds_kib = (int)value;
     else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
@@ -135,7 +136,7 @@ static const char *const kOptionNames[] = {
     "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases", "probe_pack_first", "multi_phases", "many_splits",
     "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
     "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
-    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys"};
+    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack"};
 
 static std::once_flag g_env_once;
 static void load_env() {
@@ -183,6 +184,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "varlen_hash_keys")) *value = o.varlen_hash_keys;
     else if (!strcmp(name, "varlen_hash_win")) *value = o.varlen_hash_win;
     else if (!strcmp(name, "varlen_prehash_packed")) *value = o.varlen_prehash_packed;
+    else if (!strcmp(name, "build_prepack")) *value = o.build_prepack;
     else if (!strcmp(name, "apply_threads")) *value = o.apply_threads;
     else if (!strcmp(name, "wal_lds_kib")) *value = o.wal_lds_kib;
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
@@ -282,7 +284,11 @@ static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStr
                           Grow &&grow) {
     if (kb.n == 0 || md.k == 0) return SEB_OK;
     const bool bucketed = choose_build_algo(kb.n, md.m, md.k) == 2;
-    if (bucketed && want_prehash_packed(kb, md)) {  // scratch: [packed residues | bucketed]
+    // build_prepack: fixed-width keys hashed to packed residues by a full-occupancy kernel first,
+    // so the scatter (4 waves per SIMD) only derives positions from 8-byte words
+    const bool prepack = bucketed && !kb.offsets && !kb.hashes && options().build_prepack && md.k == 7 &&
+                         md.m < (1ull << kPackBits);
+    if (bucketed && (want_prehash_packed(kb, md) || prepack)) {  // scratch: [packed residues | bucketed]
         const uint64_t pack_b = (kb.n * 8 + 255) & ~255ull;
         const uint64_t need = pack_b + bucketed_workspace_bytes(kb.n, md.m, md.k);
         if (need > ws_bytes) {
@@ -290,7 +296,10 @@ static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStr
             if (rc) return rc;
             ws_bytes = need;
         }
-        HIP_OR_FAIL(launch_hash_varlen_packed(kb, md, (uint64_t *)ws, s));
+        if (prepack)
+            HIP_OR_FAIL(launch_pack_residues(kb, md, (uint64_t *)ws, s));
+        else
+            HIP_OR_FAIL(launch_hash_varlen_packed(kb, md, (uint64_t *)ws, s));
         HIP_OR_FAIL(launch_build_bucketed_packed((const uint64_t *)ws, kb.n, words, md, (uint8_t *)ws + pack_b,
                                                  ws_bytes - pack_b, s));
         return SEB_OK;
@@ -372,7 +381,8 @@ extern "C" uint64_t seb_dev_build_workspace_size(uint64_t n, uint64_t m, uint32_
     const Options &o = options();
     const uint64_t pre_b = n >= o.varlen_prehash_min_keys ? ((n * 16 + 255) & ~255ull) : 0;
     const uint64_t perm_b = !pre_b && n >= o.varlen_sort_min_keys && n <= 0xffffffffull ? len_perm_workspace_bytes(n) : 0;
-    return pre_b + perm_b + (choose_build_algo(n, m, k) == 2 ? bucketed_workspace_bytes(n, m, k) : 0);
+    const uint64_t pack_b = o.build_prepack ? ((n * 8 + 255) & ~255ull) : 0;  // packed residues (build_prepack)
+    return std::max(pre_b + perm_b, pack_b) + (choose_build_algo(n, m, k) == 2 ? bucketed_workspace_bytes(n, m, k) : 0);
 }
 
 extern "C" int seb_dev_build_ws(const seb_keys *keys, uint32_t *words, uint64_t m, uint32_t k, void *ws,

@@ -87,6 +87,7 @@ struct Options {
     uint32_t varlen_hash_win = 72;    // pre-hash LDS window bytes per key (64, 72, 80)
     uint32_t apply_threads = 1024;    // radix-partitioned build: apply workgroup size (256, 512, 1024)
     int varlen_prehash_packed = 1;    // pre-hash to packed residues where k == 7, m < 2^29 (0/1)
+    int build_prepack = 0;            // fixed-width bucketed build: pack residues first (full-occupancy hash), 0/1
     int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)
     int probe_kpt = 2;            // k == 7 probes: keys per thread (1, 2, 4)
     int probe_slice_shift = 19;   // k == 7, m < 2^32: sliced probe with 2^shift-word (2 MiB) slices (0 = off)

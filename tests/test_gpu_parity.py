@@ -165,12 +165,13 @@ def test_host_api_chunked_pipeline(seb, monkeypatch, torch_cuda):
 
 # --------------------------------------------------------- device-resident API --------------
 
-@pytest.fixture(params=[(1, 1024, 4, 1024), (2, 1024, 4, 256), (2, 512, 4, 512), (2, 1024, 5, 1024)],
-                ids=["atomic", "bucketed", "bucketed512", "bucketed-kpt5"])
+@pytest.fixture(params=[(1, 1024, 4, 1024, 0), (2, 1024, 4, 256, 0), (2, 512, 4, 512, 0), (2, 1024, 5, 1024, 0),
+                        (2, 1024, 5, 1024, 1)],
+                ids=["atomic", "bucketed", "bucketed512", "bucketed-kpt5", "bucketed-prepack"])
 def build_algo(request, seb):
-    algo, thr, kpt, apply = request.param
+    algo, thr, kpt, apply, prepack = request.param
     with seb.option("build_algo", algo), seb.option("scatter_threads", thr), seb.option("scatter_kpt", kpt), \
-            seb.option("apply_threads", apply):
+            seb.option("apply_threads", apply), seb.option("build_prepack", prepack):
         yield algo
 
 
