@@ -1058,6 +1058,36 @@ def test_registry_multiget_list_beyond_64_files(seb, torch_cuda):
     reg.close()
 
 
+def test_registry_full_capacity(seb, torch_cuda):
+    """4096 files (the u16 slot-id capacity): one L0 file and 4095 one-key L1 files.  The
+    4097th put is refused; the list form still answers every key as Get's walk does, and a key
+    between two files' ranges visits only L0."""
+    reg = seb.Registry(0)
+    files = []
+
+    def add(file_num, level, keys, seq):
+        m, k = oc.params(len(keys), 0.01)
+        bits = oc.build(m, k, np.frombuffer(b"".join(keys), np.uint8), len(keys), stride=16)
+        slot = reg.put(file_num, level, bn.encode(bits, m, k), min(keys), max(keys))
+        files.append(dict(file=file_num, level=level, min=min(keys), max=max(keys), bits=bits, m=m, k=k, seq=seq,
+                          slot=slot))
+
+    add(1, 0, [kg.key16_bytes(2 * j) for j in range(0, 8190, 7)], 0)
+    for j in range(4095):
+        add(10 + j, 1, [kg.key16_bytes(2 * j)], 1 + j)
+    assert max(f["slot"] for f in files) == 4095
+    m, k = oc.params(1, 0.01)
+    with pytest.raises(seb.SebError):
+        reg.put(99999, 1, bn.encode(np.zeros((m + 7) // 8, np.uint8), m, k), b"zz", b"zz")
+    rng = np.random.default_rng(3)
+    probes = [kg.key16_bytes(int(i)) for i in rng.integers(0, 8190, 300)]
+    probes = [p for p in probes if len(p) == 16]
+    assert reg.max_candidates() == 2
+    got = reg.multiget_list(probes)
+    assert np.array_equal(got, _walk_rows(files, probes, 2))
+    reg.close()
+
+
 @pytest.mark.parametrize("case", ["duplicates", "skewed", "large_m"])
 def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
     """Radix-partitioned build paths a hash-distributed batch never takes: runs that overflow
