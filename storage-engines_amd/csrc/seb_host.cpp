@@ -112,6 +112,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "probe_phase0_pct") && value >= 0 && value <= 90) o.probe_phase0_pct = (int)value;
     else if (!strcmp(name, "probe_phase0_kpt") && (value == 1 || value == 2 || value == 4)) o.probe_phase0_kpt = (int)value;
     else if (!strcmp(name, "multiget_pass_kib") && value >= 0 && value <= (1 << 22)) o.multiget_pass_kib = (int)value;
+    else if (!strcmp(name, "multiget_group") && (value == 0 || value == 1)) o.multiget_group = (int)value;
     else if (!strcmp(name, "varlen_hash_keys") && (value == 256 || value == 512))
         o.varlen_hash_keys = (uint32_t)value;
     else if (!strcmp(name, "varlen_hash_win") && (value == 64 || value == 72 || value == 80))
@@ -136,7 +137,7 @@ static const char *const kOptionNames[] = {
     "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases", "probe_pack_first", "multi_phases", "many_splits",
     "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
     "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
-    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack"};
+    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group"};
 
 static std::once_flag g_env_once;
 static void load_env() {
@@ -181,6 +182,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "probe_phase0_pct")) *value = o.probe_phase0_pct;
     else if (!strcmp(name, "probe_phase0_kpt")) *value = o.probe_phase0_kpt;
     else if (!strcmp(name, "multiget_pass_kib")) *value = o.multiget_pass_kib;
+    else if (!strcmp(name, "multiget_group")) *value = o.multiget_group;
     else if (!strcmp(name, "varlen_hash_keys")) *value = o.varlen_hash_keys;
     else if (!strcmp(name, "varlen_hash_win")) *value = o.varlen_hash_win;
     else if (!strcmp(name, "varlen_prehash_packed")) *value = o.varlen_prehash_packed;

@@ -80,6 +80,7 @@ hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t ns
 struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed)
     int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
+    int multiget_group = 0;       // MultiGet (k = 7, m < 2^32): test filters 4 at a time (1; measured slower) or one by one (0)
     int multiget_pass_kib = 0;    // MultiGet: filter bytes per pass (0 = one pass; passes measured slower)
     uint64_t varlen_sort_min_keys = INT64_MAX;  // length-bucketed order (measured slower; off by default)
     uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys

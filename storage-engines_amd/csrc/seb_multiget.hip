@@ -55,6 +55,48 @@ __device__ __forceinline__ uint32_t test_filter(const RegSlot &sl, uint64_t h1, 
     return acc & 1u;
 }
 
+// MayContain of up to G filters side by side (k = 7, m < 2^32), bit j of `alive` = filter j
+// still to be tested; returns the filters whose 7 bits are all set.  Each filter keeps the
+// reference's early exit (a position is gathered only while its bits so far are set), so the
+// gathers are the same ones test_filter issues, but step q's gathers of the G filters are
+// independent and in flight together instead of one filter's chain after another's.  `fl` bit
+// q-1 = the u64 sum h1 + q*h2 wrapped at step q (shared by every filter: it does not depend on m).
+template <int G>
+__device__ __forceinline__ uint32_t test_group7(const RegSlot *const *sl, uint32_t alive, uint64_t h1, uint64_t h2,
+                                                uint32_t fl) {
+    uint32_t r[G], nb[G], nd[G], m[G];
+    const uint32_t *wp[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const ModArg &md = sl[j]->md;
+        m[j] = (uint32_t)md.m;
+        const uint32_t c = (uint32_t)md.c;
+        r[j] = (uint32_t)mod64(h1, md.m, md.mu);
+        const uint32_t b = (uint32_t)mod64(h2, md.m, md.mu);
+        nb[j] = m[j] - b;
+        nd[j] = m[j] - (b >= c ? b - c : b + (m[j] - c));
+        wp[j] = sl[j]->words;
+    }
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        uint32_t w[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) w[j] = (alive >> j & 1u) ? wp[j][r[j] >> 5] : ~0u;
+#pragma unroll
+        for (int j = 0; j < G; ++j) alive &= ~((~(w[j] >> (r[j] & 31)) & 1u) << j);
+        if (q < 6) {
+            const bool cy = fl >> q & 1u;
+#pragma unroll
+            for (int j = 0; j < G; ++j) {  // r + (h2 mod m), less 2^64 mod m on a wrap, mod m
+                const uint32_t na = cy ? nd[j] : nb[j];
+                const uint32_t t = r[j] - na;
+                r[j] = r[j] >= na ? t : t + m[j];
+            }
+        }
+    }
+    return alive;
+}
+
 // One pass tests only the filters of slots [pass_lo, pass_hi) (lookup order).  With
 // multiget_pass_kib the host groups slots into passes of that many filter bytes, so the filters a
 // pass gathers from stay in each XCD's L2 (the phased probe's idea, seb_kernels.hip).  Every pass
@@ -65,8 +107,9 @@ __device__ __forceinline__ uint32_t test_filter(const RegSlot &sl, uint64_t h1, 
 // MODE 0: u64 mask, slot table in LDS.  MODE 1: candidate list, slot table in LDS.  MODE 2:
 // candidate list, slot table read from HBM/L2 (more than kMaxSlots files: an LSM past L1 holds
 // hundreds, lsm/levels.go:10-14 with ~4 MB files, lsm/compaction.go:253).  The list form always
-// runs as one pass.
-template <typename Src, int KFIX, bool M32, int MODE>
+// runs as one pass.  GRP > 0 (k = 7, m < 2^32 registries): the L0 filters in groups of GRP and
+// the level hits as one group go through test_group7; GRP = 0 tests one filter after another.
+template <typename Src, int KFIX, bool M32, int MODE, int GRP>
 __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const RegSlot *__restrict__ gslots,
                                                   uint32_t nslots, RegLayout lay, const uint8_t *__restrict__ ranges,
                                                   uint64_t *__restrict__ maybe, uint16_t *__restrict__ cand,
@@ -96,18 +139,48 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         uint64_t mask = 0;
         uint16_t *row = kList ? cand + i * (uint64_t)cap : nullptr;
         uint32_t nc = 0;
-        auto take = [&](const RegSlot &sl) {
-            if (test_filter<KFIX, M32>(sl, h1, h2)) {
-                if constexpr (kList) {
-                    if (nc < cap) row[nc++] = (uint16_t)sl.slot;  // the host checks cap >= the walk's length
-                } else {
-                    mask |= 1ull << sl.slot;
-                }
+        auto record = [&](const RegSlot &sl) {  // in Get's visiting order
+            if constexpr (kList) {
+                if (nc < cap) row[nc++] = (uint16_t)sl.slot;  // the host checks cap >= the walk's length
+            } else {
+                mask |= 1ull << sl.slot;
             }
         };
+        auto take = [&](const RegSlot &sl) {
+            if (test_filter<KFIX, M32>(sl, h1, h2)) record(sl);
+        };
+        uint32_t fl = 0;  // wrap flags of h1 + q*h2, q = 1..6 (grouped tests)
+        if constexpr (GRP > 0) {
+            uint64_t x = h1;
+#pragma unroll
+            for (uint32_t q = 1; q < 7; ++q) {
+                const uint64_t xn = x + h2;
+                fl |= (uint32_t)(xn < x) << (q - 1);
+                x = xn;
+            }
+        }
         const uint32_t s0 = lay.lo[0] > pass_lo ? lay.lo[0] : pass_lo;
         const uint32_t s1 = lay.hi[0] < pass_hi ? lay.hi[0] : pass_hi;
-        for (uint32_t s = s0; s < s1; ++s) take(slots[s]);  // every L0 file (of this pass)
+        if constexpr (GRP > 0) {
+            for (uint32_t s = s0; s < s1; s += GRP) {  // every L0 file (of this pass), GRP at a time
+                const RegSlot *grp[GRP];
+                uint32_t live = 0;
+#pragma unroll
+                for (int j = 0; j < GRP; ++j) {
+                    const bool in = s + j < s1;
+                    grp[j] = &slots[in ? s + j : s];
+                    live |= (uint32_t)in << j;
+                }
+                const uint32_t a = test_group7<GRP>(grp, live, h1, h2, fl);
+#pragma unroll
+                for (int j = 0; j < GRP; ++j)
+                    if (a >> j & 1u) record(*grp[j]);
+            }
+        } else {
+            for (uint32_t s = s0; s < s1; ++s) take(slots[s]);  // every L0 file (of this pass)
+        }
+        const RegSlot *lvl[4];
+        uint32_t lvl_live = 0;
         for (uint32_t L = 1; L < 5; ++L) {
             uint32_t lo = lay.lo[L], hi = lay.hi[L];
             if (lo == hi || hi <= pass_lo || lo >= pass_hi) continue;  // no file of this level in the pass
@@ -135,7 +208,24 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                         hit = (int)s;
                 }
             }
-            if (hit >= (int)pass_lo && hit < (int)pass_hi) take(slots[hit]);
+            if constexpr (GRP > 0) {
+                const bool in = hit >= (int)pass_lo && hit < (int)pass_hi;
+                lvl[L - 1] = &slots[in ? hit : 0];
+                lvl_live |= (uint32_t)in << (L - 1);
+            } else {
+                if (hit >= (int)pass_lo && hit < (int)pass_hi) take(slots[hit]);
+            }
+        }
+        if constexpr (GRP > 0) {
+            if (lvl_live) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (!(lvl_live >> j & 1u)) lvl[j] = lvl[__builtin_ctz(lvl_live)];
+                const uint32_t a = test_group7<4>(lvl, lvl_live, h1, h2, fl);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (a >> j & 1u) record(*lvl[j]);
+            }
         }
         if constexpr (kList) {
             for (uint32_t j = nc; j < cap; ++j) row[j] = 0xFFFFu;
@@ -168,14 +258,18 @@ hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t ns
                 hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe,
                                    cand, cap, lo, hi, acc);
             };
-            if (lay.all_k7_m32) {
-                if (mode == 0) go(k_multiget<S, 7, true, 0>);
-                else if (mode == 1) go(k_multiget<S, 7, true, 1>);
-                else go(k_multiget<S, 7, true, 2>);
+            if (lay.all_k7_m32 && options().multiget_group) {
+                if (mode == 0) go(k_multiget<S, 7, true, 0, 4>);
+                else if (mode == 1) go(k_multiget<S, 7, true, 1, 4>);
+                else go(k_multiget<S, 7, true, 2, 4>);
+            } else if (lay.all_k7_m32) {
+                if (mode == 0) go(k_multiget<S, 7, true, 0, 0>);
+                else if (mode == 1) go(k_multiget<S, 7, true, 1, 0>);
+                else go(k_multiget<S, 7, true, 2, 0>);
             } else {
-                if (mode == 0) go(k_multiget<S, 0, false, 0>);
-                else if (mode == 1) go(k_multiget<S, 0, false, 1>);
-                else go(k_multiget<S, 0, false, 2>);
+                if (mode == 0) go(k_multiget<S, 0, false, 0, 0>);
+                else if (mode == 1) go(k_multiget<S, 0, false, 1, 0>);
+                else go(k_multiget<S, 0, false, 2, 0>);
             }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;

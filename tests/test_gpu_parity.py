@@ -872,11 +872,14 @@ def _lsm_get_walk(files, key: bytes):
     return out
 
 
-@pytest.fixture(params=[0, 4096, 1], ids=["one-pass", "passes-4MiB", "pass-per-file"])
+@pytest.fixture(params=[(0, 1), (4096, 1), (1, 1), (0, 0), (4096, 0)],
+                ids=["one-pass", "passes-4MiB", "pass-per-file", "one-pass-serial", "passes-4MiB-serial"])
 def multiget_passes(request, seb):
-    """MultiGet split into passes of filter bytes (multiget_pass_kib): the masks never change."""
-    with seb.option("multiget_pass_kib", request.param):
-        yield request.param
+    """MultiGet split into passes of filter bytes (multiget_pass_kib), filters tested 4 at a time
+    or one by one (multiget_group): the masks never change."""
+    kib, group = request.param
+    with seb.option("multiget_pass_kib", kib), seb.option("multiget_group", group):
+        yield kib
 
 
 def test_registry_multiget_matches_lsm_get_walk(seb, torch_cuda, multiget_passes):
@@ -985,7 +988,13 @@ def _walk_rows(files, probes, cap):
     return want
 
 
-def test_registry_multiget_list_beyond_64_files(seb, torch_cuda):
+@pytest.fixture(params=[1, 0], ids=["grouped", "serial"])
+def multiget_group(request, seb):
+    with seb.option("multiget_group", request.param):
+        yield request.param
+
+
+def test_registry_multiget_list_beyond_64_files(seb, torch_cuda, multiget_group):
     """A registry past 64 files (an LSM with populated L1/L2: 400 MB / ~4 MB files,
     lsm/levels.go:10-14, lsm/compaction.go:253): the slot table is read from HBM instead of LDS
     and the answer is the list form, the slots Get would consult whose filter may contain the key
@@ -1058,7 +1067,7 @@ def test_registry_multiget_list_beyond_64_files(seb, torch_cuda):
     reg.close()
 
 
-def test_registry_full_capacity(seb, torch_cuda):
+def test_registry_full_capacity(seb, torch_cuda, multiget_group):
     """4096 files (the u16 slot-id capacity): one L0 file and 4095 one-key L1 files.  The
     4097th put is refused; the list form still answers every key as Get's walk does, and a key
     between two files' ranges visits only L0."""
