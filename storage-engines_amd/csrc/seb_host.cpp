@@ -113,6 +113,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "probe_phase0_kpt") && (value == 1 || value == 2 || value == 4)) o.probe_phase0_kpt = (int)value;
     else if (!strcmp(name, "multiget_pass_kib") && value >= 0 && value <= (1 << 22)) o.multiget_pass_kib = (int)value;
     else if (!strcmp(name, "multiget_group") && (value == 0 || value == 1)) o.multiget_group = (int)value;
+    else if (!strcmp(name, "multiget_order") && (value == 0 || value == 1)) o.multiget_order = (int)value;
     else if (!strcmp(name, "varlen_hash_keys") && (value == 256 || value == 512))
         o.varlen_hash_keys = (uint32_t)value;
     else if (!strcmp(name, "varlen_hash_win") && (value == 64 || value == 72 || value == 80))
@@ -137,7 +138,7 @@ static const char *const kOptionNames[] = {
     "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases", "probe_pack_first", "multi_phases", "many_splits",
     "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
     "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
-    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group"};
+    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order"};
 
 static std::once_flag g_env_once;
 static void load_env() {
@@ -183,6 +184,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "probe_phase0_kpt")) *value = o.probe_phase0_kpt;
     else if (!strcmp(name, "multiget_pass_kib")) *value = o.multiget_pass_kib;
     else if (!strcmp(name, "multiget_group")) *value = o.multiget_group;
+    else if (!strcmp(name, "multiget_order")) *value = o.multiget_order;
     else if (!strcmp(name, "varlen_hash_keys")) *value = o.varlen_hash_keys;
     else if (!strcmp(name, "varlen_hash_win")) *value = o.varlen_hash_win;
     else if (!strcmp(name, "varlen_prehash_packed")) *value = o.varlen_prehash_packed;
@@ -1179,6 +1181,7 @@ struct seb_registry {
     uint32_t nslots = 0;
     uint32_t max_cand = 0;         // longest Get walk: every L0 file + one file per non-empty level 1..4
     uint32_t max_slot = 0;         // 1 + the largest slot id in use (the mask form needs <= 64)
+    uint32_t part_lo = 0, part_hi = 0;  // multiget_order's partition level: lookup-ordered slots [lo, hi)
     RegLayout layout{};
     std::vector<uint32_t> passes;  // MultiGet pass bounds over the lookup-ordered slots
     int pass_kib = -1;             // multiget_pass_kib the bounds were computed for
@@ -1360,6 +1363,13 @@ static int sync_registry_locked(seb_registry *r) {
     for (int L = 1; L < 5; ++L) r->max_cand += lay.hi[L] > lay.lo[L] ? 1u : 0u;
     r->max_slot = 0;
     for (const RegEntry *e : order) r->max_slot = std::max(r->max_slot, e->slot + 1);
+    r->part_lo = r->part_hi = 0;  // the disjoint level with the most files orders MultiGet batches
+    for (int L = 1; L < 5; ++L)
+        if ((lay.nonoverlap >> L & 1u) && lay.hi[L] - lay.lo[L] >= 2 && lay.hi[L] - lay.lo[L] < kMgMaxBuckets &&
+            lay.hi[L] - lay.lo[L] > r->part_hi - r->part_lo) {
+            r->part_lo = lay.lo[L];
+            r->part_hi = lay.hi[L];
+        }
     std::vector<uint64_t> bytes;
     for (const RegEntry *e : order) bytes.push_back(seb_words_bytes(e->m));
     plan_passes(r, bytes);
@@ -1380,6 +1390,19 @@ extern "C" int seb_registry_slots(seb_registry *r, uint64_t *file_nums, int32_t 
             if (levels) levels[e.slot] = e.level;
         }
     return (int)r->entries.size();
+}
+
+// multiget_order: the batch's key-range order over the registry's partition level, in the
+// stream's scratch (tag 3); null when off, too small a batch or no disjoint level of >= 2 files.
+static int multiget_order(seb_registry *r, const KeyBatch &kb, hipStream_t s, uint32_t **order) {
+    *order = nullptr;
+    if (!options().multiget_order || r->part_hi <= r->part_lo || kb.n < 65536 || kb.n > 0xffffffffull) return SEB_OK;
+    void *ws = nullptr;
+    int rc = cached_workspace(s, multiget_order_bytes(kb.n), &ws, 3);
+    if (rc) return rc;
+    HIP_OR_FAIL(launch_multiget_order(kb, (const RegSlot *)r->dslots.p, r->part_lo, r->part_hi,
+                                      (const uint8_t *)r->dranges.p, ws, order, s));
+    return SEB_OK;
 }
 
 // Mask form (maybe != null) or list form (cand, cap u16 per key); called with r->mu held and the
@@ -1403,9 +1426,12 @@ static int registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t
     if ((rc = check_keys(keys, who))) return rc;
     std::lock_guard<std::mutex> g(r->mu);
     if ((rc = sync_registry_locked(r)) || (rc = check_multiget_out(r, maybe, cand, cap, keys->n, who))) return rc;
-    HIP_OR_FAIL(launch_multiget(key_batch(keys), (const RegSlot *)r->dslots.p, r->nslots, r->layout,
-                                (const uint8_t *)r->dranges.p, maybe, cand, cap, r->passes.data(),
-                                (uint32_t)r->passes.size() - 1, (hipStream_t)stream));
+    const KeyBatch kb = key_batch(keys);
+    uint32_t *order = nullptr;
+    if ((rc = multiget_order(r, kb, (hipStream_t)stream, &order))) return rc;
+    HIP_OR_FAIL(launch_multiget(kb, (const RegSlot *)r->dslots.p, r->nslots, r->layout, (const uint8_t *)r->dranges.p,
+                                maybe, cand, cap, r->passes.data(), (uint32_t)r->passes.size() - 1, (hipStream_t)stream,
+                                order));
     return SEB_OK;
 }
 
@@ -1429,10 +1455,12 @@ static int registry_multiget_host(seb_registry *r, const seb_keys *kb, uint64_t 
         if ((rc = stage_chunk(c, kb, chunks[j], b, &dk))) return rc;
         if ((rc = c->out[b].reserve(dk.n * per_key))) return rc;
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));
+        uint32_t *order = nullptr;
+        if ((rc = multiget_order(r, dk, c->s_comp, &order))) return rc;
         HIP_OR_FAIL(launch_multiget(dk, (const RegSlot *)r->dslots.p, r->nslots, r->layout,
                                     (const uint8_t *)r->dranges.p, maybe ? (uint64_t *)c->out[b].p : nullptr,
                                     maybe ? nullptr : (uint16_t *)c->out[b].p, cap, r->passes.data(),
-                                    (uint32_t)r->passes.size() - 1, c->s_comp));
+                                    (uint32_t)r->passes.size() - 1, c->s_comp, order));
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
         uint8_t *dst = maybe ? (uint8_t *)(maybe + chunks[j].i0) : (uint8_t *)(cand + chunks[j].i0 * cap);

@@ -72,14 +72,22 @@ hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mo
 // Passes: slots [pass_bounds[p], pass_bounds[p+1]) per launch (npasses == 0: one pass, all slots).
 // cand != null: the list form (cap u16 slots per key, one pass, any nslots) instead of masks.
 constexpr uint32_t kRegMaxFiles = 4096;  // registry capacity (u16 slot ids, 0xFFFF = none)
+// order != null: walk the keys in that order (answers still at each key's own index).
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
                            const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap,
-                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s);
+                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s, const uint32_t *order);
+// Key-range order for MultiGet: buckets = files of slots [lo, hi) (a disjoint, MinKey-ordered
+// level) with MinKey <= key.  *order_out stays null when the level does not apply.
+constexpr uint32_t kMgMaxBuckets = 1025;
+uint64_t multiget_order_bytes(uint64_t n);
+hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
+                                 const uint8_t *ranges, void *ws, uint32_t **order_out, hipStream_t s);
 
 // Process-wide tuning knobs (seb_set_option).
 struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed)
     int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
+    int multiget_order = 0;       // MultiGet: probe in key-range order (1; measured slower so far) or batch order (0)
     int multiget_group = 0;       // MultiGet (k = 7, m < 2^32): test filters 4 at a time (1; measured slower) or one by one (0)
     int multiget_pass_kib = 0;    // MultiGet: filter bytes per pass (0 = one pass; passes measured slower)
     uint64_t varlen_sort_min_keys = INT64_MAX;  // length-bucketed order (measured slower; off by default)

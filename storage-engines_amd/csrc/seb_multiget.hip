@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                                                   uint32_t nslots, RegLayout lay, const uint8_t *__restrict__ ranges,
                                                   uint64_t *__restrict__ maybe, uint16_t *__restrict__ cand,
                                                   uint32_t cap, uint32_t pass_lo, uint32_t pass_hi,
-                                                  uint32_t accumulate) {
+                                                  uint32_t accumulate, const uint32_t *__restrict__ order) {
     constexpr bool kLds = MODE < 2, kList = MODE > 0;
     __shared__ RegSlot lslots[kLds ? kMaxSlots : 1];
     if constexpr (kLds) {
@@ -123,7 +123,8 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
     }
     const RegSlot *slots = kLds ? lslots : gslots;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kb.n; i += stride) {
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < kb.n; j += stride) {
+        const uint64_t i = order ? (uint64_t)order[j] : j;  // key-range order (multiget_order) or batch order
         const uint8_t *key;
         uint32_t klen;
         if (kb.offsets) {
@@ -237,9 +238,125 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
     }
 }
 
+// ---- key-range order (multiget_order).  A batch probed in key order gathers from a few files of
+// each level at a time, so those filters stay in L2: a key-sorted 10M batch took 0.70 ms against
+// 1.47 ms in batch order (bench.py --lsm-order sorted).  Three small launches put the batch in
+// that order without sorting it: k_mg_bucket finds each key's bucket, the number of files of the
+// partition level (the disjoint level with the most files) whose MinKey <= key, which is
+// monotone in the key; k_mg_scan turns the bucket counts into cursors; k_mg_scatter writes the
+// key indices bucket by bucket (each tile reserves its runs with one atomic per bucket).
+// k_multiget then walks `order` and writes every answer at the key's own index, so the results
+// are those of the batch order.  Measured (gpurun_out/s3k, 28-file layout): bucket 239 us, scatter
+// 48 us, and k_multiget through `order` 1683 us against 1470 in batch order: its key loads and
+// answer stores become 64-B sector accesses per key, which costs more than the filter locality
+// saves.  Off by default; the next form materialises the keys in bucket order.
+constexpr uint32_t kMgTile = 4096;  // keys per k_mg_scatter tile (one cursor atomic per bucket per tile)
+
+__device__ __forceinline__ void key_at(const KeyBatch &kb, uint64_t i, const uint8_t *&key, uint32_t &klen) {
+    if (kb.offsets) {
+        key = kb.data + kb.offsets[i];
+        klen = (uint32_t)(kb.offsets[i + 1] - kb.offsets[i]);
+    } else {
+        key = kb.data + i * (uint64_t)kb.stride;
+        klen = kb.stride;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mg_bucket(KeyBatch kb, const RegSlot *__restrict__ slots, uint32_t lo,
+                                                   uint32_t hi, const uint8_t *__restrict__ ranges,
+                                                   uint16_t *__restrict__ bucket, uint32_t *__restrict__ counts) {
+    __shared__ uint32_t h[kMgMaxBuckets];
+    const uint32_t nb = hi - lo + 1;
+    for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x) h[t] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kb.n; i += stride) {
+        const uint8_t *key;
+        uint32_t klen;
+        key_at(kb, i, key, klen);
+        const uint64_t k0 = be64(key, klen), k1 = klen > 8 ? be64(key + 8, klen - 8) : 0ull;
+        uint32_t a = lo, b = hi;
+        while (a < b) {
+            const uint32_t mid = (a + b) >> 1;
+            const RegSlot &sl = slots[mid];
+            if (cmp_key(key, klen, k0, k1, sl.min_be, ranges + sl.min_off, sl.min_len) >= 0)
+                a = mid + 1;
+            else
+                b = mid;
+        }
+        bucket[i] = (uint16_t)(a - lo);
+        atomicAdd(&h[a - lo], 1u);
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x)
+        if (h[t]) atomicAdd(&counts[t], h[t]);
+}
+
+__global__ void k_mg_scan(uint32_t *counts, uint32_t nb) {  // exclusive scan in place, one thread (nb <= 1025)
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint32_t run = 0;
+    for (uint32_t t = 0; t < nb; ++t) {
+        const uint32_t c = counts[t];
+        counts[t] = run;
+        run += c;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *__restrict__ bucket,
+                                                    uint32_t *__restrict__ cursor, uint32_t nb,
+                                                    uint32_t *__restrict__ order) {
+    __shared__ uint32_t h[kMgMaxBuckets];
+    constexpr uint32_t kPer = kMgTile / 256;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kMgTile; t0 < n; t0 += (uint64_t)gridDim.x * kMgTile) {
+        for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x) h[t] = 0;
+        __syncthreads();
+        uint32_t bk[kPer], rk[kPer];
+#pragma unroll
+        for (uint32_t r = 0; r < kPer; ++r) {
+            const uint64_t i = t0 + (uint64_t)r * 256 + threadIdx.x;
+            bk[r] = i < n ? bucket[i] : 0u;
+            rk[r] = i < n ? atomicAdd(&h[bk[r]], 1u) : 0u;
+        }
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x)
+            if (h[t]) h[t] = atomicAdd(&cursor[t], h[t]);  // this tile's run of bucket t starts here
+        __syncthreads();
+#pragma unroll
+        for (uint32_t r = 0; r < kPer; ++r) {
+            const uint64_t i = t0 + (uint64_t)r * 256 + threadIdx.x;
+            if (i < n) order[h[bk[r]] + rk[r]] = (uint32_t)i;
+        }
+        __syncthreads();
+    }
+}
+
+uint64_t multiget_order_bytes(uint64_t n) { return ((n * 2 + 255) & ~255ull) + ((n * 4 + 255) & ~255ull) + 4 * kMgMaxBuckets; }
+
+hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
+                                 const uint8_t *ranges, void *ws, uint32_t **order_out, hipStream_t s) {
+    *order_out = nullptr;
+    const uint32_t nb = hi - lo + 1;
+    if (kb.n == 0 || nb > kMgMaxBuckets || nb < 2 || kb.n > 0xffffffffull) return hipSuccess;
+    uint16_t *bucket = (uint16_t *)ws;
+    uint32_t *order = (uint32_t *)((uint8_t *)ws + ((kb.n * 2 + 255) & ~255ull));
+    uint32_t *counts = (uint32_t *)((uint8_t *)order + ((kb.n * 4 + 255) & ~255ull));
+    hipError_t e = hipMemsetAsync(counts, 0, 4 * nb, s);
+    if (e != hipSuccess) return e;
+    uint64_t g = (kb.n + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_mg_bucket, dim3((unsigned)g), dim3(256), 0, s, kb, slots, lo, hi, ranges, bucket, counts);
+    hipLaunchKernelGGL(k_mg_scan, dim3(1), dim3(64), 0, s, counts, nb);
+    uint64_t gt = (kb.n + kMgTile - 1) / kMgTile;
+    if (gt > 2048) gt = 2048;
+    hipLaunchKernelGGL(k_mg_scatter, dim3((unsigned)gt), dim3(256), 0, s, kb.n, bucket, counts, nb, order);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    *order_out = order;
+    return hipSuccess;
+}
+
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
                            const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap,
-                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s) {
+                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s, const uint32_t *order) {
     if (kb.n == 0) return hipSuccess;
     if (!cand && nslots > kMaxSlots) return hipErrorInvalidValue;  // the mask form stages slots in LDS
     uint64_t g = (kb.n + 255) / 256;
@@ -256,7 +373,7 @@ hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t ns
             const uint32_t lo = pass_bounds[p], hi = pass_bounds[p + 1], acc = p > 0 ? 1u : 0u;
             auto go = [&](auto kern) {
                 hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe,
-                                   cand, cap, lo, hi, acc);
+                                   cand, cap, lo, hi, acc, order);
             };
             if (lay.all_k7_m32 && options().multiget_group) {
                 if (mode == 0) go(k_multiget<S, 7, true, 0, 4>);

@@ -1067,6 +1067,66 @@ def test_registry_multiget_list_beyond_64_files(seb, torch_cuda, multiget_group)
     reg.close()
 
 
+def test_registry_multiget_key_range_order(seb, torch_cuda):
+    """multiget_order: a batch of >= 64K keys is walked in key-range order over the registry's
+    disjoint level with the most files (bucket = files whose MinKey <= key).  Every answer must
+    equal the batch-order walk's, for masks and lists, host (variable-length) and device keys,
+    keys below the first file, between files and above the last; a model check on a sample."""
+    torch = torch_cuda
+    rng = np.random.default_rng(53)
+    reg = seb.Registry(0)
+    files = []
+    seq = 0
+
+    def add(file_num, level, keys):
+        nonlocal seq
+        m, k = oc.params(max(len(keys), 1), 0.01)
+        arr = np.frombuffer(b"".join(keys), np.uint8)
+        lens = np.array([len(x) for x in keys], np.uint64)
+        off = np.zeros(len(keys) + 1, np.uint64)
+        np.cumsum(lens, out=off[1:])
+        bits = oc.build(m, k, arr, len(keys), offsets=off)
+        slot = reg.put(file_num, level, bn.encode(bits, m, k), min(keys), max(keys))
+        files.append(dict(file=file_num, level=level, min=min(keys), max=max(keys), bits=bits, m=m, k=k, seq=seq,
+                          slot=slot))
+        seq += 1
+
+    universe = [kg.key16_bytes(int(i)) for i in range(1000, 61000, 2)]  # sorted: key16 sorts as i
+    for f in range(2):
+        add(100 + f, 0, sorted(rng.choice(universe, 3000, replace=False).tolist()))
+    chunks = np.array_split(np.array(universe, dtype=object), 40)
+    for j in rng.permutation(40):  # the partition level: 40 disjoint files, registered out of order
+        add(1000 + int(j), 1, [c for c in chunks[j]][::3])
+    for j in range(3):  # an overlapping level (linear first-cover scan)
+        add(2000 + j, 2, universe[j * 8000: j * 8000 + 14000:5])
+    n = 120_000
+    idx = rng.integers(0, 64000, n)
+    probes = [kg.key16_bytes(int(i)) for i in idx]
+    probes[:4] = [b"", b"a", b"user0000000000", b"zzzz"]
+    with seb.option("multiget_order", 0):
+        want_mask = reg.multiget(probes)
+        want_list = reg.multiget_list(probes)
+    with seb.option("multiget_order", 1):
+        got_mask = reg.multiget(probes)
+        got_list = reg.multiget_list(probes)
+    assert np.array_equal(got_mask, want_mask)
+    assert np.array_equal(got_list, want_list)
+    sample = list(range(0, n, 97)) + [0, 1, 2, 3]
+    assert np.array_equal(got_list[sample], _walk_rows(files, [probes[i] for i in sample], got_list.shape[1]))
+    fixed = np.frombuffer(b"".join(p for p in probes if len(p) == 16), np.uint8)
+    nf = fixed.size // 16
+    dk = seb.dev_keys(to_dev(torch, fixed), n=nf, stride=16)
+    outs = []
+    for order in (0, 1):
+        with seb.option("multiget_order", order):
+            out = torch.zeros(nf, dtype=torch.int64, device="cuda")
+            reg.multiget_dev(dk, out)
+            torch.cuda.synchronize()
+            outs.append(out.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    reg.close()
+
+
 def test_registry_full_capacity(seb, torch_cuda, multiget_group):
     """4096 files (the u16 slot-id capacity): one L0 file and 4095 one-key L1 files.  The
     4097th put is refused; the list form still answers every key as Get's walk does, and a key
