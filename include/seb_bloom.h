@@ -98,7 +98,7 @@ int seb_abi_version(void);
  *   "varlen_prehash_packed" LDS pre-hash writes packed residues (8 B/key) for k == 7, m < 2^29
  *   "build_prepack"     fixed-width bucketed build hashes to packed residues first (0 off, 1 on)
  *   "multiget_group"    registry MultiGet tests k=7 filters 4 at a time (1) or one by one (0, default)
- *   "multiget_order"    registry MultiGet walks the batch in key-range order (1) or batch order (0, default)
+ *   "multiget_order"    registry MultiGet walks batches of >= 64K keys in key-range order (1, default) or batch order (0)
  *                     filters, read directly by the bucketed build and the phased probe (0/1)
  * Environment variables SEB_<NAME> (upper case) set the initial values. */
 int seb_set_option(const char *name, int64_t value);

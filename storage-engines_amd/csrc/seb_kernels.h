@@ -87,7 +87,7 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
 struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed)
     int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
-    int multiget_order = 0;       // MultiGet: probe in key-range order (1; measured slower so far) or batch order (0)
+    int multiget_order = 1;       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
     int multiget_group = 0;       // MultiGet (k = 7, m < 2^32): test filters 4 at a time (1; measured slower) or one by one (0)
     int multiget_pass_kib = 0;    // MultiGet: filter bytes per pass (0 = one pass; passes measured slower)
     uint64_t varlen_sort_min_keys = INT64_MAX;  // length-bucketed order (measured slower; off by default)

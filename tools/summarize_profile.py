@@ -32,8 +32,8 @@ STEP_KERNELS = {  # per config: timed step name -> kernels launched by that step
     "c4": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned", "k_hash_varlen"),
            "probe": ("k_probe", "k_hash_varlen")},
     "c5": {"probe": ("k_probe_interleaved", "k_interleave", "k_probe_multi")},
-    "lsm": {"probe": ("k_multiget",)},
-    "lsm_wide": {"probe": ("k_multiget",)},
+    "lsm": {"probe": ("k_multiget", "k_mg_")},
+    "lsm_wide": {"probe": ("k_multiget", "k_mg_")},
     "route": {"route": ("k_route_tile", "k_route_scan_rows", "k_route_scatter")},
     "wal": {"wal_verify": ("k_wal_crc",)},
     "many": {"build_many": ("k_build_many",)},
