@@ -1394,14 +1394,20 @@ extern "C" int seb_registry_slots(seb_registry *r, uint64_t *file_nums, int32_t 
 
 // multiget_order: the batch's key-range order over the registry's partition level, in the
 // stream's scratch (tag 3); null when off, too small a batch or no disjoint level of >= 2 files.
-static int multiget_order(seb_registry *r, const KeyBatch &kb, hipStream_t s, uint32_t **order) {
+static int multiget_order(seb_registry *r, KeyBatch &kb, hipStream_t s, uint32_t **order, bool *order_keys) {
     *order = nullptr;
+    *order_keys = true;
     if (!options().multiget_order || r->part_hi <= r->part_lo || kb.n < 65536 || kb.n > 0xffffffffull) return SEB_OK;
     void *ws = nullptr;
     int rc = cached_workspace(s, multiget_order_bytes(kb.n), &ws, 3);
     if (rc) return rc;
+    const uint8_t *moved = nullptr;
     HIP_OR_FAIL(launch_multiget_order(kb, (const RegSlot *)r->dslots.p, r->part_lo, r->part_hi,
-                                      (const uint8_t *)r->dranges.p, ws, order, s));
+                                      (const uint8_t *)r->dranges.p, ws, order, &moved, s));
+    if (moved) {  // the MultiGet streams the moved keys; answers still land at each key's index
+        kb.data = moved;
+        *order_keys = false;
+    }
     return SEB_OK;
 }
 
@@ -1426,12 +1432,13 @@ static int registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t
     if ((rc = check_keys(keys, who))) return rc;
     std::lock_guard<std::mutex> g(r->mu);
     if ((rc = sync_registry_locked(r)) || (rc = check_multiget_out(r, maybe, cand, cap, keys->n, who))) return rc;
-    const KeyBatch kb = key_batch(keys);
+    KeyBatch kb = key_batch(keys);
     uint32_t *order = nullptr;
-    if ((rc = multiget_order(r, kb, (hipStream_t)stream, &order))) return rc;
+    bool order_keys = true;
+    if ((rc = multiget_order(r, kb, (hipStream_t)stream, &order, &order_keys))) return rc;
     HIP_OR_FAIL(launch_multiget(kb, (const RegSlot *)r->dslots.p, r->nslots, r->layout, (const uint8_t *)r->dranges.p,
                                 maybe, cand, cap, r->passes.data(), (uint32_t)r->passes.size() - 1, (hipStream_t)stream,
-                                order));
+                                order, order_keys));
     return SEB_OK;
 }
 
@@ -1456,11 +1463,12 @@ static int registry_multiget_host(seb_registry *r, const seb_keys *kb, uint64_t 
         if ((rc = c->out[b].reserve(dk.n * per_key))) return rc;
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));
         uint32_t *order = nullptr;
-        if ((rc = multiget_order(r, dk, c->s_comp, &order))) return rc;
+        bool order_keys = true;
+        if ((rc = multiget_order(r, dk, c->s_comp, &order, &order_keys))) return rc;
         HIP_OR_FAIL(launch_multiget(dk, (const RegSlot *)r->dslots.p, r->nslots, r->layout,
                                     (const uint8_t *)r->dranges.p, maybe ? (uint64_t *)c->out[b].p : nullptr,
                                     maybe ? nullptr : (uint16_t *)c->out[b].p, cap, r->passes.data(),
-                                    (uint32_t)r->passes.size() - 1, c->s_comp, order));
+                                    (uint32_t)r->passes.size() - 1, c->s_comp, order, order_keys));
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
         uint8_t *dst = maybe ? (uint8_t *)(maybe + chunks[j].i0) : (uint8_t *)(cand + chunks[j].i0 * cap);

@@ -72,16 +72,20 @@ hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mo
 // Passes: slots [pass_bounds[p], pass_bounds[p+1]) per launch (npasses == 0: one pass, all slots).
 // cand != null: the list form (cap u16 slots per key, one pass, any nslots) instead of masks.
 constexpr uint32_t kRegMaxFiles = 4096;  // registry capacity (u16 slot ids, 0xFFFF = none)
-// order != null: walk the keys in that order (answers still at each key's own index).
+// order != null: key j answers at index order[j]; order_keys: key j is read as key order[j] of kb
+// (else kb already holds the keys in that order).
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
                            const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap,
-                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s, const uint32_t *order);
+                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s, const uint32_t *order,
+                           bool order_keys);
 // Key-range order for MultiGet: buckets = files of slots [lo, hi) (a disjoint, MinKey-ordered
 // level) with MinKey <= key.  *order_out stays null when the level does not apply.
 constexpr uint32_t kMgMaxBuckets = 1025;
 uint64_t multiget_order_bytes(uint64_t n);
+// *keys_out: the 16-B keys moved into that order (aligned fixed 16-B batches), else null.
 hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
-                                 const uint8_t *ranges, void *ws, uint32_t **order_out, hipStream_t s);
+                                 const uint8_t *ranges, void *ws, uint32_t **order_out, const uint8_t **keys_out,
+                                 hipStream_t s);
 
 // Process-wide tuning knobs (seb_set_option).
 struct Options {

@@ -128,7 +128,8 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                                                   uint32_t nslots, RegLayout lay, const uint8_t *__restrict__ ranges,
                                                   uint64_t *__restrict__ maybe, uint16_t *__restrict__ cand,
                                                   uint32_t cap, uint32_t pass_lo, uint32_t pass_hi,
-                                                  uint32_t accumulate, const uint32_t *__restrict__ order) {
+                                                  uint32_t accumulate, const uint32_t *__restrict__ order,
+                                                  uint32_t order_keys) {
     constexpr bool kLds = MODE < 2, kList = MODE > 0;
     __shared__ RegSlot lslots[kLds ? kMaxSlots : 1];
     if constexpr (kLds) {
@@ -138,7 +139,10 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
     const RegSlot *slots = kLds ? lslots : gslots;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < kb.n; j += stride) {
-        const uint64_t i = order ? (uint64_t)order[j] : j;  // key-range order (multiget_order) or batch order
+        // key-range order (multiget_order): answer index oi = order[j]; the keys are read through the
+        // order too, or (order_keys == 0) were moved into that order by k_mg_scatter
+        const uint64_t oi = order ? (uint64_t)order[j] : j;
+        const uint64_t i = order_keys ? oi : j;
         const uint8_t *key;
         uint32_t klen;
         if (kb.offsets) {
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         uint64_t k0, k1;
         key_prefix(kb, key, klen, k0, k1);
         uint64_t mask = 0;
-        uint16_t *row = kList ? cand + i * (uint64_t)cap : nullptr;
+        uint16_t *row = kList ? cand + oi * (uint64_t)cap : nullptr;
         uint32_t nc = 0;
         auto record = [&](const RegSlot &sl) {  // in Get's visiting order
             if constexpr (kList) {
@@ -244,11 +248,11 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
             }
         }
         if constexpr (kList) {
-            for (uint32_t j = nc; j < cap; ++j) row[j] = 0xFFFFu;
+            for (uint32_t t = nc; t < cap; ++t) row[t] = 0xFFFFu;
         } else if (!accumulate) {
-            maybe[i] = mask;
+            maybe[oi] = mask;
         } else if (mask) {
-            maybe[i] |= mask;
+            maybe[oi] |= mask;
         }
     }
 }
@@ -320,7 +324,8 @@ __global__ void k_mg_scan(uint32_t *counts, uint32_t nb) {  // exclusive scan in
 
 __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *__restrict__ bucket,
                                                     uint32_t *__restrict__ cursor, uint32_t nb,
-                                                    uint32_t *__restrict__ order) {
+                                                    uint32_t *__restrict__ order, const uint4 *__restrict__ keys,
+                                                    uint4 *__restrict__ keys_out) {
     __shared__ uint32_t h[kMgMaxBuckets];
     constexpr uint32_t kPer = kMgTile / 256;
     for (uint64_t t0 = (uint64_t)blockIdx.x * kMgTile; t0 < n; t0 += (uint64_t)gridDim.x * kMgTile) {
@@ -340,22 +345,32 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *
 #pragma unroll
         for (uint32_t r = 0; r < kPer; ++r) {
             const uint64_t i = t0 + (uint64_t)r * 256 + threadIdx.x;
-            if (i < n) order[h[bk[r]] + rk[r]] = (uint32_t)i;
+            if (i < n) {
+                order[h[bk[r]] + rk[r]] = (uint32_t)i;
+                if (keys_out) keys_out[h[bk[r]] + rk[r]] = keys[i];  // 16-B keys move with their index
+            }
         }
         __syncthreads();
     }
 }
 
-uint64_t multiget_order_bytes(uint64_t n) { return ((n * 2 + 255) & ~255ull) + ((n * 4 + 255) & ~255ull) + 4 * kMgMaxBuckets; }
+uint64_t multiget_order_bytes(uint64_t n) {
+    return ((n * 2 + 255) & ~255ull) + ((n * 4 + 255) & ~255ull) + ((4 * kMgMaxBuckets + 255) & ~255ull) + n * 16;
+}
 
 hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
-                                 const uint8_t *ranges, void *ws, uint32_t **order_out, hipStream_t s) {
+                                 const uint8_t *ranges, void *ws, uint32_t **order_out, const uint8_t **keys_out,
+                                 hipStream_t s) {
     *order_out = nullptr;
+    *keys_out = nullptr;
     const uint32_t nb = hi - lo + 1;
     if (kb.n == 0 || nb > kMgMaxBuckets || nb < 2 || kb.n > 0xffffffffull) return hipSuccess;
     uint16_t *bucket = (uint16_t *)ws;
     uint32_t *order = (uint32_t *)((uint8_t *)ws + ((kb.n * 2 + 255) & ~255ull));
     uint32_t *counts = (uint32_t *)((uint8_t *)order + ((kb.n * 4 + 255) & ~255ull));
+    // aligned fixed 16-B keys are moved into bucket order as well (the MultiGet then streams them)
+    const bool move = !kb.offsets && !kb.hashes && kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0;
+    uint4 *sorted = move ? (uint4 *)((uint8_t *)counts + ((4 * kMgMaxBuckets + 255) & ~255ull)) : nullptr;
     hipError_t e = hipMemsetAsync(counts, 0, 4 * nb, s);
     if (e != hipSuccess) return e;
     uint64_t g = (kb.n + 255) / 256;
@@ -364,15 +379,18 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
     hipLaunchKernelGGL(k_mg_scan, dim3(1), dim3(64), 0, s, counts, nb);
     uint64_t gt = (kb.n + kMgTile - 1) / kMgTile;
     if (gt > 2048) gt = 2048;
-    hipLaunchKernelGGL(k_mg_scatter, dim3((unsigned)gt), dim3(256), 0, s, kb.n, bucket, counts, nb, order);
+    hipLaunchKernelGGL(k_mg_scatter, dim3((unsigned)gt), dim3(256), 0, s, kb.n, bucket, counts, nb, order,
+                       (const uint4 *)kb.data, sorted);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     *order_out = order;
+    *keys_out = (const uint8_t *)sorted;
     return hipSuccess;
 }
 
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
                            const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap,
-                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s, const uint32_t *order) {
+                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s, const uint32_t *order,
+                           bool order_keys) {
     if (kb.n == 0) return hipSuccess;
     if (!cand && nslots > kMaxSlots) return hipErrorInvalidValue;  // the mask form stages slots in LDS
     uint64_t g = (kb.n + 255) / 256;
@@ -389,7 +407,7 @@ hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t ns
             const uint32_t lo = pass_bounds[p], hi = pass_bounds[p + 1], acc = p > 0 ? 1u : 0u;
             auto go = [&](auto kern) {
                 hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe,
-                                   cand, cap, lo, hi, acc, order);
+                                   cand, cap, lo, hi, acc, order, (uint32_t)(order && order_keys));
             };
             if (lay.all_k7_m32 && options().multiget_group) {
                 if (mode == 0) go(k_multiget<S, 7, true, 0, 4>);
