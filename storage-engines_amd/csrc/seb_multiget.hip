@@ -285,8 +285,13 @@ __global__ __launch_bounds__(256) void k_mg_bucket(KeyBatch kb, const RegSlot *_
                                                    uint32_t hi, const uint8_t *__restrict__ ranges,
                                                    uint16_t *__restrict__ bucket, uint32_t *__restrict__ counts) {
     __shared__ uint32_t h[kMgMaxBuckets];
+    __shared__ uint64_t pmin[2 * (kMgMaxBuckets - 1)];  // the level's MinKey prefixes (16 B per file)
     const uint32_t nb = hi - lo + 1;
     for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x) h[t] = 0;
+    for (uint32_t t = threadIdx.x; t < nb - 1; t += blockDim.x) {
+        pmin[2 * t] = slots[lo + t].min_be[0];
+        pmin[2 * t + 1] = slots[lo + t].min_be[1];
+    }
     __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kb.n; i += stride) {
@@ -298,8 +303,17 @@ __global__ __launch_bounds__(256) void k_mg_bucket(KeyBatch kb, const RegSlot *_
         uint32_t a = lo, b = hi;
         while (a < b) {
             const uint32_t mid = (a + b) >> 1;
-            const RegSlot &sl = slots[mid];
-            if (cmp_key(key, klen, k0, k1, sl.min_be, ranges + sl.min_off, sl.min_len) >= 0)
+            const uint64_t p0 = pmin[2 * (mid - lo)], p1 = pmin[2 * (mid - lo) + 1];
+            int c;
+            if (k0 != p0) {
+                c = k0 < p0 ? -1 : 1;
+            } else if (k1 != p1) {
+                c = k1 < p1 ? -1 : 1;
+            } else {  // equal 16-byte prefixes: the full compare (tail bytes in HBM)
+                const RegSlot &sl = slots[mid];
+                c = cmp_key(key, klen, k0, k1, sl.min_be, ranges + sl.min_off, sl.min_len);
+            }
+            if (c >= 0)
                 a = mid + 1;
             else
                 b = mid;
