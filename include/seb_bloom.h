@@ -167,6 +167,14 @@ int seb_timer_record(void *event, void *stream);
 int seb_timer_elapsed_ms(void *start, void *end, float *ms);
 int seb_timer_destroy(void *event);
 
+/* Library-owned scratch.  Entry points that need scratch and take no workspace argument use
+ * grow-only buffers kept per (device, stream); a call holds its stream's buffers until it returns,
+ * so calls from several threads on one stream are safe (their launches do not interleave).
+ * seb_workspace_bytes: bytes currently held; seb_workspace_release: synchronise the streams that
+ * own scratch and free all of it (the next call re-allocates). */
+uint64_t seb_workspace_bytes(void);
+int seb_workspace_release(void);
+
 /* ------------------------------------------- host-buffer batched entry points ------------ */
 /* Keys and bits in host memory: H2D, kernels and D2H on the context's streams, synchronous.
  * A context owns a device, streams and grow-only scratch buffers; one context per thread
@@ -239,6 +247,13 @@ int seb_registry_max_candidates(seb_registry *reg); /* >= 0, or < 0 on error */
 int seb_registry_multiget_list(seb_registry *reg, const seb_keys *keys, uint16_t *cand, uint32_t cap); /* host */
 int seb_registry_multiget_list_dev(seb_registry *reg, const seb_keys *keys, uint16_t *cand, uint32_t cap,
                                    void *stream);
+/* The list form with file numbers instead of slots (host keys): files[i*cap + j] is the file_num of
+ * the j-th file Get would read for key i, padded with UINT64_MAX.  Sizing, lookup and slot->file
+ * mapping happen under one hold of the registry lock, so a concurrent put/remove (flush,
+ * compaction) cannot make rows overflow or a reused slot name the wrong file.  *need (nullable)
+ * receives the row width the registry needs now; cap < *need returns SEB_ERR_RANGE (retry). */
+int seb_registry_multiget_files(seb_registry *reg, const seb_keys *keys, uint64_t *files, uint32_t cap,
+                                uint32_t *need);
 
 /* ---------- hash-index shard routing + WAL record checksums (off the bloom path) ---- */
 /* shard[i] = FNV-1a32(key i) & ((1 << shard_bits) - 1), the reference's getShard

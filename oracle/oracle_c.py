@@ -16,7 +16,7 @@ u64p = C.POINTER(C.c_uint64)
 u32p = C.POINTER(C.c_uint32)
 
 
-def build() -> str:
+def build_library() -> str:
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
 
@@ -25,7 +25,7 @@ def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(_LIB_PATH):
-            build()
+            build_library()
         L = C.CDLL(_LIB_PATH)
         L.oracle_params.argtypes = [C.c_int64, C.c_double, u64p, u32p]
         L.oracle_params.restype = C.c_int

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -42,6 +43,20 @@ static int fail(int code, const char *fmt, ...) {
         hipError_t e_ = (expr);                                                                        \
         if (e_ != hipSuccess) return fail(SEB_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_));    \
     } while (0)
+
+// Makes `device` current for one call and restores the caller's device when it returns.
+struct DeviceGuard {
+    int saved = -1;
+    int set(int device) {
+        HIP_OR_FAIL(hipGetDevice(&saved));
+        if (saved != device) HIP_OR_FAIL(hipSetDevice(device));
+        return SEB_OK;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (saved >= 0 && hipGetDevice(&cur) == hipSuccess && cur != saved) (void)hipSetDevice(saved);
+    }
+};
 
 extern "C" const char *seb_last_error(void) { return t_err.c_str(); }
 extern "C" int seb_abi_version(void) { return SEB_ABI_VERSION; }
@@ -222,32 +237,64 @@ extern "C" int seb_dev_clear(uint32_t *words, uint64_t m, void *stream) {
     return SEB_OK;
 }
 
-// Workspace for the bucketed build: grow-only scratch owned by the library, one per
-// (device, stream) so concurrent streams never share it (stream order protects reuse).
-struct WsKey {
-    int device;
-    hipStream_t stream;
-    int tag;  // 0: build / key preparation scratch; 1: the phased probe's packed residues
-};
+// Library-owned scratch: grow-only buffers, one set per (device, stream), so concurrent streams
+// never share one.  Calls on ONE stream are ordered by the stream, but their enqueue phases can
+// overlap across host threads; so an ABI call holds its stream's slot (a recursive lock) from its
+// first workspace request until it returns (WsCall at the entry point).  A second thread's call
+// on the same stream therefore enqueues after the first call's launches, and a grow (stream sync
+// + free) can never free a buffer that another thread has been handed but not yet launched on.
 struct WsEntry {
-    WsKey key;
+    int tag;  // 0: build / key preparation; 1: packed residues; 3: MultiGet key-range order
     void *p;
     uint64_t bytes;
 };
-static std::mutex g_ws_mu;
-static std::vector<WsEntry> g_ws;
+struct WsSlot {
+    int device;
+    hipStream_t stream;
+    std::recursive_mutex mu;  // held by the call enqueueing against this slot's buffers
+    std::vector<WsEntry> bufs;
+};
+static std::mutex g_ws_mu;  // guards the slot list; each slot's buffers are guarded by slot->mu
+static std::vector<std::unique_ptr<WsSlot>> g_ws;
+static thread_local int t_ws_depth = 0;
+static thread_local std::vector<std::unique_lock<std::recursive_mutex>> t_ws_held;
+
+// Scope of one ABI call that may use library scratch: slots locked inside it stay locked until
+// the call returns (its last launch is enqueued by then).
+struct WsCall {
+    size_t mark;
+    WsCall() : mark(t_ws_held.size()) { ++t_ws_depth; }
+    ~WsCall() {
+        while (t_ws_held.size() > mark) t_ws_held.pop_back();
+        --t_ws_depth;
+    }
+    WsCall(const WsCall &) = delete;
+    WsCall &operator=(const WsCall &) = delete;
+};
+
+static WsSlot *ws_slot(int dev, hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    for (auto &sl : g_ws)
+        if (sl->device == dev && sl->stream == s) return sl.get();
+    g_ws.emplace_back(new WsSlot());
+    g_ws.back()->device = dev;
+    g_ws.back()->stream = s;
+    return g_ws.back().get();
+}
 
 static int cached_workspace(hipStream_t s, uint64_t bytes, void **out, int tag = 0) {
+    if (t_ws_depth == 0) return fail(SEB_ERR_INVALID, "internal: library scratch requested outside a WsCall scope");
     int dev = 0;
     HIP_OR_FAIL(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> g(g_ws_mu);
-    for (auto &e : g_ws)
-        if (e.key.device == dev && e.key.stream == s && e.key.tag == tag) {
+    WsSlot *sl = ws_slot(dev, s);
+    t_ws_held.emplace_back(sl->mu);  // released when the outermost WsCall of this thread returns
+    for (auto &e : sl->bufs)
+        if (e.tag == tag) {
             if (e.bytes >= bytes) {
                 *out = e.p;
                 return SEB_OK;
             }
-            HIP_OR_FAIL(hipStreamSynchronize(s));
+            HIP_OR_FAIL(hipStreamSynchronize(s));  // earlier launches on this stream may still read it
             HIP_OR_FAIL(hipFree(e.p));
             e.p = nullptr;
             e.bytes = 0;
@@ -260,9 +307,48 @@ static int cached_workspace(hipStream_t s, uint64_t bytes, void **out, int tag =
     void *p = nullptr;
     hipError_t a = hipMalloc(&p, bytes);
     if (a != hipSuccess) return fail(SEB_ERR_NOMEM, "workspace hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(a));
-    g_ws.push_back({{dev, s, tag}, p, bytes});
+    sl->bufs.push_back({tag, p, bytes});
     *out = p;
     return SEB_OK;
+}
+
+// Slots are never deleted, so the pointers stay valid after g_ws_mu is dropped (a call holding a
+// slot's lock may take g_ws_mu for another request, so the two are never held in that order here).
+static std::vector<WsSlot *> ws_slots_snapshot() {
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    std::vector<WsSlot *> v;
+    for (auto &sl : g_ws) v.push_back(sl.get());
+    return v;
+}
+
+extern "C" uint64_t seb_workspace_bytes(void) {
+    uint64_t total = 0;
+    for (WsSlot *sl : ws_slots_snapshot()) {
+        std::lock_guard<std::recursive_mutex> g(sl->mu);
+        for (auto &e : sl->bufs) total += e.bytes;
+    }
+    return total;
+}
+
+extern "C" int seb_workspace_release(void) {
+    int saved = 0;
+    HIP_OR_FAIL(hipGetDevice(&saved));
+    int rc = SEB_OK;
+    for (WsSlot *sl : ws_slots_snapshot()) {
+        std::lock_guard<std::recursive_mutex> g2(sl->mu);  // waits for a call still enqueueing on it
+        if (sl->bufs.empty()) continue;
+        hipError_t e = hipSetDevice(sl->device);
+        if (e == hipSuccess) e = hipStreamSynchronize(sl->stream);
+        for (auto &b : sl->bufs)
+            if (e == hipSuccess) e = hipFree(b.p);
+        if (e != hipSuccess) {
+            rc = fail(SEB_ERR_DEVICE, "seb_workspace_release: %s", hipGetErrorString(e));
+            break;
+        }
+        sl->bufs.clear();
+    }
+    (void)hipSetDevice(saved);
+    return rc;
 }
 
 static bool want_prehash(const KeyBatch &kb) {
@@ -403,6 +489,7 @@ extern "C" int seb_dev_build_ws(const seb_keys *keys, uint32_t *words, uint64_t 
 }
 
 extern "C" int seb_dev_build(const seb_keys *keys, uint32_t *words, uint64_t m, uint32_t k, void *stream) {
+    WsCall ws_call;
     std::call_once(g_env_once, load_env);
     int rc;
     if ((rc = check_keys(keys, "seb_dev_build")) || (rc = check_filter_args(m, k, "seb_dev_build"))) return rc;
@@ -414,6 +501,7 @@ extern "C" int seb_dev_build(const seb_keys *keys, uint32_t *words, uint64_t m, 
 
 extern "C" int seb_dev_probe(const seb_keys *keys, const uint32_t *words, uint64_t m, uint32_t k, uint8_t *out,
                              void *stream) {
+    WsCall ws_call;
     std::call_once(g_env_once, load_env);
     int rc;
     if ((rc = check_keys(keys, "seb_dev_probe")) || (rc = check_filter_args(m, k, "seb_dev_probe"))) return rc;
@@ -432,6 +520,7 @@ static int check_packed_args(uint64_t m, uint32_t k, const char *who) {
 }
 
 extern "C" int seb_dev_pack_residues(const seb_keys *keys, uint64_t m, uint32_t k, uint64_t *packed, void *stream) {
+    WsCall ws_call;
     std::call_once(g_env_once, load_env);
     int rc;
     if ((rc = check_keys(keys, "seb_dev_pack_residues")) || (rc = check_packed_args(m, k, "seb_dev_pack_residues")))
@@ -464,6 +553,7 @@ extern "C" int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const ui
 
 extern "C" int seb_dev_probe_emit_packed(const seb_keys *keys, const uint32_t *words, uint64_t m, uint32_t k,
                                          uint8_t *out, uint64_t *packed, void *stream) {
+    WsCall ws_call;
     std::call_once(g_env_once, load_env);
     int rc;
     if ((rc = check_keys(keys, "seb_dev_probe_emit_packed")) ||
@@ -506,6 +596,7 @@ static int fill_multi(const seb_filter_ref *filters, uint32_t nf, uint32_t mask_
 
 extern "C" int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *filters, uint32_t nf, void *mask,
                                    uint32_t mask_bytes, void *stream) {
+    WsCall ws_call;
     std::call_once(g_env_once, load_env);
     int rc;
     MultiArg ma;
@@ -533,6 +624,7 @@ extern "C" int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *f
 
 extern "C" int seb_dev_probe_multi_packed(const uint64_t *packed, uint64_t n, const seb_filter_ref *filters,
                                           uint32_t nf, void *mask, uint32_t mask_bytes, void *stream) {
+    WsCall ws_call;
     std::call_once(g_env_once, load_env);
     int rc;
     MultiArg ma;
@@ -867,6 +959,7 @@ extern "C" int seb_build(seb_ctx *c, const seb_keys *kb, uint8_t *bits, uint64_t
 }
 
 extern "C" int seb_probe(seb_ctx *c, const seb_keys *kb, const uint8_t *bits, uint64_t m, uint32_t k, uint8_t *out) {
+    WsCall ws_call;
     int rc;
     if (!c) return fail(SEB_ERR_INVALID, "seb_probe: null ctx");
     if ((rc = check_keys(kb, "seb_probe")) || (rc = check_filter_args(m, k, "seb_probe")) ||
@@ -1075,6 +1168,7 @@ extern "C" int seb_filter_add_batch(seb_filter *f, const seb_keys *kb) {
 }
 
 extern "C" int seb_filter_may_contain_batch(seb_filter *f, const seb_keys *kb, uint8_t *out) {
+    WsCall ws_call;
     if (!f) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: null filter");
     int rc;
     if ((rc = check_keys(kb, "BloomFilter.MayContain")) || (rc = validate_offsets(kb, "BloomFilter.MayContain")))
@@ -1399,7 +1493,11 @@ static int multiget_order(seb_registry *r, KeyBatch &kb, hipStream_t s, uint32_t
     *order_keys = true;
     if (!options().multiget_order || r->part_hi <= r->part_lo || kb.n < 65536 || kb.n > 0xffffffffull) return SEB_OK;
     void *ws = nullptr;
-    int rc = cached_workspace(s, multiget_order_bytes(kb.n), &ws, 3);
+    int rc = cached_workspace(s, multiget_order_bytes(kb), &ws, 3);
+    if (rc == SEB_ERR_NOMEM) {  // the order is only a speed-up: batch order needs no scratch
+        t_err.clear();
+        return SEB_OK;
+    }
     if (rc) return rc;
     const uint8_t *moved = nullptr;
     HIP_OR_FAIL(launch_multiget_order(kb, (const RegSlot *)r->dslots.p, r->part_lo, r->part_hi,
@@ -1430,6 +1528,9 @@ static int registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t
     int rc;
     if (!r) return fail(SEB_ERR_INVALID, "%s: null registry", who);
     if ((rc = check_keys(keys, who))) return rc;
+    DeviceGuard dg;  // the registry's tables, and so the stream and its scratch, are on r->device
+    if ((rc = dg.set(r->device))) return rc;
+    WsCall ws_call;
     std::lock_guard<std::mutex> g(r->mu);
     if ((rc = sync_registry_locked(r)) || (rc = check_multiget_out(r, maybe, cand, cap, keys->n, who))) return rc;
     KeyBatch kb = key_batch(keys);
@@ -1442,6 +1543,9 @@ static int registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t
     return SEB_OK;
 }
 
+static int registry_multiget_host_locked(seb_registry *r, const seb_keys *kb, uint64_t *maybe, uint16_t *cand,
+                                         uint32_t cap);
+
 static int registry_multiget_host(seb_registry *r, const seb_keys *kb, uint64_t *maybe, uint16_t *cand, uint32_t cap,
                                   const char *who) {
     int rc;
@@ -1449,6 +1553,14 @@ static int registry_multiget_host(seb_registry *r, const seb_keys *kb, uint64_t 
     if ((rc = check_keys(kb, who)) || (rc = validate_offsets(kb, who))) return rc;
     std::lock_guard<std::mutex> g(r->mu);
     if ((rc = sync_registry_locked(r)) || (rc = check_multiget_out(r, maybe, cand, cap, kb->n, who))) return rc;
+    return registry_multiget_host_locked(r, kb, maybe, cand, cap);
+}
+
+// Host keys through the registry's own context; r->mu held, registry synced, outputs checked.
+static int registry_multiget_host_locked(seb_registry *r, const seb_keys *kb, uint64_t *maybe, uint16_t *cand,
+                                         uint32_t cap) {
+    WsCall ws_call;
+    int rc;
     if (!r->ctx && (rc = seb_ctx_create(r->device, &r->ctx))) return rc;
     seb_ctx *c = r->ctx;
     std::lock_guard<std::mutex> g2(c->mu);
@@ -1499,6 +1611,32 @@ extern "C" int seb_registry_max_candidates(seb_registry *r) {
 extern "C" int seb_registry_multiget_list(seb_registry *r, const seb_keys *kb, uint16_t *cand, uint32_t cap) {
     if (!cand && kb && kb->n) return fail(SEB_ERR_INVALID, "seb_registry_multiget_list: null output");
     return registry_multiget_host(r, kb, nullptr, cand, cap, "seb_registry_multiget_list");
+}
+
+// The list form translated to file numbers under ONE hold of the registry lock, so a Put or
+// Remove between sizing the rows, running the lookup and mapping slots to files cannot make the
+// rows overflow or a freed-and-reused slot name the wrong file (the three-call sequence
+// max_candidates / multiget_list / slots is not atomic).
+extern "C" int seb_registry_multiget_files(seb_registry *r, const seb_keys *kb, uint64_t *files, uint32_t cap,
+                                           uint32_t *need) {
+    const char *who = "seb_registry_multiget_files";
+    int rc;
+    if (!r) return fail(SEB_ERR_INVALID, "%s: null registry", who);
+    if ((rc = check_keys(kb, who)) || (rc = validate_offsets(kb, who))) return rc;
+    if (!files && kb->n) return fail(SEB_ERR_INVALID, "%s: null output", who);
+    std::lock_guard<std::mutex> g(r->mu);
+    if ((rc = sync_registry_locked(r))) return rc;
+    const uint32_t want = std::max<uint32_t>(r->max_cand, 1);
+    if (need) *need = want;
+    if (cap < want)
+        return fail(SEB_ERR_RANGE, "%s: cap %u < %u candidates a key can have now; retry with *need", who, cap, want);
+    if (kb->n == 0) return SEB_OK;
+    std::vector<uint16_t> cand(kb->n * (uint64_t)cap);
+    if ((rc = registry_multiget_host_locked(r, kb, nullptr, cand.data(), cap))) return rc;
+    std::vector<uint64_t> by_slot(kRegMaxFiles, UINT64_MAX);
+    for (auto &e : r->entries) by_slot[e.slot] = e.file_num;
+    for (uint64_t i = 0; i < cand.size(); ++i) files[i] = cand[i] == 0xFFFF ? UINT64_MAX : by_slot[cand[i]];
+    return SEB_OK;
 }
 
 extern "C" int seb_registry_multiget_list_dev(seb_registry *r, const seb_keys *keys, uint16_t *cand, uint32_t cap,

@@ -81,8 +81,10 @@ hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t ns
 // Key-range order for MultiGet: buckets = files of slots [lo, hi) (a disjoint, MinKey-ordered
 // level) with MinKey <= key.  *order_out stays null when the level does not apply.
 constexpr uint32_t kMgMaxBuckets = 1025;
-uint64_t multiget_order_bytes(uint64_t n);
-// *keys_out: the 16-B keys moved into that order (aligned fixed 16-B batches), else null.
+// Aligned fixed 16-B batches are moved into that order with their index (16 B more per key).
+bool multiget_order_moves(const KeyBatch &kb);
+uint64_t multiget_order_bytes(const KeyBatch &kb);
+// *keys_out: the 16-B keys moved into that order (multiget_order_moves), else null.
 hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
                                  const uint8_t *ranges, void *ws, uint32_t **order_out, const uint8_t **keys_out,
                                  hipStream_t s);

@@ -368,8 +368,14 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *
     }
 }
 
-uint64_t multiget_order_bytes(uint64_t n) {
-    return ((n * 2 + 255) & ~255ull) + ((n * 4 + 255) & ~255ull) + ((4 * kMgMaxBuckets + 255) & ~255ull) + n * 16;
+bool multiget_order_moves(const KeyBatch &kb) {
+    return !kb.offsets && !kb.hashes && kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0;
+}
+
+uint64_t multiget_order_bytes(const KeyBatch &kb) {
+    const uint64_t n = kb.n;
+    return ((n * 2 + 255) & ~255ull) + ((n * 4 + 255) & ~255ull) + ((4 * kMgMaxBuckets + 255) & ~255ull) +
+           (multiget_order_moves(kb) ? n * 16 : 0);
 }
 
 hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
@@ -383,7 +389,7 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
     uint32_t *order = (uint32_t *)((uint8_t *)ws + ((kb.n * 2 + 255) & ~255ull));
     uint32_t *counts = (uint32_t *)((uint8_t *)order + ((kb.n * 4 + 255) & ~255ull));
     // aligned fixed 16-B keys are moved into bucket order as well (the MultiGet then streams them)
-    const bool move = !kb.offsets && !kb.hashes && kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0;
+    const bool move = multiget_order_moves(kb);
     uint4 *sorted = move ? (uint4 *)((uint8_t *)counts + ((4 * kMgMaxBuckets + 255) & ~255ull)) : nullptr;
     hipError_t e = hipMemsetAsync(counts, 0, 4 * nb, s);
     if (e != hipSuccess) return e;

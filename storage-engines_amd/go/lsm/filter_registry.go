@@ -17,12 +17,14 @@ import "C"
 
 import (
 	"runtime"
+	"sync/atomic"
 	"unsafe"
 )
 
 // FilterRegistry holds the bloom filters of the open SSTables in HBM (one per LSM instance).
 type FilterRegistry struct {
-	h *C.seb_registry
+	h       *C.seb_registry
+	capHint atomic.Uint32 // row width of the last Candidates call (the C side re-checks it)
 }
 
 func regPanic(op string) {
@@ -78,30 +80,38 @@ func (r *FilterRegistry) Candidates(keys []string) [][]uint64 {
 	data, offs := packKeys(keys)
 	ks := C.seb_keys{data: (*C.uint8_t)(unsafe.Pointer(&data[0])), offsets: (*C.uint64_t)(unsafe.Pointer(&offs[0])),
 		n: C.uint64_t(len(keys))}
-	capRow := int(C.seb_registry_max_candidates(r.h))
-	if capRow < 0 {
-		regPanic("Candidates")
-	}
+	// One C call sizes the rows, runs the lookup and maps slots to file numbers under the
+	// registry's lock, so a concurrent flush (Put) or compaction (Remove + Put reusing the slot)
+	// cannot overflow a row or make a slot name the wrong file.  SEB_ERR_RANGE: the registry
+	// grew since the last call; retry with the width it reports.
+	capRow := C.uint32_t(r.capHint.Load())
 	if capRow == 0 {
 		capRow = 1
 	}
-	cand := make([]uint16, len(keys)*capRow)
-	if C.seb_registry_multiget_list(r.h, &ks, (*C.uint16_t)(unsafe.Pointer(&cand[0])), C.uint32_t(capRow)) != 0 {
-		regPanic("Candidates")
+	var files []uint64
+	for {
+		files = make([]uint64, len(keys)*int(capRow))
+		var need C.uint32_t
+		rc := C.seb_registry_multiget_files(r.h, &ks, (*C.uint64_t)(unsafe.Pointer(&files[0])), capRow, &need)
+		if rc == C.int(C.SEB_ERR_RANGE) && need > capRow {
+			capRow = need
+			continue
+		}
+		if rc != 0 {
+			regPanic("Candidates")
+		}
+		r.capHint.Store(uint32(capRow))
+		break
 	}
 	runtime.KeepAlive(data)
 	runtime.KeepAlive(offs)
-	const maxFiles = 4096 // kRegMaxFiles
-	fileNums := make([]uint64, maxFiles)
-	if C.seb_registry_slots(r.h, (*C.uint64_t)(unsafe.Pointer(&fileNums[0])), nil, C.uint32_t(maxFiles)) < 0 {
-		regPanic("Candidates")
-	}
+	w := int(capRow)
 	for i := range keys {
-		for _, s := range cand[i*capRow : (i+1)*capRow] {
-			if s == 0xFFFF {
+		for _, f := range files[i*w : (i+1)*w] {
+			if f == ^uint64(0) {
 				break
 			}
-			out[i] = append(out[i], fileNums[s])
+			out[i] = append(out[i], f)
 		}
 	}
 	return out

@@ -102,6 +102,9 @@ _SIGS = {
     "seb_registry_max_candidates": (_i, [_vp]),
     "seb_registry_multiget_list": (_i, [_vp, C.POINTER(seb_keys), _vp, _u32]),
     "seb_registry_multiget_list_dev": (_i, [_vp, C.POINTER(seb_keys), _vp, _u32, _vp]),
+    "seb_registry_multiget_files": (_i, [_vp, C.POINTER(seb_keys), _vp, _u32, C.POINTER(_u32)]),
+    "seb_workspace_bytes": (_u64, []),
+    "seb_workspace_release": (_i, []),
     "seb_dev_shard_route": (_i, [C.POINTER(seb_keys), _u32, _vp, _vp, _vp]),
     "seb_dev_shard_partition_workspace_size": (_u64, [_u64, _u32]),
     "seb_dev_shard_partition": (_i, [C.POINTER(seb_keys), _u32, _vp, _vp, _vp, _vp, _u64, _vp]),
@@ -394,6 +397,21 @@ class Registry:
     def multiget_list_dev(self, keys: "seb_keys", out, cap: int, stream=None) -> None:
         check(lib().seb_registry_multiget_list_dev(self._h, C.byref(keys), out.data_ptr(), cap, _stream(stream)))
 
+    def multiget_files(self, keys, cap: int = 1) -> np.ndarray:
+        """Per key, the file numbers Get would read whose filter may contain it, in visiting order,
+        padded with 2^64-1: an (n, cap) u64 array from one atomic registry call (retried while the
+        registry grows between sizing and lookup)."""
+        kb = as_keys(keys)
+        need = _u32()
+        while True:
+            out = np.zeros((max(kb.n, 1), cap), dtype=np.uint64)
+            rc = lib().seb_registry_multiget_files(self._h, kb.ref, out.ctypes.data, cap, C.byref(need))
+            if rc == -4 and need.value > cap:
+                cap = need.value
+                continue
+            check(rc)
+            return out[: kb.n]
+
     def multiget(self, keys) -> np.ndarray:
         kb = as_keys(keys)
         out = np.zeros(max(kb.n, 1), dtype=np.uint64)
@@ -405,6 +423,16 @@ class Registry:
 
 
 # ------------------------------------------------- device-resident API (torch tensors) ----
+
+def workspace_bytes() -> int:
+    """Bytes of library-owned scratch (per device and stream) currently held."""
+    return int(lib().seb_workspace_bytes())
+
+
+def workspace_release() -> None:
+    """Synchronise the streams that own library scratch and free it."""
+    check(lib().seb_workspace_release())
+
 
 def _stream(stream=None) -> int:
     import torch

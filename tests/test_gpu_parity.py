@@ -1116,15 +1116,132 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
     fixed = np.frombuffer(b"".join(p for p in probes if len(p) == 16), np.uint8)
     nf = fixed.size // 16
     dk = seb.dev_keys(to_dev(torch, fixed), n=nf, stride=16)
-    outs = []
+    outs, lists = [], []
     for order in (0, 1):
         with seb.option("multiget_order", order):
             out = torch.zeros(nf, dtype=torch.int64, device="cuda")
             reg.multiget_dev(dk, out)
+            lst = torch.zeros((nf, want_list.shape[1]), dtype=torch.int16, device="cuda")
+            reg.multiget_list_dev(dk, lst, want_list.shape[1])  # list form with the keys moved
             torch.cuda.synchronize()
             outs.append(out.cpu().numpy())
+            lists.append(lst.cpu().numpy().view(np.uint16))
     assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(lists[0], lists[1])
+    fixed_rows = np.array([i for i, p in enumerate(probes) if len(p) == 16])
+    assert np.array_equal(lists[1], want_list[fixed_rows])
+    # host fixed 16-B chunks: staged into aligned device buffers, so the keys move as well
+    host16 = fixed.reshape(nf, 16)
+    with seb.option("multiget_order", 1):
+        assert np.array_equal(reg.multiget(host16), want_mask[fixed_rows])
+        assert np.array_equal(reg.multiget_list(host16), want_list[fixed_rows])
+        # file numbers from one atomic call equal the list form mapped through the slot table
+        files_got = reg.multiget_files(probes[:70000])
+    by_slot = {s: fn for s, (fn, _) in reg.slots().items()}
+    want_files = np.full((70000, files_got.shape[1]), np.iinfo(np.uint64).max, np.uint64)
+    for i, row in enumerate(want_list[:70000]):
+        for j, s in enumerate(row[row != 0xFFFF]):
+            want_files[i, j] = by_slot[int(s)]
+    assert files_got.shape[1] == reg.max_candidates()
+    assert np.array_equal(files_got, want_files)
     reg.close()
+
+
+def test_registry_key_range_order_long_min_keys(seb, torch_cuda):
+    """Key-range order over a partition level whose MinKeys are longer than 16 bytes and share
+    their first 16 bytes: the bucket pass must break the tie with the HBM tail compare.  Probes
+    share that 16-byte prefix and differ only after byte 16 (host variable-length keys, which
+    go through the index, and a device stride-22 batch, which is not moved)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(59)
+    reg = seb.Registry(0)
+    files = []
+    pre = b"tenant/0000042/x"  # 16 bytes shared by every key and every MinKey
+    assert len(pre) == 16
+    universe = [pre + b"%06d" % i for i in range(0, 90000, 3)]  # sorted
+
+    def add(file_num, level, keys, seq):
+        m, k = oc.params(len(keys), 0.01)
+        lens = np.array([len(x) for x in keys], np.uint64)
+        off = np.zeros(len(keys) + 1, np.uint64)
+        np.cumsum(lens, out=off[1:])
+        bits = oc.build(m, k, np.frombuffer(b"".join(keys), np.uint8), len(keys), offsets=off)
+        slot = reg.put(file_num, level, bn.encode(bits, m, k), min(keys), max(keys))
+        files.append(dict(file=file_num, level=level, min=min(keys), max=max(keys), bits=bits, m=m, k=k, seq=seq,
+                          slot=slot))
+
+    chunks = np.array_split(np.array(universe, dtype=object), 24)
+    for seq, j in enumerate(rng.permutation(24)):
+        add(500 + int(j), 1, list(chunks[j])[::2], seq)
+    add(900, 0, universe[::50], 99)
+    n = 70_000
+    idx = rng.integers(0, 92000, n)
+    probes = [pre + b"%06d" % int(i) for i in idx]
+    probes[:6] = [pre, pre[:15], pre + b"\x00", pre + b"000000", pre + b"999999", pre[:15] + b"y"]
+    with seb.option("multiget_order", 0):
+        want = reg.multiget_list(probes)
+    with seb.option("multiget_order", 1):
+        got = reg.multiget_list(probes)
+    assert np.array_equal(got, want)
+    sample = list(range(0, n, 131)) + list(range(6))
+    assert np.array_equal(got[sample], _walk_rows(files, [probes[i] for i in sample], got.shape[1]))
+    dev = np.frombuffer(b"".join(p for p in probes if len(p) == 22), np.uint8)
+    rows = np.array([i for i, p in enumerate(probes) if len(p) == 22])
+    dk = seb.dev_keys(to_dev(torch, dev), n=rows.size, stride=22)
+    for order in (0, 1):
+        with seb.option("multiget_order", order):
+            out = torch.zeros((rows.size, want.shape[1]), dtype=torch.int16, device="cuda")
+            reg.multiget_list_dev(dk, out, want.shape[1])
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint16), want[rows])
+    reg.close()
+
+
+def test_shared_stream_threads_and_workspace_release(seb, golden, torch_cuda):
+    """Library scratch is per (device, stream); two host threads calling on ONE stream must not
+    interleave launches on it or free it under each other (growing batch sizes force the grow
+    path).  seb_workspace_release frees it all; the next call re-allocates."""
+    import threading
+    torch = torch_cuda
+    m, k = seb.params(10_000_000, 0.01)  # a 12 MB filter: the phased probe keeps packed scratch
+    keys = kg.key16(np.arange(1_000_000)).reshape(-1)
+    words = seb.new_words(m)
+    dk_all = seb.dev_keys(to_dev(torch, keys), n=1_000_000, stride=16)
+    seb.dev_build(dk_all, words, m, k)
+    qn = [200_000, 1_000_000]
+    qkeys = [kg.key16(kg.probe_indices(1_000_000, count=q)).reshape(-1) for q in qn]
+    qdev = [to_dev(torch, q) for q in qkeys]
+    want = [oc.probe(oc.build(m, k, keys, 1_000_000, stride=16), m, k, q, q.size // 16, stride=16) for q in qkeys]
+    stream = torch.cuda.current_stream()
+    errors = []
+
+    def worker(t):
+        try:
+            dk = seb.dev_keys(qdev[t], n=qn[t], stride=16)
+            for it in range(12):
+                out = torch.zeros(qn[t], dtype=torch.uint8, device="cuda")
+                seb.dev_probe(dk, words, m, k, out, stream=stream)
+                stream.synchronize()
+                if not np.array_equal(out.cpu().numpy(), want[t]):
+                    errors.append((t, it))
+        except Exception as e:  # surfaced below
+            errors.append((t, repr(e)))
+
+    seb.workspace_release()
+    assert seb.workspace_bytes() == 0
+    th = [threading.Thread(target=worker, args=(t,)) for t in (0, 1, 0, 1)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    assert seb.workspace_bytes() > 0
+    seb.workspace_release()
+    assert seb.workspace_bytes() == 0
+    out = torch.zeros(qn[1], dtype=torch.uint8, device="cuda")
+    seb.dev_probe(seb.dev_keys(qdev[1], n=qn[1], stride=16), words, m, k, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), want[1])
 
 
 def test_registry_full_capacity(seb, torch_cuda, multiget_group):
