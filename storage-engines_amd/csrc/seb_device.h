@@ -230,9 +230,25 @@ __device__ __forceinline__ uint64_t mod64(uint64_t x, uint64_t m, uint64_t mu) {
     return r;
 }
 
+// x mod m for m < kM32Limit (2^31).  With mu = floor((2^64-1)/m) the Barrett quotient
+// q = floor(x*mu / 2^64) is at most one below floor(x/m) (mu*m > 2^64 - m), so r = x - q*m lies in
+// [0, 2m) and fits 32 bits: only q's low word is needed, and r = low32(x) - low32(q)*m exactly.
+// q's low word from three 32x32 products (the full 64x64 high product, low word kept), then
+// one conditional subtract as min(r, r - m): 9 VALU instructions instead of mod64's ~26.
+__device__ __forceinline__ uint32_t mod_m31(uint64_t x, uint32_t m, uint64_t mu) {
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const uint32_t ul = (uint32_t)mu, uh = (uint32_t)(mu >> 32);
+    const uint64_t a = (uint64_t)xh * ul + __umulhi(xl, ul);  // < 2^64
+    const uint64_t b = (uint64_t)xl * uh + (uint32_t)a;       // < 2^64
+    const uint32_t qlo = xh * uh + (uint32_t)(a >> 32) + (uint32_t)(b >> 32);
+    const uint32_t r = xl - qlo * m;
+    const uint32_t s = r - m;  // wraps past r exactly when r < m
+    return s < r ? s : r;
+}
+
 // Calls f(i, pos_i) for i < k with pos_i = (h1 + i*h2 mod 2^64) mod m, bit-exact with
 // lsm/bloom.go:64.  Residues advance incrementally: r_{i+1} = r_i + (h2 mod m), minus
-// (2^64 mod m) whenever the u64 sum h1 + (i+1)*h2 wraps.  M32: m < 2^32 -> u32 residues.
+// (2^64 mod m) whenever the u64 sum h1 + (i+1)*h2 wraps.  M32: m < kM32Limit -> u32 residues.
 template <int KFIX, bool M32, typename F>
 __device__ __forceinline__ void for_positions(uint64_t h1, uint64_t h2, const ModArg &md, uint32_t krt, F &&f) {
     const uint32_t k = KFIX > 0 ? (uint32_t)KFIX : krt;
@@ -240,11 +256,11 @@ __device__ __forceinline__ void for_positions(uint64_t h1, uint64_t h2, const Mo
     uint64_t x = h1;
     if constexpr (M32) {
         const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
-        uint32_t r = (uint32_t)mod64(h1, md.m, md.mu);
-        const uint32_t b = (uint32_t)mod64(h2, md.m, md.mu);
+        uint32_t r = mod_m31(h1, m, md.mu);
+        const uint32_t b = mod_m31(h2, m, md.mu);
         // Step addend: b, or (b - c) mod m when the u64 sum wraps.  Kept negated (m - a, in
         // [1, m]) so r + a mod m is one subtract, one compare and a conditional add of m, with
-        // no u32 overflow for any m < 2^32.
+        // no u32 overflow for any m < 2^31.
         const uint32_t nb = m - b;
         const uint32_t bc = b >= c ? b - c : b + (m - c);
         const uint32_t nd = m - bc;
@@ -297,7 +313,7 @@ static inline hipError_t with_src(const KeyBatch &kb, Fn &&fn) {
 // 58-63 bit q-1 = "the u64 sum h1 + q*h2 wrapped at step q" for q = 1..6.  The positions follow
 // for_positions' recurrence, so they are exactly (h1 + q*h2 mod 2^64) mod m of lsm/bloom.go:64.
 __device__ __forceinline__ uint64_t pack_residue(uint64_t h1, uint64_t h2, const ModArg &md) {
-    const uint64_t r0 = mod64(h1, md.m, md.mu), b = mod64(h2, md.m, md.mu);
+    const uint64_t r0 = mod_m31(h1, (uint32_t)md.m, md.mu), b = mod_m31(h2, (uint32_t)md.m, md.mu);
     uint64_t f = 0, x = h1;
 #pragma unroll
     for (uint32_t q = 1; q < 7; ++q) {

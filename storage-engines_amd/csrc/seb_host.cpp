@@ -1417,7 +1417,7 @@ static int sync_registry_locked(seb_registry *r) {
         const int L = order[i]->level;
         if (i == 0 || order[i - 1]->level != L) lay.lo[L] = (uint32_t)i;
         lay.hi[L] = (uint32_t)i + 1;
-        if (order[i]->k != 7 || order[i]->m > 0xffffffffull) lay.all_k7_m32 = 0;
+        if (order[i]->k != 7 || order[i]->m >= kM32Limit) lay.all_k7_m32 = 0;
     }
     for (int L = 0; L < 5; ++L)
         if (lay.hi[L] == 0) lay.lo[L] = lay.hi[L] = (uint32_t)order.size();  // empty level

@@ -13,6 +13,9 @@ struct ModArg {
     uint32_t k;   // numHashes
     uint32_t pad;
 };
+// Filters with m below this take the u32-residue kernels (template flag M32): the Barrett
+// quotient (mod_m31) is at most one low, so x - q*m < 2m fits in 32 bits.
+constexpr uint64_t kM32Limit = 1ull << 31;
 
 struct KeyBatch {  // device pointers
     const uint8_t *data;
@@ -60,7 +63,7 @@ struct RegSlot {
 struct RegLayout {          // slot index ranges per level (lookup order) + shape flags
     uint32_t lo[5], hi[5];
     uint32_t nonoverlap;    // bit L: level L's files are disjoint and in MinKey order (bisection exact)
-    uint32_t all_k7_m32;    // every filter has k == 7 and m < 2^32
+    uint32_t all_k7_m32;    // every filter has k == 7 and m < kM32Limit (2^31)
 };
 // seb_codec.hip: shard routing (FNV-1a32) and WAL CRC32
 hipError_t launch_route(const KeyBatch &kb, uint32_t bits, uint16_t *shard, uint32_t *hash, hipStream_t s);
@@ -94,7 +97,7 @@ struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed)
     int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
     int multiget_order = 1;       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
-    int multiget_group = 0;       // MultiGet (k = 7, m < 2^32): test filters 4 at a time (1; measured slower) or one by one (0)
+    int multiget_group = 0;       // MultiGet (k = 7, m < 2^31): test filters 4 at a time (1; measured slower) or one by one (0)
     int multiget_pass_kib = 0;    // MultiGet: filter bytes per pass (0 = one pass; passes measured slower)
     uint64_t varlen_sort_min_keys = INT64_MAX;  // length-bucketed order (measured slower; off by default)
     uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys
@@ -105,7 +108,7 @@ struct Options {
     int build_prepack = 0;            // fixed-width bucketed build: pack residues first (full-occupancy hash), 0/1
     int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)
     int probe_kpt = 2;            // k == 7 probes: keys per thread (1, 2, 4)
-    int probe_slice_shift = 19;   // k == 7, m < 2^32: sliced probe with 2^shift-word (2 MiB) slices (0 = off)
+    int probe_slice_shift = 19;   // k == 7, m < 2^31: sliced probe with 2^shift-word (2 MiB) slices (0 = off)
     unsigned probe_slice_grid = 0;  // workgroups of the sliced probe (0 = one thread per KPT keys)
     uint64_t bucket_min_keys = 1u << 18;  // auto: bucketed build from this many keys on
     int scatter_threads = 1024;
@@ -148,7 +151,7 @@ hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s);
 // The same pre-hash writing packed residues for filter md (k == 7, m < 2^kPackBits) instead.
 hipError_t launch_hash_varlen_packed(const KeyBatch &kb, const ModArg &md, uint64_t *packed, hipStream_t s);
 
-// Interleaved multi-filter probe (all filters share (m, k), k == 7, m < 2^32): scratch bytes
+// Interleaved multi-filter probe (all filters share (m, k), k == 7, m < 2^31): scratch bytes
 // needed for the per-call table (0 = not applicable), and the launch (table in `ws`).
 uint64_t interleaved_bytes(const MultiArg &ma, uint32_t mask_bytes);
 // packed != nullptr: phased (multi_phase_count > 1), with n * 8 bytes of packed-residue scratch.

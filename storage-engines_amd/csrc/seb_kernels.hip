@@ -10,7 +10,7 @@
 // reference's bit array.
 //
 // Integer-only work; no MFMA.  Per key: two FNV chains over the key bytes (VALU), two exact
-// 64-bit Barrett reductions, then k-1 incremental residue steps (u32 when m < 2^32), then k
+// 64-bit Barrett reductions, then k-1 incremental residue steps (u32 when m < 2^31), then k
 // random word touches (atomic OR for build, gather for probe).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void k_probe(Src src, uint64_t n, const uint32
     }
 }
 
-// Sliced probe (k == 7, m < 2^32): a filter larger than one XCD's 4 MiB L2 is probed in
+// Sliced probe (k == 7, m < 2^31): a filter larger than one XCD's 4 MiB L2 is probed in
 // phases.  Each thread keeps the 7 positions of its KPT keys in registers and, in phase s, gathers
 // only the words of slice s (2^slice_shift words).  Workgroups that progress at the same pace on
 // one XCD then share a single slice in that XCD's L2 instead of thrashing the whole filter; a
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, const
     }
 }
 
-// Compact sliced probe (MODE 7; k == 7, m < 2^32).  The sliced probe's L2 reuse grows with the
+// Compact sliced probe (MODE 7; k == 7, m < 2^31).  The sliced probe's L2 reuse grows with the
 // number of keys an XCD has in flight during one sweep over the slices, and holding 7 positions per
 // key in registers caps that (68 VGPRs at 2 keys per thread).  Here a key costs 4 registers: its
 // first residue r0, the two negated step addends (nb = m - b, nd = m - ((b - c) mod m)) and a word
@@ -253,8 +253,8 @@ __global__ __launch_bounds__(256) void k_probe_compact(Src src, uint64_t n, cons
             const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
             uint64_t h1 = 0, h2 = 0;
             if (i < n) src.hash(i, h1, h2);
-            r0[r] = (uint32_t)mod64(h1, md.m, md.mu);
-            const uint32_t b = (uint32_t)mod64(h2, md.m, md.mu);
+            r0[r] = mod_m31(h1, m, md.mu);
+            const uint32_t b = mod_m31(h2, m, md.mu);
             const uint32_t bc = b >= c ? b - c : b + (m - c);
             nb[r] = m - b;
             nd[r] = m - bc;
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(256) void k_probe_sliced_emit(Src src, uint64_t n, 
                     f |= (uint64_t)(xn < x) << (q - 1);
                     x = xn;
                 }
-                const uint64_t b = mod64(h2, md.m, md.mu);
+                const uint64_t b = mod_m31(h2, (uint32_t)md.m, md.mu);
                 __builtin_nontemporal_store((uint64_t)pos[r][0] | (b << kPackBits) | (f << (2 * kPackBits)),
                                             packed + src.index(i));
             }
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256) void k_probe_phase0(Src src, uint64_t n, const
                     f |= (uint64_t)(xn < x) << (q - 1);
                     x = xn;
                 }
-                const uint64_t b = mod64(h2, md.m, md.mu);
+                const uint64_t b = mod_m31(h2, (uint32_t)md.m, md.mu);
                 __builtin_nontemporal_store((uint64_t)pos[r][0] | (b << kPackBits) | (f << (2 * kPackBits)),
                                             packed + i);
             }
@@ -989,7 +989,7 @@ static hipError_t launch_probe7(const Src &src, uint64_t n, const uint32_t *word
 
 hipError_t launch_build(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s) {
     if (kb.n == 0 || md.k == 0) return hipSuccess;
-    const bool m32 = md.m <= 0xffffffffull;
+    const bool m32 = md.m < kM32Limit;
     const bool k7 = md.k == 7;
     return with_src(kb, [&](auto src) {
         using S = decltype(src);
@@ -1001,7 +1001,7 @@ hipError_t launch_build(const KeyBatch &kb, uint32_t *words, const ModArg &md, h
 hipError_t launch_probe(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s) {
     if (kb.n == 0) return hipSuccess;
     if (md.k == 0) return hipMemsetAsync(out, 1, kb.n, s);  // zero hashes: MayContain is true
-    const bool m32 = md.m <= 0xffffffffull;
+    const bool m32 = md.m < kM32Limit;
     const bool k7 = md.k == 7;
     return with_src(kb, [&](auto src) {
         using S = decltype(src);
@@ -1070,7 +1070,7 @@ uint64_t interleaved_bytes(const MultiArg &ma, uint32_t mask_bytes) {
     if (ma.nf < 2) return 0;
     for (uint32_t f = 1; f < ma.nf; ++f)
         if (ma.f[f].md.m != ma.f[0].md.m || ma.f[f].md.k != ma.f[0].md.k) return 0;
-    if (ma.f[0].md.k != 7 || ma.f[0].md.m > 0xffffffffull) return 0;
+    if (ma.f[0].md.k != 7 || ma.f[0].md.m >= kM32Limit) return 0;
     return ((ma.f[0].md.m + 31) / 32) * 32 * mask_bytes;
 }
 
@@ -1090,7 +1090,7 @@ static hipError_t multi_mask(const KeyBatch &kb, const MultiArg &ma, void *mask,
     bool same = true, m32 = true;
     for (uint32_t f = 0; f < ma.nf; ++f) {
         same &= ma.f[f].md.m == ma.f[0].md.m && ma.f[f].md.k == ma.f[0].md.k;
-        m32 &= ma.f[f].md.m <= 0xffffffffull;
+        m32 &= ma.f[f].md.m < kM32Limit;
     }
     const bool k7same = same && ma.f[0].md.k == 7;
     return with_src(kb, [&](auto src) {
@@ -1119,7 +1119,7 @@ hipError_t launch_build_many_lds(const KeyBatch &kb, const ManyArg &ma, uint32_t
     if (ma.nf == 0) return hipSuccess;
     bool m32 = true, k7 = true;
     for (uint32_t f = 0; f < ma.nf; ++f) {
-        m32 &= ma.f[f].md.m <= 0xffffffffull;
+        m32 &= ma.f[f].md.m < kM32Limit;
         k7 &= ma.f[f].md.k == 7;
     }
     return with_src(kb, [&](auto src) {

@@ -69,7 +69,7 @@ __device__ __forceinline__ uint32_t test_filter(const RegSlot &sl, uint64_t h1, 
     return acc & 1u;
 }
 
-// MayContain of up to G filters side by side (k = 7, m < 2^32), bit j of `alive` = filter j
+// MayContain of up to G filters side by side (k = 7, m < 2^31), bit j of `alive` = filter j
 // still to be tested; returns the filters whose 7 bits are all set.  Each filter keeps the
 // reference's early exit (a position is gathered only while its bits so far are set), so the
 // gathers are the same ones test_filter issues, but step q's gathers of the G filters are
@@ -85,8 +85,8 @@ __device__ __forceinline__ uint32_t test_group7(const RegSlot *const *sl, uint32
         const ModArg &md = sl[j]->md;
         m[j] = (uint32_t)md.m;
         const uint32_t c = (uint32_t)md.c;
-        r[j] = (uint32_t)mod64(h1, md.m, md.mu);
-        const uint32_t b = (uint32_t)mod64(h2, md.m, md.mu);
+        r[j] = mod_m31(h1, m[j], md.mu);
+        const uint32_t b = mod_m31(h2, m[j], md.mu);
         nb[j] = m[j] - b;
         nd[j] = m[j] - (b >= c ? b - c : b + (m[j] - c));
         wp[j] = sl[j]->words;
@@ -121,7 +121,7 @@ __device__ __forceinline__ uint32_t test_group7(const RegSlot *const *sl, uint32
 // MODE 0: u64 mask, slot table in LDS.  MODE 1: candidate list, slot table in LDS.  MODE 2:
 // candidate list, slot table read from HBM/L2 (more than kMaxSlots files: an LSM past L1 holds
 // hundreds, lsm/levels.go:10-14 with ~4 MB files, lsm/compaction.go:253).  The list form always
-// runs as one pass.  GRP > 0 (k = 7, m < 2^32 registries): the L0 filters in groups of GRP and
+// runs as one pass.  GRP > 0 (k = 7, m < 2^31 registries): the L0 filters in groups of GRP and
 // the level hits as one group go through test_group7; GRP = 0 tests one filter after another.
 template <typename Src, int KFIX, bool M32, int MODE, int GRP>
 __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const RegSlot *__restrict__ gslots,

@@ -538,10 +538,12 @@ def test_fixed_strides_and_alignment(seb, torch_cuda, stride, build_algo):
 
 
 @pytest.mark.parametrize("algo", [1, 2])
-@pytest.mark.parametrize("m,k", [(1, 1), (1, 7), (2, 3), (31, 7), (32, 7), (33, 7), (4096, 30),
-                                 (2**31 - 1, 7), (2**32 - 5, 7), (2**32 + 977, 7), (3 * 2**32 + 12345, 9)])
+@pytest.mark.parametrize("m,k", [(1, 1), (1, 7), (2, 3), (31, 7), (32, 7), (33, 7), (4096, 30), (1 << 30, 7),
+                                 (3 * 2**29 + 1, 7), (2**31 - 2, 5), (2**31 - 1, 7), (2**31, 7), (2**31 + 1, 7),
+                                 (2**32 - 5, 7), (2**32 + 977, 7), (3 * 2**32 + 12345, 9)])
 def test_modulus_edge_cases(seb, torch_cuda, m, k, algo):
-    """u32 and u64 residue paths, m near 2^32, runtime k != 7 (lsm/bloom.go:64 wraparound).
+    """u32 residue path (m < 2^31, mod_m31) and u64 path, m at and around 2^31 and 2^32, runtime
+    k != 7 (lsm/bloom.go:64 wraparound).
     algo 2 runs the radix-partitioned build where it applies (m <= 2^28), atomics elsewhere."""
     torch = torch_cuda
     seb.set_option("build_algo", algo)
