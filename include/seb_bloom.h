@@ -83,12 +83,6 @@ int seb_abi_version(void);
  *   "probe_phase0_pct", "probe_phase0_kpt"  phased probe: range 0's share of the filter (0 = even),
  *                     keys per thread in phase 0 (1, 2, 4)
  *   "probe_pack_first" phased probe: a streaming pack pass, then every range from packed words (0/1)
- *   "probe_compact"   phased probe, ranges after the first: each position step's gathers compacted
- *                     across the wave, 4 or 8 keys per thread (0 = off)
- *   "probe_eager"     phased probe, ranges after the first: load the packed words together with the
- *                     answer bytes (0/1)
- *   "probe_pf_grid"   phased probe, ranges after the first: grid-stride kernel of this many workgroups
- *                     that prefetches its next iteration's answers and packed words (0 = off)
  *   "probe_persistent" sliced probe: persistent 1024-thread workgroups (0 = off)
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
  *   "multi_phases"    interleaved multi-filter probe: 1 = in-kernel slices (default), 0 = one launch

@@ -122,9 +122,6 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "probe_mode") && value >= 0 && value <= 8) o.probe_mode = (int)value;
     else if (!strcmp(name, "probe_phases") && value >= 0 && value <= 64) o.probe_phases = (int)value;
     else if (!strcmp(name, "probe_pack_first") && (value == 0 || value == 1)) o.probe_pack_first = (int)value;
-    else if (!strcmp(name, "probe_compact") && (value == 0 || value == 4 || value == 8)) o.probe_compact = (int)value;
-    else if (!strcmp(name, "probe_eager") && (value == 0 || value == 1)) o.probe_eager = (int)value;
-    else if (!strcmp(name, "probe_pf_grid") && value >= 0 && value <= (1 << 20)) o.probe_pf_grid = (int)value;
     else if (!strcmp(name, "multi_phases") && value >= 0 && value <= 64) o.multi_phases = (int)value;
     else if (!strcmp(name, "many_splits") && value >= 0 && value <= 64) o.many_splits = (uint32_t)value;
     else if (!strcmp(name, "probe_phase0_pct") && value >= 0 && value <= 90) o.probe_phase0_pct = (int)value;
@@ -156,8 +153,7 @@ static const char *const kOptionNames[] = {
     "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases", "probe_pack_first", "multi_phases", "many_splits",
     "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
     "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
-    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order",
-    "probe_compact", "probe_eager", "probe_pf_grid"};
+    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order"};
 
 static std::once_flag g_env_once;
 static void load_env() {
@@ -197,9 +193,6 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "probe_mode")) *value = o.probe_mode;
     else if (!strcmp(name, "probe_phases")) *value = o.probe_phases;
     else if (!strcmp(name, "probe_pack_first")) *value = o.probe_pack_first;
-    else if (!strcmp(name, "probe_compact")) *value = o.probe_compact;
-    else if (!strcmp(name, "probe_eager")) *value = o.probe_eager;
-    else if (!strcmp(name, "probe_pf_grid")) *value = o.probe_pf_grid;
     else if (!strcmp(name, "multi_phases")) *value = o.multi_phases;
     else if (!strcmp(name, "many_splits")) *value = o.many_splits;
     else if (!strcmp(name, "probe_phase0_pct")) *value = o.probe_phase0_pct;

@@ -122,9 +122,6 @@ struct Options {
     int multi_phases = 1;         // phased interleaved multi-filter probe: ranges (1 = off, the default: measured slower
                                   // on C5; 0 = one per 4 MiB of table; n > 1 = n ranges)
     int probe_pack_first = 0;     // phased probe: pack residues in a streaming pass instead of in phase 0
-    int probe_pf_grid = 0;        // phased probe, ranges 1..: grid-stride kernel of this many workgroups prefetching the next iteration (0 = off)
-    int probe_eager = 0;          // phased probe, ranges 1..: load packed words with the answers, not after them
-    int probe_compact = 0;        // phased probe, ranges 1..: gathers compacted across the wave, 4 or 8 keys per thread (0 = off)
     int probe_phases = 0;         // phased probe: number of phases (0 = one per 4 MiB of filter)
     int probe_mode = 8;           // k == 7 probe: 8 = phased (one launch per filter range, default); 0-6 k_probe_sliced MODE, 7 k_probe_compact
     unsigned grid_cap = 1u << 20;

@@ -422,9 +422,7 @@ __global__ __launch_bounds__(256) void k_probe_phase0(Src src, uint64_t n, const
 // Phase p > 0 over words [lo, hi): thread t owns keys 4t..4t+3 (one u32 of answers, two 16-B
 // loads of packed words); `out` is 4-byte aligned (the host checks).  PMAJOR: walk the 7
 // positions of the 4 keys position-major (4 independent gathers per step) instead of key by key.
-// EAGER: load the packed words together with the answer bytes instead of after them (one memory
-// round trip per iteration instead of two; the packed words of an all-dead group are read anyway).
-template <bool PMAJOR, bool EAGER>
+template <bool PMAJOR>
 __global__ __launch_bounds__(256) void k_probe_phase(const uint64_t *__restrict__ packed, uint64_t n,
                                                      const uint32_t *__restrict__ words, ModArg md,
                                                      uint8_t *__restrict__ out, uint32_t lo, uint32_t hi,
@@ -434,22 +432,6 @@ __global__ __launch_bounds__(256) void k_probe_phase(const uint64_t *__restrict_
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
     for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < n; i0 += stride) {
         const bool full = i0 + 4 <= n;
-        uint64_t pv[4];
-        auto load_packed = [&]() {
-            if (full) {
-                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 p0 = __builtin_nontemporal_load((const u32x4 *)(packed + i0));
-                const u32x4 p1 = __builtin_nontemporal_load((const u32x4 *)(packed + i0 + 2));
-                pv[0] = (uint64_t)p0.x | ((uint64_t)p0.y << 32);
-                pv[1] = (uint64_t)p0.z | ((uint64_t)p0.w << 32);
-                pv[2] = (uint64_t)p1.x | ((uint64_t)p1.y << 32);
-                pv[3] = (uint64_t)p1.z | ((uint64_t)p1.w << 32);
-            } else {
-#pragma unroll
-                for (uint32_t r = 0; r < 4; ++r) pv[r] = i0 + r < n ? packed[i0 + r] : 0ull;
-            }
-        };
-        if (EAGER) load_packed();
         uint32_t a;
         if (first) {  // a batch probed from packed words alone: every key starts alive
             a = full ? 0x01010101u : 0x01010101u & ((1u << (8 * (uint32_t)(n - i0))) - 1u);
@@ -460,7 +442,19 @@ __global__ __launch_bounds__(256) void k_probe_phase(const uint64_t *__restrict_
             for (uint32_t r = 0; i0 + r < n; ++r) a |= (uint32_t)out[i0 + r] << (8 * r);
         }
         if (a == 0u) continue;
-        if (!EAGER) load_packed();
+        uint64_t pv[4];
+        if (full) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 p0 = __builtin_nontemporal_load((const u32x4 *)(packed + i0));
+            const u32x4 p1 = __builtin_nontemporal_load((const u32x4 *)(packed + i0 + 2));
+            pv[0] = (uint64_t)p0.x | ((uint64_t)p0.y << 32);
+            pv[1] = (uint64_t)p0.z | ((uint64_t)p0.w << 32);
+            pv[2] = (uint64_t)p1.x | ((uint64_t)p1.y << 32);
+            pv[3] = (uint64_t)p1.z | ((uint64_t)p1.w << 32);
+        } else {
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) pv[r] = i0 + r < n ? packed[i0 + r] : 0ull;
+        }
         uint32_t na = a;
         if constexpr (PMAJOR) {
             uint32_t live[4], x[4], nb[4], nd[4], f[4];
@@ -517,192 +511,6 @@ __global__ __launch_bounds__(256) void k_probe_phase(const uint64_t *__restrict_
                 *(uint32_t *)(out + i0) = na;
             else
                 for (uint32_t r = 0; i0 + r < n; ++r) out[i0 + r] = (uint8_t)(na >> (8 * r));
-        }
-    }
-}
-
-// Phase p > 0 as a grid-stride loop (probe_pf_grid workgroups) that loads the next iteration's
-// answer bytes and packed words before it walks this iteration's gathers, so the stream's memory
-// latency overlaps the gather chain instead of adding to it.  Keys, gathers and answers as in
-// k_probe_phase<false>.
-__global__ __launch_bounds__(256) void k_probe_phase_pf(const uint64_t *__restrict__ packed, uint64_t n,
-                                                        const uint32_t *__restrict__ words, ModArg md,
-                                                        uint8_t *__restrict__ out, uint32_t lo, uint32_t hi,
-                                                        uint32_t first) {
-    const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
-    constexpr uint64_t kMask = (1ull << kPackBits) - 1;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    auto fetch = [&](uint64_t i, uint32_t &a, uint64_t pv[4]) {
-        if (i + 4 <= n) {
-            a = first ? 0x01010101u : *(const uint32_t *)(out + i);
-            const u32x4 p0 = __builtin_nontemporal_load((const u32x4 *)(packed + i));
-            const u32x4 p1 = __builtin_nontemporal_load((const u32x4 *)(packed + i + 2));
-            pv[0] = (uint64_t)p0.x | ((uint64_t)p0.y << 32);
-            pv[1] = (uint64_t)p0.z | ((uint64_t)p0.w << 32);
-            pv[2] = (uint64_t)p1.x | ((uint64_t)p1.y << 32);
-            pv[3] = (uint64_t)p1.z | ((uint64_t)p1.w << 32);
-        } else {
-            a = 0;
-#pragma unroll
-            for (uint32_t r = 0; r < 4; ++r) {
-                const bool in = i + r < n;
-                a |= (uint32_t)(in ? (first ? 1u : (uint32_t)out[i + r]) : 0u) << (8 * r);
-                pv[r] = in ? packed[i + r] : 0ull;
-            }
-        }
-    };
-    uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    uint32_t an = 0;
-    uint64_t pn[4] = {0, 0, 0, 0};
-    if (i0 < n) fetch(i0, an, pn);
-    for (; i0 < n; i0 += stride) {
-        const uint32_t a = an;
-        uint64_t pv[4] = {pn[0], pn[1], pn[2], pn[3]};
-        if (i0 + stride < n) fetch(i0 + stride, an, pn);
-        if (a == 0u) continue;
-        uint32_t na = a;
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) {
-            uint32_t live = (a >> (8 * r)) & 1u;
-            uint32_t x = (uint32_t)(pv[r] & kMask);
-            const uint32_t b = (uint32_t)((pv[r] >> kPackBits) & kMask), f = (uint32_t)(pv[r] >> (2 * kPackBits));
-            const uint32_t nb = m - b, bc = b >= c ? b - c : b + (m - c), nd = m - bc;
-#pragma unroll
-            for (int q = 0; q < 7; ++q) {
-                if (q > 0) {
-                    const uint32_t d = (f >> (q - 1)) & 1u ? nd : nb;
-                    const uint32_t t = x - d;
-                    x = x >= d ? t : t + m;
-                }
-                const uint32_t w = x >> 5;
-                if (live && w >= lo && w < hi) live &= words[w] >> (x & 31);
-            }
-            na &= ~((((a >> (8 * r)) & 1u) & (live ^ 1u)) << (8 * r));
-        }
-        if (na != a || first) {
-            if (i0 + 4 <= n)
-                *(uint32_t *)(out + i0) = na;
-            else
-                for (uint32_t r = 0; i0 + r < n; ++r) out[i0 + r] = (uint8_t)(na >> (8 * r));
-        }
-    }
-}
-
-// Wave-scope ordering of LDS traffic between the lanes of one wave (a wave's DS instructions
-// execute in order; this keeps the compiler from moving them across the hand-off).
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Phase p > 0 with the range's gathers compacted across the wave (probe_compact = KPT).  In
-// k_probe_phase each of a wave's 4 x 7 (key, position) steps issues a gather instruction in which
-// only the lanes whose position lies in the range and whose key is alive take part: about a fifth
-// of the lanes with 3 ranges.  Here, for each position index q, the wave collects the (key,
-// position) pairs that need a gather at q (alive, in range) into LDS with one ballot per key slot,
-// issues them as full gather instructions (one per 64 pairs) and hands each bit back to its key:
-// 7 mostly-full gather instructions per wave and range instead of 28 sparse ones.  A key still
-// tests its in-range positions in order q = 0..6 and stops at its first clear bit, so the gathers
-// and the answers are those of k_probe_phase (MayContain's early exit, lsm/bloom.go:86-89).
-// Thread t of the wave owns keys [wave_base + KPT t, + KPT); the wave loop is uniform so that every
-// lane is present to serve the compacted gathers.
-template <int KPT>
-__global__ __launch_bounds__(256) void k_probe_phase_c(const uint64_t *__restrict__ packed, uint64_t n,
-                                                       const uint32_t *__restrict__ words, ModArg md,
-                                                       uint8_t *__restrict__ out, uint32_t lo, uint32_t hi,
-                                                       uint32_t first) {
-    static_assert(KPT == 4 || KPT == 8, "k_probe_phase_c: 4 or 8 keys per thread");
-    __shared__ uint32_t items[4][64 * KPT];
-    __shared__ uint8_t hits[4][64 * KPT];
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint32_t *const it = items[wv];
-    uint8_t *const ht = hits[wv];
-    const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
-    constexpr uint64_t kMask = (1ull << kPackBits) - 1;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * KPT;
-    for (uint64_t wb = ((uint64_t)blockIdx.x * blockDim.x + wv * 64) * KPT; wb < n; wb += stride) {
-        const uint64_t i0 = wb + (uint64_t)lane * KPT;
-        const bool full = i0 + KPT <= n;
-        // alive: bit r = key i0 + r is still a candidate (its bits so far are all set)
-        uint64_t a = 0;  // the answer bytes as read
-        uint32_t alive = 0;
-        if (i0 < n) {
-            if (first) {
-                alive = full ? (1u << KPT) - 1u : (1u << (uint32_t)(n - i0)) - 1u;
-            } else {
-                if (full) a = KPT == 8 ? *(const uint64_t *)(out + i0) : (uint64_t)*(const uint32_t *)(out + i0);
-                else
-                    for (uint32_t r = 0; i0 + r < n; ++r) a |= (uint64_t)out[i0 + r] << (8 * r);
-#pragma unroll
-                for (uint32_t r = 0; r < KPT; ++r) alive |= (uint32_t)((a >> (8 * r)) & 1u) << r;
-            }
-        }
-        uint32_t x[KPT], nb[KPT], nd[KPT], f[KPT];
-        uint64_t pv[KPT];
-        if (alive && full) {
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-            for (uint32_t h = 0; h < KPT / 2; ++h) {
-                const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(packed + i0 + 2 * h));
-                pv[2 * h] = (uint64_t)v.x | ((uint64_t)v.y << 32);
-                pv[2 * h + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
-            }
-        } else {
-#pragma unroll
-            for (uint32_t r = 0; r < KPT; ++r) pv[r] = (alive >> r & 1u) ? packed[i0 + r] : 0ull;
-        }
-#pragma unroll
-        for (uint32_t r = 0; r < KPT; ++r) {
-            x[r] = (uint32_t)(pv[r] & kMask);
-            const uint32_t b = (uint32_t)((pv[r] >> kPackBits) & kMask);
-            f[r] = (uint32_t)(pv[r] >> (2 * kPackBits));
-            nb[r] = m - b;
-            nd[r] = m - (b >= c ? b - c : b + (m - c));
-        }
-        const uint32_t alive0 = alive;
-#pragma unroll
-        for (int q = 0; q < 7; ++q) {
-            uint32_t slot[KPT];
-            uint32_t need = 0, total = 0;
-#pragma unroll
-            for (uint32_t r = 0; r < KPT; ++r) {
-                if (q > 0) {
-                    const uint32_t d = (f[r] >> (q - 1)) & 1u ? nd[r] : nb[r];
-                    const uint32_t t = x[r] - d;
-                    x[r] = x[r] >= d ? t : t + m;
-                }
-                const uint32_t w = x[r] >> 5;
-                const bool act = (alive >> r & 1u) && w >= lo && w < hi;
-                const uint64_t bal = __ballot(act);
-                slot[r] = total + lanes_below(bal);
-                total += (uint32_t)__popcll(bal);
-                need |= (uint32_t)act << r;
-                if (act) it[slot[r]] = x[r];
-            }
-            if (total == 0) continue;  // wave-uniform
-            wave_lds_sync();
-            for (uint32_t t = lane; t < total; t += 64) {
-                const uint32_t p = it[t];
-                ht[t] = (uint8_t)((words[p >> 5] >> (p & 31)) & 1u);
-            }
-            wave_lds_sync();
-#pragma unroll
-            for (uint32_t r = 0; r < KPT; ++r)
-                if (need >> r & 1u) alive &= ~((uint32_t)(ht[slot[r]] ^ 1u) << r);
-            wave_lds_sync();  // the next round's item writes reuse it / ht
-        }
-        if (i0 < n && (alive != alive0 || first)) {
-            uint64_t na = a;
-#pragma unroll
-            for (uint32_t r = 0; r < KPT; ++r) na = (na & ~(0xffull << (8 * r))) | ((uint64_t)(alive >> r & 1u) << (8 * r));
-            if (full) {
-                if (KPT == 8) *(uint64_t *)(out + i0) = na;
-                else *(uint32_t *)(out + i0) = (uint32_t)na;
-            } else {
-                for (uint32_t r = 0; i0 + r < n; ++r) out[i0 + r] = (uint8_t)(na >> (8 * r));
-            }
         }
     }
 }
@@ -1408,30 +1216,15 @@ hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *w
         if (e != hipSuccess) return e;
         p0 = 1;
     }
-    // probe_compact: 4 or 8 keys per thread with the range's gathers compacted across the wave
-    // (8 needs an 8-byte aligned answer array)
-    const int ckpt = o.probe_compact == 8 && ((uintptr_t)out & 7) == 0 ? 8 : o.probe_compact ? 4 : 0;
     const unsigned g = grid_for((n + 3) / 4, 256, o.grid_cap);
     for (uint64_t p = p0; p < np; ++p) {
         const uint32_t first = p == 0 ? 1u : 0u;
-        if (ckpt == 8)
-            hipLaunchKernelGGL(k_probe_phase_c<8>, dim3(grid_for((n + 7) / 8, 256, o.grid_cap)), dim3(256), 0, s, packed,
-                               n, words, md, out, bound(p), bound(p + 1), first);
-        else if (ckpt == 4)
-            hipLaunchKernelGGL(k_probe_phase_c<4>, dim3(g), dim3(256), 0, s, packed, n, words, md, out, bound(p),
+        if (o.probe_kpt == 4)
+            hipLaunchKernelGGL(k_probe_phase<true>, dim3(g), dim3(256), 0, s, packed, n, words, md, out, bound(p),
                                bound(p + 1), first);
-        else if (o.probe_kpt == 4)
-            hipLaunchKernelGGL((k_probe_phase<true, false>), dim3(g), dim3(256), 0, s, packed, n, words, md, out,
-                               bound(p), bound(p + 1), first);
-        else if (o.probe_pf_grid)
-            hipLaunchKernelGGL(k_probe_phase_pf, dim3(std::min<unsigned>(g, (unsigned)o.probe_pf_grid)), dim3(256), 0, s,
-                               packed, n, words, md, out, bound(p), bound(p + 1), first);
-        else if (o.probe_eager)
-            hipLaunchKernelGGL((k_probe_phase<false, true>), dim3(g), dim3(256), 0, s, packed, n, words, md, out,
-                               bound(p), bound(p + 1), first);
         else
-            hipLaunchKernelGGL((k_probe_phase<false, false>), dim3(g), dim3(256), 0, s, packed, n, words, md, out,
-                               bound(p), bound(p + 1), first);
+            hipLaunchKernelGGL(k_probe_phase<false>, dim3(g), dim3(256), 0, s, packed, n, words, md, out, bound(p),
+                               bound(p + 1), first);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;

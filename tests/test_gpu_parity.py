@@ -240,29 +240,21 @@ def test_sliced_probe_gather_orders(seb, golden, torch_cuda):
     ragged = 999_983
     ref_ragged = oc.probe(bits, m, k, kg.key16(kg.probe_indices(n)[:ragged]), ragged, stride=16)
     # mode 8 (phased): the second number is the phase count (0 = one per 4 MiB of filter)
-    # probe_compact (mode 8): the later ranges' gathers compacted across the wave, 4 or 8 keys per thread
-    cases = [(mode, kpt, 0) for mode in range(7) for kpt in (1, 2, 4)] + [(7, kpt, 0) for kpt in (2, 4, 6, 8)] + \
-        [(8, ph, cp) for ph in (0, 2, 4, 7) for cp in (0, 4, 8)]
-    for mode, kpt, cp in cases:
+    cases = [(mode, kpt) for mode in range(7) for kpt in (1, 2, 4)] + [(7, kpt) for kpt in (2, 4, 6, 8)] + \
+        [(8, ph) for ph in (0, 2, 4, 7)]
+    for mode, kpt in cases:
         with seb.option("probe_mode", mode), seb.option("probe_kpt", kpt if mode < 8 else 2), \
-                seb.option("probe_phases", kpt if mode == 8 else 0), seb.option("probe_slice_shift", 19), \
-                seb.option("probe_compact", cp):
+                seb.option("probe_phases", kpt if mode == 8 else 0), seb.option("probe_slice_shift", 19):
             out = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
             seb.dev_probe(seb.dev_keys(pk, n=n, stride=16), words, m, k, out)
             torch.cuda.synchronize()
-            assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"], (mode, kpt, cp)
+            assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"], (mode, kpt)
             outr = torch.full((ragged + 1,), 7, dtype=torch.uint8, device="cuda")
             seb.dev_probe(seb.dev_keys(pk[:ragged], n=ragged, stride=16), words, m, k, outr)
             torch.cuda.synchronize()
             got = outr.cpu().numpy()
-            assert np.array_equal(got[:ragged], ref_ragged), (mode, kpt, cp)
-            assert got[ragged] == 7, (mode, kpt, cp)  # nothing written past the batch
-            if mode == 8 and cp == 8:  # answers 4- but not 8-byte aligned: compaction with 4 keys per thread
-                outu = torch.full((ragged + 5,), 7, dtype=torch.uint8, device="cuda")
-                seb.dev_probe(seb.dev_keys(pk[:ragged], n=ragged, stride=16), words, m, k, outu[4:])
-                torch.cuda.synchronize()
-                got = outu.cpu().numpy()
-                assert np.array_equal(got[4:4 + ragged], ref_ragged) and (got[:4] == 7).all() and got[-1] == 7
+            assert np.array_equal(got[:ragged], ref_ragged), (mode, kpt)
+            assert got[ragged] == 7, (mode, kpt)  # nothing written past the batch
 
 
 def test_multi_packed_matches_multi(seb, golden, torch_cuda):
@@ -336,12 +328,10 @@ def test_packed_residues(seb, golden, torch_cuda):
     pk = seb.dev_keys(to_dev(torch, kg.key16(pidx)), n=n, stride=16)
     packed = torch.zeros(n, dtype=torch.int64, device="cuda")
     seb.dev_pack_residues(pk, m, k, packed)
-    for cp in (4, 8, 0):  # every range from packed words, gathers compacted across the wave or not
-        with seb.option("probe_compact", cp):
-            out = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
-            seb.dev_probe_packed(packed, n, words, m, k, out)
-            torch.cuda.synchronize()
-            assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"], cp
+    out = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    seb.dev_probe_packed(packed, n, words, m, k, out)
+    torch.cuda.synchronize()
+    assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
     # the root's fused probe: the same answers and the same packed words in one pass
     packed2 = torch.zeros(n, dtype=torch.int64, device="cuda")
     out2 = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
@@ -363,15 +353,12 @@ def test_packed_residues(seb, golden, torch_cuda):
     vpk = seb.dev_keys(to_dev(torch, pdata), to_dev(torch, poff))
     vpacked = torch.zeros(nv, dtype=torch.int64, device="cuda")
     seb.dev_pack_residues(vpk, mv, kv, vpacked)
-    vref = oc.probe(vbits, mv, kv, pdata, nv, offsets=poff)
-    for cp in (0, 4, 8):
-        with seb.option("probe_compact", cp), seb.option("probe_phases", 3):
-            vout = torch.full((nv + 1,), 7, dtype=torch.uint8, device="cuda")
-            seb.dev_probe_packed(vpacked, nv, vwords, mv, kv, vout)
-            torch.cuda.synchronize()
-            got = vout.cpu().numpy()
-            assert np.array_equal(got[:nv], vref), cp
-            assert got[nv] == 7
+    vout = torch.full((nv + 1,), 7, dtype=torch.uint8, device="cuda")
+    seb.dev_probe_packed(vpacked, nv, vwords, mv, kv, vout)
+    torch.cuda.synchronize()
+    got = vout.cpu().numpy()
+    assert np.array_equal(got[:nv], oc.probe(vbits, mv, kv, pdata, nv, offsets=poff))
+    assert got[nv] == 7
     for bad_m, bad_k in ((1 << 29, 7), (m, 6)):
         with pytest.raises(seb.SebError):
             seb.dev_pack_residues(pk, bad_m, bad_k, packed)
