@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "lsm", "lsm_wide", "route", "wal",
-                                                           "many"])
+                                                           "many", "c2_sharded"])
     ap.add_argument("--keys", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
@@ -161,6 +161,48 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
                 else f"MISMATCH build={ok_b} probe={ok_p}")
 
     st.build, st.probe, st.parity = build, probe, parity
+    return st
+
+
+def setup_c2_sharded(args, seb, kg, torch, dev, rank, world, dist):
+    """SURVEY §8(e) sharded build of ONE filter: the 10M keys of one SSTable spread over the ranks
+    (contiguous shards, resident in HBM); every rank builds a partial filter from its shard, an
+    all-to-all + OR kernel reduces each word slice on its owner and an all-gather gives every rank
+    the filter (dist_build.ShardedBuild).  Total work fixed as N grows: strong scaling."""
+    import dist_build as db
+
+    st = Setup()
+    n = args.keys
+    m, k = seb.params(n, 0.01)
+    st.m, st.k, st.n = m, k, n
+    lo, hi = db.shard_bounds(n, world, rank)
+    keys = torch.from_numpy(kg.key16(np.arange(lo, hi))).to(dev)
+    st.kd = seb.dev_keys(keys, n=hi - lo, stride=16)
+    st.sb = db.ShardedBuild(m, k, world, rank, dev)
+    build_fn, or_fn = db.gpu_fns(seb)
+    nb = (m + 7) // 8
+    # per rank: its key shard + partial filter write/clear + (world > 1) the slices read and the
+    # filter gathered back
+    st.kernel_bytes = {"sharded_build": 16.0 * (hi - lo) + 2 * nb + (3.0 * nb if world > 1 else 0.0)}
+    st.units_per_step = float(n)
+    st.scaling = "strong"
+    st.probe_name = "sharded_build"
+    st.workload = (f"C2 sharded: one filter of {n} x 16B keys @1% FPR (m={m:,}, k={k}) built from key shards on "
+                   f"{world} GPU(s): partial filters, all-to-all + OR kernel per word slice, all-gather (RCCL)")
+    st.parallelism = f"key shards x{world}, reduce-scatter(OR) + all-gather"
+
+    def step(j, buf, target):
+        st.words = st.sb.build(st.kd, build_fn, or_fn)
+
+    def parity(j):
+        if n != 10_000_000 or rank != 0:
+            return None
+        bits = seb.words_to_bits(st.words, m)
+        ok = sha(m.to_bytes(8, "little") + k.to_bytes(4, "little") + bits.tobytes()) == GOLDEN_C2
+        return "bit-exact (sha256 of the assembled filter's Encode() matches tests/golden C2)" if ok \
+            else "MISMATCH filter"
+
+    st.probe, st.parity = step, parity
     return st
 
 
@@ -469,8 +511,8 @@ def main():
         if v is not None:
             seb.set_option(o, v)
 
-    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "lsm": setup_lsm, "lsm_wide": setup_lsm, "route": setup_route, "many": setup_many,
-             "wal": setup_wal}[args.config]
+    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "lsm": setup_lsm, "lsm_wide": setup_lsm,
+             "route": setup_route, "many": setup_many, "wal": setup_wal, "c2_sharded": setup_c2_sharded}[args.config]
     st = setup(args, seb, kg, torch, dev, rank, world, dist)
     torch.cuda.synchronize()
     overlap = bool(args.overlap) and st.build is not None
@@ -541,7 +583,6 @@ def main():
     for j in range(args.warmup):
         step(j, False)
     torch.cuda.synchronize()
-    parity = st.parity(args.warmup - 1)  # on the same run, after the warm-up steps
 
     if world > 1:
         dist.barrier()
@@ -563,6 +604,11 @@ def main():
 
     kern_ms = {(st.probe_name if name == "probe" else name): float(np.mean([a.elapsed_ms(b) for a, b in pairs]))
                for name, pairs in times.items() if pairs}
+    # Parity of the last timed step's outputs, checked after the timed region: a large pageable
+    # D2H (.cpu()) delays the next kernel launch by ~20 ms on this runtime (tools/dbg_sharded_timing.py),
+    # which must not land inside the timed steps.
+    torch.cuda.synchronize()
+    parity = st.parity(args.warmup + args.steps - 1)
     value = st.units_per_step * args.steps / elapsed / 1e6
     result = None
     if rank == 0:
@@ -575,7 +621,8 @@ def main():
                 traffic = json.load(f).get(st.pmc_key or args.config, {}).get(dom, {}).get("hbm_bytes_per_launch")
         ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
         result = {
-            "metric": METRIC if args.config in ("c2c3", "c4", "c5", "lsm", "lsm_wide") else f"{args.config} {st.unit}",
+            "metric": METRIC if args.config in ("c2c3", "c4", "c5", "lsm", "lsm_wide", "c2_sharded")
+            else f"{args.config} {st.unit}",
             "value": round(value, 2), "unit": st.unit, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),
             "higher_is_better": True, "scaling": st.scaling, "vs_baseline": None, "dtype": st.dtype,

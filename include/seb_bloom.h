@@ -151,6 +151,12 @@ int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *filters, uin
 int seb_dev_build_many(const seb_keys *keys, const uint64_t *key_begin, const seb_filter_ref *filters,
                        uint32_t num_filters, void *stream);
 
+/* Sharded build of one filter: every rank ORs its key shard into a partial filter,
+ * an all-to-all hands rank g the G partials of word slice g (slice after slice), and this call
+ * ORs them: out[w] = OR_s slices[s * slice_words + w].  RCCL has no bitwise-OR reduction, so the
+ * reduce step of the exchange runs here.  Device pointers; out may not overlap slices. */
+int seb_dev_or_slices(const uint32_t *slices, uint32_t num_slices, uint64_t slice_words, uint32_t *out, void *stream);
+
 /* Small device/stream helpers for hosts without their own HIP binding (ctypes, cgo). */
 int seb_dev_alloc(void **ptr, uint64_t bytes);
 int seb_dev_free(void *ptr);

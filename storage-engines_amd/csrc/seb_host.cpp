@@ -643,6 +643,14 @@ extern "C" int seb_dev_probe_multi_packed(const uint64_t *packed, uint64_t n, co
     return SEB_OK;
 }
 
+extern "C" int seb_dev_or_slices(const uint32_t *slices, uint32_t num_slices, uint64_t slice_words, uint32_t *out,
+                                 void *stream) {
+    std::call_once(g_env_once, load_env);
+    if (slice_words && num_slices && (!slices || !out)) return fail(SEB_ERR_INVALID, "seb_dev_or_slices: null pointer");
+    HIP_OR_FAIL(launch_or_slices(slices, num_slices, slice_words, out, (hipStream_t)stream));
+    return SEB_OK;
+}
+
 static const uint32_t kLdsMax = 160 * 1024;
 
 extern "C" int seb_dev_build_many(const seb_keys *keys, const uint64_t *key_begin, const seb_filter_ref *filters,

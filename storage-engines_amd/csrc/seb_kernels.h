@@ -168,6 +168,8 @@ hipError_t launch_build_many_lds(const KeyBatch &kb, const ManyArg &ma, uint32_t
 // Packed residues (k == 7, m < 2^kPackBits): 8 bytes per key instead of the key itself.
 constexpr uint32_t kPackBits = 29;
 hipError_t launch_pack_residues(const KeyBatch &kb, const ModArg &md, uint64_t *packed, hipStream_t s);
+// out[w] = OR over s < nslices of in[s * slice_words + w] (the sharded build's reduction step)
+hipError_t launch_or_slices(const uint32_t *in, uint32_t nslices, uint64_t slice_words, uint32_t *out, hipStream_t s);
 hipError_t launch_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
                                uint8_t *out, hipStream_t s);
 // Phased probe (probe_mode 8; k == 7, m < 2^kPackBits, 4-byte aligned out): one launch per word

@@ -1240,4 +1240,48 @@ uint64_t probe_phase_count(uint64_t m) {
     return np < 1 ? 1 : np;
 }
 
+// ---- sharded build of one filter: each rank ORs its key shard into a partial
+// filter; after an all-to-all every rank holds the G partials of its own word slice, laid out
+// slice after slice, and ORs them into its slice of the final filter.  RCCL has no bitwise-OR
+// reduction (rccl.h: sum/prod/max/min/avg), so this kernel is the reduction step.  Streaming:
+// one 16-B load per slice and one 16-B store per lane when the slice is a multiple of 4 words.
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_or_slices(const uint32_t *__restrict__ in, uint32_t nslices,
+                                                   uint64_t slice_words, uint32_t *__restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    if constexpr (VEC) {
+        const uint64_t nv = slice_words / 4;
+        const uint4 *v = (const uint4 *)in;
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+            uint4 a = v[i];
+            for (uint32_t s = 1; s < nslices; ++s) {
+                const uint4 b = v[(uint64_t)s * nv + i];
+                a.x |= b.x;
+                a.y |= b.y;
+                a.z |= b.z;
+                a.w |= b.w;
+            }
+            ((uint4 *)out)[i] = a;
+        }
+    } else {
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < slice_words; i += stride) {
+            uint32_t a = in[i];
+            for (uint32_t s = 1; s < nslices; ++s) a |= in[(uint64_t)s * slice_words + i];
+            out[i] = a;
+        }
+    }
+}
+
+hipError_t launch_or_slices(const uint32_t *in, uint32_t nslices, uint64_t slice_words, uint32_t *out, hipStream_t s) {
+    if (slice_words == 0 || nslices == 0) return hipSuccess;
+    const bool vec = slice_words % 4 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0;
+    const uint64_t items = vec ? slice_words / 4 : slice_words;
+    const unsigned g = grid_for(items, 256, options().grid_cap);
+    if (vec)
+        hipLaunchKernelGGL(k_or_slices<true>, dim3(g), dim3(256), 0, s, in, nslices, slice_words, out);
+    else
+        hipLaunchKernelGGL(k_or_slices<false>, dim3(g), dim3(256), 0, s, in, nslices, slice_words, out);
+    return hipGetLastError();
+}
+
 }  // namespace seb

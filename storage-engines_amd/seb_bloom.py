@@ -104,6 +104,7 @@ _SIGS = {
     "seb_registry_multiget_list_dev": (_i, [_vp, C.POINTER(seb_keys), _vp, _u32, _vp]),
     "seb_registry_multiget_files": (_i, [_vp, C.POINTER(seb_keys), _vp, _u32, C.POINTER(_u32)]),
     "seb_workspace_bytes": (_u64, []),
+    "seb_dev_or_slices": (_i, [_vp, _u32, _u64, _vp, _vp]),
     "seb_workspace_release": (_i, []),
     "seb_dev_shard_route": (_i, [C.POINTER(seb_keys), _u32, _vp, _vp, _vp]),
     "seb_dev_shard_partition_workspace_size": (_u64, [_u64, _u32]),
@@ -472,6 +473,15 @@ def dev_keys(data, offsets=None, n: int | None = None, stride: int = 16) -> seb_
         kd = seb_keys(data.data_ptr(), None, nn, stride, 0)
     kd._keep = (data, offsets)
     return kd
+
+
+def dev_or_slices(slices, num_slices: int, out, stream=None) -> None:
+    """out = OR of the num_slices equal slices of `slices` (int32 tensors; the sharded build's
+    reduction after the all-to-all)."""
+    sw = out.numel()
+    if slices.numel() < num_slices * sw:
+        raise ValueError("slices holds fewer than num_slices * out.numel() words")
+    check(lib().seb_dev_or_slices(slices.data_ptr(), num_slices, sw, out.data_ptr(), _stream(stream)))
 
 
 def dev_clear(words, m: int, stream=None) -> None:

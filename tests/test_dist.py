@@ -169,3 +169,71 @@ def test_broadcast_pipeline_delivers_each_batch_in_order(world, lead):
         for j, got in enumerate(results[r]):
             want = _batch(7 if lead == 1 else j, n).numpy()
             assert np.array_equal(got, want), (r, j)
+
+
+# ------------------------------------------- sharded build of one filter (dist_build) ----
+
+def _oracle_build_fn(keys, words: torch.Tensor, m: int, k: int) -> None:
+    """OR the oracle's bits of `keys` ((n, 16) u8) into an int32 word tensor (little-endian words:
+    bit h = word h >> 5, bit h & 31, the device layout)."""
+    if keys.shape[0] == 0:
+        return
+    bits = oc.build(m, k, keys, keys.shape[0], stride=16)
+    buf = np.zeros(words.numel() * 4, np.uint8)
+    buf[: bits.size] = bits
+    words |= torch.from_numpy(buf.view(np.int32))
+
+
+def _oracle_or_fn(slices: torch.Tensor, nslices: int, out: torch.Tensor) -> None:
+    out.copy_(torch.from_numpy(np.bitwise_or.reduce(slices.numpy().reshape(nslices, -1), axis=0)))
+
+
+def _build_worker(rank, world, port, n, dst, q):
+    import dist_build as db
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m, k = oc.params(n, 0.01)
+        lo, hi = db.shard_bounds(n, world, rank)
+        sb = db.ShardedBuild(m, k, world, rank, "cpu")
+        got = None
+        for _ in range(2):  # a second build on the same buffers gives the same filter
+            words = sb.build(kg.key16(np.arange(lo, hi)), _oracle_build_fn, _oracle_or_fn, dst=dst)
+            got = None if words is None else words.numpy().view(np.uint8)[: (m + 7) // 8].copy()
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,dst", [(2, 50_000, None), (3, 40_001, None), (3, 30_000, 1), (2, 7, 0)])
+def test_sharded_build_matches_single_build(world, n, dst):
+    """dist_build.ShardedBuild: partial filters per key shard, all-to-all, OR of the slices,
+    all-gather (dst None) or gather to dst.  The filter equals the oracle's build of all n keys
+    (lsm/bloom.go's bit array) on every rank that receives it."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_build_worker, args=(r, world, port, n, dst, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m, k = oc.params(n, 0.01)
+    want = oc.build(m, k, kg.key16(np.arange(n)), n, stride=16)
+    for r in range(world):
+        if dst is None or r == dst:
+            assert np.array_equal(results[r], want), r
+        else:
+            assert results[r] is None
+
+
+def test_slice_words_cover_filter():
+    import dist_build as db
+    for m in (1, 31, 32, 33, 958_506, 95_850_584):
+        for world in (1, 2, 3, 8):
+            per = db.slice_words(m, world)
+            assert per % 4 == 0 and per * world >= (m + 31) // 32 and per * world * 4 >= (((m + 127) // 128) * 16)
+    assert [db.shard_bounds(10, 3, r) for r in range(3)] == [(0, 3), (3, 6), (6, 10)]

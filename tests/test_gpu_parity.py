@@ -1303,3 +1303,83 @@ def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
         assert np.array_equal(bits, ref)
     finally:
         seb.set_option("build_algo", 0)
+
+
+# ------------------------------------------------ sharded build of one filter (§8(e)) ----
+
+def test_or_slices_kernel(seb, torch_cuda):
+    """seb_dev_or_slices: out = OR of the slices, vector (multiple of 4 words, aligned) and scalar
+    (odd slice length) paths, 1..8 slices."""
+    torch = torch_cuda
+    rng = np.random.default_rng(3)
+    for ns, sw in ((1, 4096), (2, 1000), (3, 7), (8, 65536), (5, 12345)):
+        host = rng.integers(-2**31, 2**31, ns * sw, dtype=np.int64).astype(np.int32)
+        host[rng.random(host.size) < 0.5] = 0
+        slices = torch.from_numpy(host).cuda()
+        out = torch.full((sw + 1,), 77, dtype=torch.int32, device="cuda")
+        seb.dev_or_slices(slices, ns, out[:sw])
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert np.array_equal(got[:sw], np.bitwise_or.reduce(host.reshape(ns, sw), axis=0)), (ns, sw)
+        assert got[sw] == 77
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sharded_build_emulated_on_one_gpu(seb, torch_cuda, world):
+    """dist_build's data path with the collectives done by hand on one GPU: partial filters of
+    `world` key shards (the bucketed HIP build), the all-to-all as slice copies, the OR kernel per
+    slice, the all-gather as a concatenation.  Equals the single build of all keys (the oracle)."""
+    import dist_build as db
+    torch = torch_cuda
+    n = 1_000_003
+    m, k = seb.params(n, 0.01)
+    per = db.slice_words(m, world)
+    parts = []
+    for r in range(world):
+        lo, hi = db.shard_bounds(n, world, r)
+        w = torch.zeros(per * world, dtype=torch.int32, device="cuda")
+        seb.dev_build(seb.dev_keys(to_dev(torch, kg.key16(np.arange(lo, hi))), n=hi - lo, stride=16), w, m, k)
+        parts.append(w)
+    full = torch.empty(per * world, dtype=torch.int32, device="cuda")
+    for g in range(world):
+        recv = torch.cat([p[g * per:(g + 1) * per] for p in parts])
+        seb.dev_or_slices(recv, world, full[g * per:(g + 1) * per])
+    torch.cuda.synchronize()
+    want = oc.build(m, k, kg.key16(np.arange(n)), n, stride=16)
+    assert np.array_equal(seb.words_to_bits(full, m), want)
+
+
+def test_sharded_build_nccl_one_rank(seb, golden, torch_cuda):
+    """The nccl (RCCL) backend carries the int32 collectives dist_build uses (all-to-all single,
+    all-gather into a tensor, gather), on a one-rank group in this process; ShardedBuild at world 1
+    gives the C2 filter (golden digest)."""
+    import socket
+    import torch.distributed as dist
+    import dist_build as db
+    torch = torch_cuda
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        x = torch.arange(16, dtype=torch.int32, device="cuda")
+        y = torch.empty_like(x)
+        dist.all_to_all_single(y, x)
+        z = torch.empty_like(x)
+        dist.all_gather_into_tensor(z, x)
+        g = [torch.empty_like(x)]
+        dist.gather(x, gather_list=g, dst=0)
+        torch.cuda.synchronize()
+        assert torch.equal(y, x) and torch.equal(z, x) and torch.equal(g[0], x)
+    finally:
+        dist.destroy_process_group()
+    row = next(r for r in golden["fixed16"] if r["n"] == 10_000_000)
+    n, m, k = row["n"], row["m"], row["k"]
+    sb = db.ShardedBuild(m, k, 1, 0, "cuda")
+    build_fn, or_fn = db.gpu_fns(seb)
+    words = sb.build(seb.dev_keys(to_dev(torch, kg.key16(np.arange(n))), n=n, stride=16), build_fn, or_fn)
+    torch.cuda.synchronize()
+    bits = seb.words_to_bits(words, m)
+    assert sha(m.to_bytes(8, "little") + k.to_bytes(4, "little") + bits.tobytes()) == row["encode_sha256"]
