@@ -12,6 +12,9 @@ batch travels as 8-byte packed residues that rank 0's own probe emits (--bcast p
 --bcast keys sends the 16-B keys).  Per-GPU work is fixed as N grows (weak scaling); value =
 (build + probe keys over all ranks) / max-over-ranks wall time, inputs already resident in HBM.
 c4: the same with variable-length keys (8-256 B, zipf); no broadcast.
+c2_sharded / c3_partitioned: ONE filter over the ranks: its 10M keys built from key
+shards (all-to-all + OR kernel + all-gather), or its 10M-key probe batch split by key with the
+filter replicated and the answers gathered (strong scaling).
 c5: 64 compaction-sized filters (100K keys each) sharded over the ranks, a 10M-key batch
 broadcast from rank 0, multi-filter probe, answer planes gathered to rank 0 (strong scaling;
 value = batch keys / s).
@@ -61,7 +64,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "lsm", "lsm_wide", "route", "wal",
-                                                           "many", "c2_sharded"])
+                                                           "many", "c2_sharded", "c3_partitioned"])
     ap.add_argument("--keys", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
@@ -201,6 +204,49 @@ def setup_c2_sharded(args, seb, kg, torch, dev, rank, world, dist):
         ok = sha(m.to_bytes(8, "little") + k.to_bytes(4, "little") + bits.tobytes()) == GOLDEN_C2
         return "bit-exact (sha256 of the assembled filter's Encode() matches tests/golden C2)" if ok \
             else "MISMATCH filter"
+
+    st.probe, st.parity = step, parity
+    return st
+
+
+def setup_c3_partitioned(args, seb, kg, torch, dev, rank, world, dist):
+    """SURVEY §8(e) key-partitioned probe of ONE filter: the C2 filter is built on rank 0 and
+    replicated once (RCCL broadcast, setup); each step every rank probes its contiguous shard of
+    the 10M-key C3 batch (resident in HBM) and the answer bytes are gathered to rank 0
+    (dist_build.PartitionedProbe).  Total work fixed as N grows: strong scaling."""
+    import dist_build as db
+
+    st = Setup()
+    n = args.keys
+    m, k = seb.params(n, 0.01)
+    st.m, st.k, st.n = m, k, n
+    st.words = torch.zeros(db.slice_words(m, 1), dtype=torch.int32, device=dev)
+    if rank == 0:
+        seb.dev_build(seb.dev_keys(torch.from_numpy(kg.key16(np.arange(n))).to(dev), n=n, stride=16), st.words, m, k)
+    torch.cuda.synchronize()
+    if world > 1:
+        db.replicate_filter(st.words, src=0)
+    st.pp = db.PartitionedProbe(n, world, rank, dev)
+    keys = torch.from_numpy(kg.key16(kg.probe_indices(n)[st.pp.lo:st.pp.hi])).to(dev)
+    st.kd = seb.dev_keys(keys, n=st.pp.hi - st.pp.lo, stride=16)
+    probe_fn = db.gpu_probe_fn(seb)
+    nb = (m + 7) // 8
+    st.kernel_bytes = {"partitioned_probe": 17.0 * (st.pp.hi - st.pp.lo) + nb}
+    st.units_per_step = float(n)
+    st.scaling = "strong"
+    st.probe_name = "partitioned_probe"
+    st.workload = (f"C3 partitioned: one 10M-key filter (m={m:,}, k={k}) replicated to {world} GPU(s); the 10M-key "
+                   "batch (50% present) split by key over the ranks, answers gathered to rank 0 (RCCL)")
+    st.parallelism = f"key shards x{world}, filter replicated, answers gathered"
+
+    def step(j, buf, target):
+        st.ans = st.pp.probe(st.kd, st.words, m, k, probe_fn)
+
+    def parity(j):
+        if n != 10_000_000 or rank != 0:
+            return None
+        ok = sha(st.ans.cpu().numpy().tobytes()) == GOLDEN_C3
+        return "bit-exact (sha256 of the 10M gathered answers matches tests/golden C3)" if ok else "MISMATCH answers"
 
     st.probe, st.parity = step, parity
     return st
@@ -512,7 +558,8 @@ def main():
             seb.set_option(o, v)
 
     setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "lsm": setup_lsm, "lsm_wide": setup_lsm,
-             "route": setup_route, "many": setup_many, "wal": setup_wal, "c2_sharded": setup_c2_sharded}[args.config]
+             "route": setup_route, "many": setup_many, "wal": setup_wal, "c2_sharded": setup_c2_sharded,
+             "c3_partitioned": setup_c3_partitioned}[args.config]
     st = setup(args, seb, kg, torch, dev, rank, world, dist)
     torch.cuda.synchronize()
     overlap = bool(args.overlap) and st.build is not None
@@ -621,7 +668,8 @@ def main():
                 traffic = json.load(f).get(st.pmc_key or args.config, {}).get(dom, {}).get("hbm_bytes_per_launch")
         ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
         result = {
-            "metric": METRIC if args.config in ("c2c3", "c4", "c5", "lsm", "lsm_wide", "c2_sharded")
+            "metric": METRIC if args.config in ("c2c3", "c4", "c5", "lsm", "lsm_wide", "c2_sharded",
+                                                             "c3_partitioned")
             else f"{args.config} {st.unit}",
             "value": round(value, 2), "unit": st.unit, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),

@@ -1,4 +1,5 @@
-"""Sharded build of ONE SSTable filter over the GPUs of a node: one process per GPU, RCCL over xGMI.
+"""One SSTable filter over the GPUs of a node (sharded build, key-partitioned probe): one process per
+GPU, RCCL over xGMI.
 
 SURVEY.md §8(e): "Does build shard?  With one exchange step."  The reference builds a filter in one
 goroutine, one Add per entry (lsm/sstable_builder.go:30,53 -> lsm/bloom.go:70-77).  When the keys
@@ -88,3 +89,54 @@ def gpu_fns(seb) -> tuple[BuildFn, OrFn]:
         seb.dev_or_slices(slices, nslices, out)
 
     return build_fn, or_fn
+
+
+# --------------------------------------------- one filter, probe batch partitioned by key ----
+# "For one large filter: key-partition (scatter keys, broadcast the filter, gather
+# answers)".  The filter is replicated once from the rank that built or opened it; each rank
+# answers MayContain (lsm/bloom.go:82-92) for its own contiguous shard of the batch, and the
+# answer bytes are gathered (padded to equal shards) to the rank that serves the Gets.
+
+def replicate_filter(words: torch.Tensor, src: int = 0, group=None) -> torch.Tensor:
+    """RCCL broadcast of a filter's word array from its owner (in place on every rank)."""
+    dist.broadcast(words, src=src, group=group)
+    return words
+
+
+ProbeFn = Callable[[object, torch.Tensor, int, int, torch.Tensor], None]  # (keys, words, m, k, out u8)
+
+
+class PartitionedProbe:
+    """Answer buffers for repeated key-partitioned probes of one (m, k) filter: rank r owns keys
+    shard_bounds(n, world, r) of every n-key batch."""
+
+    def __init__(self, n: int, world: int, rank: int, device, group=None):
+        self.n, self.world, self.rank, self.group = n, world, rank, group
+        self.lo, self.hi = shard_bounds(n, world, rank)
+        self.width = max(hi - lo for lo, hi in (shard_bounds(n, world, r) for r in range(world)))
+        self.out = torch.zeros(max(self.width, 1), dtype=torch.uint8, device=device)
+        self.all = torch.empty(self.width * world, dtype=torch.uint8, device=device) if world > 1 else None
+
+    def probe(self, keys, words: torch.Tensor, m: int, k: int, probe_fn: ProbeFn, dst: int = 0):
+        """Probe this rank's shard `keys`; returns the batch's n answers (u8, batch order) on dst, None
+        elsewhere."""
+        if self.hi > self.lo:
+            probe_fn(keys, words, m, k, self.out[: self.hi - self.lo])
+        if self.world == 1:
+            return self.out[: self.n]
+        chunks = list(self.all.chunk(self.world)) if self.rank == dst else None
+        dist.gather(self.out[: self.width], gather_list=chunks, dst=dst, group=self.group)
+        if self.rank != dst:
+            return None
+        parts = []
+        for r in range(self.world):
+            lo, hi = shard_bounds(self.n, self.world, r)
+            parts.append(self.all[r * self.width: r * self.width + (hi - lo)])
+        return torch.cat(parts)
+
+
+def gpu_probe_fn(seb) -> ProbeFn:
+    def probe_fn(keys, words: torch.Tensor, m: int, k: int, out: torch.Tensor) -> None:
+        seb.dev_probe(keys, words, m, k, out)
+
+    return probe_fn

@@ -237,3 +237,53 @@ def test_slice_words_cover_filter():
             per = db.slice_words(m, world)
             assert per % 4 == 0 and per * world >= (m + 31) // 32 and per * world * 4 >= (((m + 127) // 128) * 16)
     assert [db.shard_bounds(10, 3, r) for r in range(3)] == [(0, 3), (3, 6), (6, 10)]
+
+
+def _oracle_single_probe_fn(keys, words: torch.Tensor, m: int, k: int, out: torch.Tensor) -> None:
+    bits = words.numpy().view(np.uint8)[: (m + 7) // 8]
+    out.copy_(torch.from_numpy(oc.probe(bits, m, k, keys, keys.shape[0], stride=16)))
+
+
+def _pprobe_worker(rank, world, port, n, nq, dst, q):
+    import dist_build as db
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m, k = oc.params(n, 0.01)
+        nw = db.slice_words(m, 1)
+        words = torch.zeros(nw, dtype=torch.int32)
+        if rank == 1 % world:  # the filter's owner builds it; the others receive it
+            _oracle_build_fn(kg.key16(np.arange(n)), words, m, k)
+        db.replicate_filter(words, src=1 % world)
+        pp = db.PartitionedProbe(nq, world, rank, "cpu")
+        keys = kg.key16(kg.probe_indices(n, count=nq)[pp.lo:pp.hi])
+        ans = pp.probe(keys, words, m, k, _oracle_single_probe_fn, dst=dst)
+        q.put((rank, None if ans is None else ans.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,nq,dst", [(2, 20_001, 0), (3, 30_000, 2), (3, 2, 0)])
+def test_partitioned_probe_of_one_filter(world, nq, dst):
+    """dist_build.PartitionedProbe: the filter replicated from its owner, the batch split by key
+    over the ranks, answers gathered in batch order = the oracle's MayContain of every key."""
+    n = 20_000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pprobe_worker, args=(r, world, port, n, nq, dst, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m, k = oc.params(n, 0.01)
+    bits = oc.build(m, k, kg.key16(np.arange(n)), n, stride=16)
+    want = oc.probe(bits, m, k, kg.key16(kg.probe_indices(n, count=nq)), nq, stride=16)
+    for r in range(world):
+        if r == dst:
+            assert np.array_equal(results[r], want)
+        else:
+            assert results[r] is None

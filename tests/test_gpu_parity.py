@@ -1383,3 +1383,18 @@ def test_sharded_build_nccl_one_rank(seb, golden, torch_cuda):
     torch.cuda.synchronize()
     bits = seb.words_to_bits(words, m)
     assert sha(m.to_bytes(8, "little") + k.to_bytes(4, "little") + bits.tobytes()) == row["encode_sha256"]
+
+
+def test_partitioned_probe_one_rank(seb, golden, torch_cuda):
+    """dist_build.PartitionedProbe on one rank through the HIP probe: the C3 answers (golden)."""
+    import dist_build as db
+    torch = torch_cuda
+    row = next(r for r in golden["fixed16"] if r["n"] == 10_000_000)
+    n, m, k = row["n"], row["m"], row["k"]
+    words = torch.zeros(db.slice_words(m, 1), dtype=torch.int32, device="cuda")
+    seb.dev_build(seb.dev_keys(to_dev(torch, kg.key16(np.arange(n))), n=n, stride=16), words, m, k)
+    pp = db.PartitionedProbe(n, 1, 0, "cuda")
+    kd = seb.dev_keys(to_dev(torch, kg.key16(kg.probe_indices(n))), n=n, stride=16)
+    ans = pp.probe(kd, words, m, k, db.gpu_probe_fn(seb))
+    torch.cuda.synchronize()
+    assert sha(ans.cpu().numpy().tobytes()) == row["probe_sha256"]
