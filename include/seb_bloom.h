@@ -71,10 +71,12 @@ uint64_t seb_words_bytes(uint64_t num_bits);
 
 int seb_abi_version(void);
 /* Process-wide tuning knobs (results never change, only speed):
- *   "build_algo"      0 auto, 1 device-scope atomic OR, 2 radix-partitioned LDS build
+ *   "build_algo"      0 auto, 1 device-scope atomic OR, 2 radix-partitioned LDS build, 3 the whole
+ *                     filter in one CU's LDS (word array <= 160 KiB), keys split over workgroups
  *   "probe_split"     k == 7 probes: words gathered before the first test (0 = all 7, 2, 3)
  *   "probe_kpt"       k == 7 probes: keys per thread (1, 2, 4) — gathers in flight per lane
  *   "bucket_min_keys" auto build_algo: radix-partitioned from this many keys on
+ *   "lds_min_keys"    auto build_algo: LDS-resident filter (<= 160 KiB) from this many keys on
  *   "grid_cap"        maximum workgroups of the grid-stride kernels
  *   "probe_slice_shift" k == 7, m < 2^32 probes: slice of 2^shift words gathered per phase (0 = off)
  *   "probe_slice_grid"  sliced probe: workgroup cap (0 = grid_cap)
@@ -93,8 +95,8 @@ int seb_abi_version(void);
  *   "stream_nt"       non-temporal loads of 16-B key batches (0/1)
  *   "varlen_prehash_min_keys", "varlen_sort_min_keys"  variable-length batches: LDS pre-hash and
  *                     global length-sort thresholds
- *   "varlen_hash_keys", "varlen_hash_win"  LDS pre-hash: keys per workgroup (256, 512) and window
- *                     bytes per key (64, 72, 80)
+ *   "varlen_hash_keys", "varlen_hash_win"  LDS pre-hash: keys per workgroup (256, 512, 1024) and
+ *                     window bytes per key (48, 56, 64, 72, 80; 1024-key workgroups use 48 or 56)
  *   "varlen_prehash_packed" LDS pre-hash writes packed residues (8 B/key) for k == 7, m < 2^29
  *   "build_prepack"     fixed-width bucketed build hashes to packed residues first (0 off, 1 on)
  *   "multiget_group"    registry MultiGet tests k=7 filters 4 at a time (1) or one by one (0, default)

@@ -109,7 +109,7 @@ static bool env_flag(const char *name, long *out) {
 
 // Validated assignment of one knob; false for an unknown name or an out-of-range value.
 static bool set_opt(Options &o, const char *name, int64_t value) {
-    if (!strcmp(name, "build_algo") && value >= 0 && value <= 2) o.build_algo = (int)value;
+    if (!strcmp(name, "build_algo") && value >= 0 && value <= 3) o.build_algo = (int)value;
     else if (!strcmp(name, "probe_split") && (value == 0 || value == 2 || value == 3)) o.probe_split = (int)value;
     else if (!strcmp(name, "probe_kpt") && (value == 1 || value == 2 || value == 4 || value == 6 || value == 8)) o.probe_kpt = (int)value;
     else if (!strcmp(name, "probe_slice_shift") && value >= 0 && value <= 26) o.probe_slice_shift = (int)value;
@@ -129,9 +129,9 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "multiget_pass_kib") && value >= 0 && value <= (1 << 22)) o.multiget_pass_kib = (int)value;
     else if (!strcmp(name, "multiget_group") && (value == 0 || value == 1)) o.multiget_group = (int)value;
     else if (!strcmp(name, "multiget_order") && (value == 0 || value == 1)) o.multiget_order = (int)value;
-    else if (!strcmp(name, "varlen_hash_keys") && (value == 256 || value == 512))
+    else if (!strcmp(name, "varlen_hash_keys") && (value == 256 || value == 512 || value == 1024))
         o.varlen_hash_keys = (uint32_t)value;
-    else if (!strcmp(name, "varlen_hash_win") && (value == 64 || value == 72 || value == 80))
+    else if (!strcmp(name, "varlen_hash_win") && (value == 48 || value == 56 || value == 64 || value == 72 || value == 80))
         o.varlen_hash_win = (uint32_t)value;
     else if (!strcmp(name, "apply_threads") && (value == 256 || value == 512 || value == 1024))
         o.apply_threads = (uint32_t)value;
@@ -143,6 +143,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
     else if (!strcmp(name, "grid_cap") && value > 0 && value <= (1 << 30)) o.grid_cap = (unsigned)value;
     else if (!strcmp(name, "bucket_min_keys") && value >= 0) o.bucket_min_keys = (uint64_t)value;
+    else if (!strcmp(name, "lds_min_keys") && value >= 0) o.lds_min_keys = (uint64_t)value;
     else return false;
     return true;
 }
@@ -153,7 +154,8 @@ static const char *const kOptionNames[] = {
     "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases", "probe_pack_first", "multi_phases", "many_splits",
     "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
     "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
-    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order"};
+    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order",
+    "lds_min_keys"};
 
 static std::once_flag g_env_once;
 static void load_env() {
@@ -210,6 +212,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;
     else if (!strcmp(name, "grid_cap")) *value = o.grid_cap;
     else if (!strcmp(name, "bucket_min_keys")) *value = (int64_t)o.bucket_min_keys;
+    else if (!strcmp(name, "lds_min_keys")) *value = (int64_t)o.lds_min_keys;
     else return fail(SEB_ERR_INVALID, "seb_get_option: unknown option %s", name);
     return SEB_OK;
 }
@@ -373,7 +376,8 @@ template <typename Grow>
 static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStream_t s, void *ws, uint64_t ws_bytes,
                           Grow &&grow) {
     if (kb.n == 0 || md.k == 0) return SEB_OK;
-    const bool bucketed = choose_build_algo(kb.n, md.m, md.k) == 2;
+    const int algo = choose_build_algo(kb.n, md.m, md.k);
+    const bool bucketed = algo == 2;
     // build_prepack: fixed-width keys hashed to packed residues by a full-occupancy kernel first,
     // so the scatter (4 waves per SIMD) only derives positions from 8-byte words
     const bool prepack = bucketed && !kb.offsets && !kb.hashes && options().build_prepack && md.k == 7 &&
@@ -410,6 +414,18 @@ static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStr
     if (perm_b) HIP_OR_FAIL(launch_len_perm(kb, (uint8_t *)ws + pre_b, perm_b, s, &kb.perm));
     if (bucketed) {
         HIP_OR_FAIL(launch_build_bucketed(kb, words, md, (uint8_t *)ws + head, ws_bytes - head, s));
+        return SEB_OK;
+    }
+    if (algo == 3) {  // the whole filter in one CU's LDS, the keys split over workgroups (build_many's kernel)
+        ManyArg ma;
+        memset(&ma, 0, sizeof ma);
+        ma.nf = 1;
+        ma.f[0].words = words;
+        ma.f[0].nwords = seb_words_bytes(md.m) / 4;
+        ma.f[0].key_begin = 0;
+        ma.f[0].key_end = kb.n;
+        ma.f[0].md = md;
+        HIP_OR_FAIL(launch_build_many_lds(kb, ma, (uint32_t)seb_words_bytes(md.m), s));
         return SEB_OK;
     }
     HIP_OR_FAIL(launch_build(kb, words, md, s));

@@ -38,6 +38,7 @@ struct MultiArg {  // passed by value (kernel arguments), <= 64 filters
 };
 
 constexpr int kMaxMany = 32;
+constexpr uint64_t kLdsFilterBytes = 160 * 1024;  // a filter whose word array fits one CU's LDS
 struct ManyFilter {
     uint32_t *words;
     uint64_t nwords;
@@ -94,7 +95,7 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
 
 // Process-wide tuning knobs (seb_set_option).
 struct Options {
-    int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed)
+    int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed), 3 LDS-resident filter
     int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
     int multiget_order = 1;       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
     int multiget_group = 0;       // MultiGet (k = 7, m < 2^31): test filters 4 at a time (1; measured slower) or one by one (0)
@@ -110,7 +111,8 @@ struct Options {
     int probe_kpt = 2;            // k == 7 probes: keys per thread (1, 2, 4)
     int probe_slice_shift = 19;   // k == 7, m < 2^31: sliced probe with 2^shift-word (2 MiB) slices (0 = off)
     unsigned probe_slice_grid = 0;  // workgroups of the sliced probe (0 = one thread per KPT keys)
-    uint64_t bucket_min_keys = 1u << 18;  // auto: bucketed build from this many keys on
+    uint64_t bucket_min_keys = 100000;  // auto: bucketed build from this many keys on
+    uint64_t lds_min_keys = 75000;      // auto: LDS-resident build (filter <= 160 KiB) from this many keys on
     int scatter_threads = 1024;
     int scatter_kpt = 5;          // bucketed build, k == 7: keys per thread per round (4: 112 KiB LDS, 5: 140 KiB)
     int stream_nt = 1;            // non-temporal loads for 16-B key batches (keeps filter lines in L2)

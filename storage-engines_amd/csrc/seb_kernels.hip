@@ -873,11 +873,18 @@ Options &options() {
     return o;
 }
 
+// 1 device-scope atomics, 2 radix-partitioned (bucketed), 3 the whole filter in one CU's LDS
+// with the keys split over workgroups (k_build_many_lds).  Auto (tools/small_builds.py,
+// profiles/r02_small_builds.jsonl): atomics below ~75K keys, the LDS build while the filter fits
+// 160 KiB (m <= 1.31M bits), bucketed from 100K keys for larger filters.
 int choose_build_algo(uint64_t n, uint64_t m, uint32_t k) {
     const Options &o = options();
-    if (o.build_algo == 1 || !bucketed_supported(m, k)) return 1;
-    if (o.build_algo == 2) return 2;
-    return n >= o.bucket_min_keys ? 2 : 1;
+    const bool lds = (m + 127) / 128 * 16 <= kLdsFilterBytes;
+    if (o.build_algo == 1) return 1;
+    if (o.build_algo == 2) return bucketed_supported(m, k) ? 2 : 1;
+    if (o.build_algo == 3) return lds ? 3 : 1;
+    if (lds && n >= o.lds_min_keys) return 3;
+    return bucketed_supported(m, k) && n >= o.bucket_min_keys ? 2 : 1;
 }
 
 template <typename Src, int KFIX, bool M32>

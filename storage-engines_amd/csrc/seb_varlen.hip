@@ -210,9 +210,17 @@ __global__ __launch_bounds__(KEYS) void k_hash_varlen(const uint8_t *__restrict_
 template <uint32_t KEYS, bool PACK>
 static hipError_t launch_hash_varlen_keys(const KeyBatch &kb, void *out, const ModArg &md, uint32_t win,
                                           hipStream_t s) {
-    auto k = win == 64   ? k_hash_varlen<KEYS, 64, PACK>
-             : win == 72 ? k_hash_varlen<KEYS, 72, PACK>
-                         : k_hash_varlen<KEYS, 80, PACK>;
+    // 1024-key workgroups: the window is at most 56 B per key (16-bit window offsets); two such
+    // workgroups (55 KB of LDS each) share a CU
+    void (*k)(const uint8_t *, const uint64_t *, uint64_t, void *, ModArg);
+    if constexpr (KEYS == 1024)
+        k = win <= 48 ? k_hash_varlen<1024, 48, PACK> : k_hash_varlen<1024, 56, PACK>;
+    else
+        k = win == 48   ? k_hash_varlen<KEYS, 48, PACK>
+            : win == 56 ? k_hash_varlen<KEYS, 56, PACK>
+            : win == 64 ? k_hash_varlen<KEYS, 64, PACK>
+            : win == 72 ? k_hash_varlen<KEYS, 72, PACK>
+                        : k_hash_varlen<KEYS, 80, PACK>;
     hipLaunchKernelGGL(k, dim3((unsigned)((kb.n + KEYS - 1) / KEYS)), dim3(KEYS), 0, s, kb.data, kb.offsets, kb.n, out,
                        md);
     return hipGetLastError();
@@ -223,6 +231,7 @@ static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const Mo
     if (!kb.offsets || kb.n == 0) return hipSuccess;
     const Options &o = options();
     if (o.varlen_hash_keys == 256) return launch_hash_varlen_keys<256, PACK>(kb, out, md, o.varlen_hash_win, s);
+    if (o.varlen_hash_keys == 1024) return launch_hash_varlen_keys<1024, PACK>(kb, out, md, o.varlen_hash_win, s);
     return launch_hash_varlen_keys<512, PACK>(kb, out, md, o.varlen_hash_win, s);
 }
 

@@ -166,9 +166,11 @@ def test_host_api_chunked_pipeline(seb, monkeypatch, torch_cuda):
 # --------------------------------------------------------- device-resident API --------------
 
 @pytest.fixture(params=[(1, 1024, 4, 1024, 0), (2, 1024, 4, 256, 0), (2, 512, 4, 512, 0), (2, 1024, 5, 1024, 0),
-                        (2, 1024, 5, 1024, 1)],
-                ids=["atomic", "bucketed", "bucketed512", "bucketed-kpt5", "bucketed-prepack"])
+                        (2, 1024, 5, 1024, 1), (3, 1024, 5, 1024, 0)],
+                ids=["atomic", "bucketed", "bucketed512", "bucketed-kpt5", "bucketed-prepack", "lds"])
 def build_algo(request, seb):
+    """Build paths: device-scope atomics, radix-partitioned (several geometries), and the
+    LDS-resident filter (algo 3; a filter over 160 KiB falls back to atomics)."""
     algo, thr, kpt, apply, prepack = request.param
     with seb.option("build_algo", algo), seb.option("scatter_threads", thr), seb.option("scatter_kpt", kpt), \
             seb.option("apply_threads", apply), seb.option("build_prepack", prepack):
@@ -409,7 +411,8 @@ def test_varlen_processing_order_invisible(seb, torch_cuda, mode, build_algo):
         assert np.array_equal(out.cpu().numpy(), oc.probe(ref, m, k, pd, n, offsets=off))
 
 
-@pytest.mark.parametrize("keys,win", [(256, 64), (256, 80), (512, 64), (512, 72), (512, 80)])
+@pytest.mark.parametrize("keys,win", [(256, 64), (256, 80), (512, 48), (512, 64), (512, 72), (512, 80), (1024, 48),
+                                      (1024, 56)])
 def test_varlen_prehash_geometries(seb, torch_cuda, keys, win):
     """Every pre-hash workgroup size and LDS window hashes like the oracle, over
     lengths that mix empty, sub-word, bucket-edge and window-overflowing keys, and a ragged
