@@ -26,6 +26,7 @@ Printed (rank 0): one JSON line with the metric, a `roofline` object for the dom
 from __future__ import annotations
 
 import argparse
+import glob
 import hashlib
 import json
 import os
@@ -662,11 +663,12 @@ def main():
     if rank == 0:
         kern = {name: (ms, st.kernel_bytes[name]) for name, ms in kern_ms.items()}
         dom = max(kern, key=lambda x: kern[x][0])
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
-        if os.path.exists(pmc_path):
+        traffic = None  # PMC-measured HBM bytes of the dominant step (the newest round's profile that has it)
+        for pmc_path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")), reverse=True):
             with open(pmc_path) as f:
                 traffic = json.load(f).get(st.pmc_key or args.config, {}).get(dom, {}).get("hbm_bytes_per_launch")
+            if traffic is not None:
+                break
         ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
         result = {
             "metric": METRIC if args.config in ("c2c3", "c4", "c5", "lsm", "lsm_wide", "c2_sharded",

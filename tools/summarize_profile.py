@@ -4,8 +4,8 @@
 
 Writes profiles/TAG_kernel_stats.csv (the rocprofv3 --kernel-trace --stats summary, verbatim),
 profiles/TAG_pmc.csv (per-kernel mean of every PMC counter over its dispatches) and merges the
-per-launch HBM traffic of the build and probe steps into profiles/pmc_r01.json, which bench.py
-reports as roofline.traffic.
+per-launch HBM traffic of the build and probe steps into profiles/pmc_r02.json (one file per
+round; --pmc-json), which bench.py reports as roofline.traffic.
 
 HBM bytes per launch, per MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB and
 come from the L2's memory-side (EA) request counters (Infinity-Cache hits included).  gfx950's
@@ -37,6 +37,8 @@ STEP_KERNELS = {  # per config: timed step name -> kernels launched by that step
     "route": {"route": ("k_route_tile", "k_route_scan_rows", "k_route_scatter")},
     "wal": {"wal_verify": ("k_wal_crc",)},
     "many": {"build_many": ("k_build_many",)},
+    "c2_sharded": {"sharded_build": ("k_bkt_scatter", "k_bkt_apply", "k_or_slices", "elementwise")},
+    "c3_partitioned": {"partitioned_probe": ("k_probe",)},
 }
 
 
@@ -51,6 +53,7 @@ def main():
     ap.add_argument("--key-bytes", type=float, default=16.0 * 10_000_000,
                     help="bytes of the 16-B-per-lane stream (keys; the WAL image for --config wal)")
     ap.add_argument("--out-tag", default=None)
+    ap.add_argument("--pmc-json", default="pmc_r02.json", help="profiles/ file the per-launch traffic is merged into")
     a = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
     tag = a.out_tag or a.tag
@@ -91,7 +94,7 @@ def main():
         steps[step] = {"hbm_bytes_per_launch": int(read + write * 1024), "read_bytes": int(read),
                        "write_bytes": int(write * 1024), "fetch_size_kib": fetch, "write_size_kib": write,
                        "kernels": sorted(set(kernels)), "source": f"profiles/{tag}_pmc.csv"}
-    out = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    out = os.path.join(ROOT, "profiles", a.pmc_json)
     doc = json.load(open(out)) if os.path.exists(out) else {}
     doc[a.config] = steps
     doc["_correction"] = __doc__.split("HBM bytes per launch")[1].strip()
