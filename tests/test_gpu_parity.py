@@ -847,6 +847,31 @@ def test_c_harness_replays_sstable_sequence(seb, golden, n, expected):
         assert res["probe_sha256"] == row["probe_sha256"]
 
 
+@pytest.mark.parametrize("n,expected", [(1000, 1000), (70000, 100000)])
+def test_c_harness_under_host_asan(seb, golden, n, expected):
+    """The SSTable replay harness against libseb_bloom.so built with host-side AddressSanitizer +
+    UndefinedBehaviorSanitizer (tools/sanitize/Makefile; device code unchanged): the C ABI's host
+    code (arena, chunked H2D pipeline, context pool, Encode/Decode) runs clean on the GPU and gives
+    the same digests as the oracle."""
+    import json
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(seb.LIB_PATH), "asan", "sstable_replay_asan")
+    if not os.path.exists(exe):
+        pytest.skip("host-ASan build missing: make -C tools/sanitize (part of __graft_entry__.build())")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
+    out = subprocess.run([exe, str(n), str(expected)], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "AddressSanitizer" not in out.stderr and "runtime error" not in out.stderr, out.stderr[-3000:]
+    res = json.loads(out.stdout)
+    m, k = oc.params(expected, 0.01)
+    bits = oc.build(m, k, kg.key16(np.arange(n)), n, stride=16)
+    assert res["batch_matches_single"]
+    assert res["encode_sha256"] == sha(bn.encode(bits, m, k))
+    assert res["probe_sha256"] == sha(oc.probe(bits, m, k, kg.key16(kg.probe_indices(n)), n, stride=16).tobytes())
+
+
 # ------------------------------------------- registry + batched LSM lookup (SURVEY §8(f)) ----
 
 def _lsm_get_model(files, key: bytes):
