@@ -501,7 +501,11 @@ __global__ __launch_bounds__(256) void k_probe_phase(const uint64_t *__restrict_
                         x = x >= d ? t : t + m;
                     }
                     const uint32_t w = x >> 5;
+#ifdef SEB_DIAG_PHASE_NO_GATHER  // diagnostic builds only (tools/diag_lib.sh): the phase without its gathers
+                    if (live && w >= lo && w < hi) live &= (uint32_t)(x != 0xFFFFFFFFu);
+#else
                     if (live && w >= lo && w < hi) live &= words[w] >> (x & 31);
+#endif
                 }
                 na &= ~((((a >> (8 * r)) & 1u) & (live ^ 1u)) << (8 * r));
             }
