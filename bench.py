@@ -43,6 +43,8 @@ METRIC = "bloom build+probe Mkeys/s device-resident, 10M×16B keys @1% FPR, 1/2/
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
 GOLDEN_C2 = "a86f3c69041ea0caac1dc559cfb36b06d5d5513d4ee203d22878715f612a0c3a"  # sha256(Encode()) n=10M
 GOLDEN_C3 = "aba77536fae51d566de525f519cd4c573799880d63000d88a2ce3052d0b90f95"  # sha256(answers)
+GOLDEN_C4 = "1c9309f93b5b33eb6e8544eb396b918688fb408ff1049bb8cdc6d988e91d7d49"  # sha256(Encode()), C4 10M
+GOLDEN_C4_PROBE = "5e074aff5c8b95958f92af966a7cf6772997ad090e1f1b699422908cd44bb5ba"  # sha256(answers)
 GOLDEN_C5 = "0668715db8804f529bc6795461a1cbd9905bbaab44b18b88a3b29881cd29f375"  # sha256(u64 masks)
 GOLDEN_LSM = "caf8282a71e15e15141639089e86e2ae5adabdfc91f69ea47e28fe5d71a941f9"  # sha256(MultiGet masks)
 GOLDEN_LSM_WIDE = "0f50077ccda60050f48634839339b470a5ab0dd5454a277b17c296f0a0dc65b6"  # sha256(candidate rows)
@@ -51,7 +53,7 @@ GOLDEN_ROUTE_BEGIN = "0afec9b77141e0845ef7750736ed4667d1d1adf3df91c0ab47e85c0930
 GOLDEN_MANY = "18f390ebd4082f2282f8f6352c2e02f946e855b57078fcd4f21e81956050baa7"  # sha256 of the 64 C5 filter digests
 GOLDEN_WAL = "7d661e321c2804cebf541abd9c1a34463b70fe27fce3c5459a71408ac91b3e01"  # sha256(u32 CRCs), 2M records
 OPTIONS = ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "bucket_min_keys",
-           "lds_min_keys",
+           "lds_min_keys", "probe_phase_grid", "grid_cap",
            "multi_interleave", "varlen_prehash_min_keys", "varlen_sort_min_keys", "scatter_threads",
            "stream_nt", "probe_persistent", "scatter_kpt", "probe_mode", "wal_lds_kib", "probe_phases", "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win", "varlen_prehash_packed", "apply_threads", "probe_pack_first", "multi_phases", "many_splits", "build_prepack", "multiget_group", "multiget_order")
 
@@ -280,11 +282,13 @@ def setup_c4(args, seb, kg, torch, dev, rank, world, dist):
         seb.dev_build(st.kb, w, m, k)
 
     def parity(j):
-        if rank != 0:
+        if n != 10_000_000 or rank != 0:
             return None
-        ok = bool(st.out.cpu().numpy()[0::2].all())  # every even probe is a built key
-        return "no false negatives on the 5M present probes (bit-exactness: tests/test_gpu_parity.py C4)" if ok \
-            else "MISMATCH: false negative"
+        bits = seb.words_to_bits(st.wbufs[j % len(st.wbufs)], m)
+        ok_b = sha(m.to_bytes(8, "little") + k.to_bytes(4, "little") + bits.tobytes()) == GOLDEN_C4
+        ok_p = sha(st.out.cpu().numpy().tobytes()) == GOLDEN_C4_PROBE
+        return ("bit-exact (sha256 of Encode() and of the 10M answers match tests/golden varlen n=10M)"
+                if ok_b and ok_p else f"MISMATCH build={ok_b} probe={ok_p}")
 
     st.build = build
     st.probe = lambda j, buf, target: seb.dev_probe(st.pk[j % 2], st.wbufs[j % len(st.wbufs)], m, k, st.out)

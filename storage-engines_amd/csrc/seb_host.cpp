@@ -129,7 +129,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "multiget_pass_kib") && value >= 0 && value <= (1 << 22)) o.multiget_pass_kib = (int)value;
     else if (!strcmp(name, "multiget_group") && (value == 0 || value == 1)) o.multiget_group = (int)value;
     else if (!strcmp(name, "multiget_order") && (value == 0 || value == 1)) o.multiget_order = (int)value;
-    else if (!strcmp(name, "varlen_hash_keys") && (value == 256 || value == 512 || value == 1024))
+    else if (!strcmp(name, "varlen_hash_keys") && (value == 256 || value == 448 || value == 512 || value == 1024))
         o.varlen_hash_keys = (uint32_t)value;
     else if (!strcmp(name, "varlen_hash_win") && (value == 48 || value == 56 || value == 64 || value == 72 || value == 80))
         o.varlen_hash_win = (uint32_t)value;
@@ -142,6 +142,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
     else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
     else if (!strcmp(name, "grid_cap") && value > 0 && value <= (1 << 30)) o.grid_cap = (unsigned)value;
+    else if (!strcmp(name, "probe_phase_grid") && value >= 0 && value <= (1 << 30)) o.probe_phase_grid = (unsigned)value;
     else if (!strcmp(name, "bucket_min_keys") && value >= 0) o.bucket_min_keys = (uint64_t)value;
     else if (!strcmp(name, "lds_min_keys") && value >= 0) o.lds_min_keys = (uint64_t)value;
     else return false;
@@ -155,7 +156,7 @@ static const char *const kOptionNames[] = {
     "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
     "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
     "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order",
-    "lds_min_keys"};
+    "lds_min_keys", "probe_phase_grid"};
 
 static std::once_flag g_env_once;
 static void load_env() {
@@ -211,6 +212,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;
     else if (!strcmp(name, "grid_cap")) *value = o.grid_cap;
+    else if (!strcmp(name, "probe_phase_grid")) *value = o.probe_phase_grid;
     else if (!strcmp(name, "bucket_min_keys")) *value = (int64_t)o.bucket_min_keys;
     else if (!strcmp(name, "lds_min_keys")) *value = (int64_t)o.lds_min_keys;
     else return fail(SEB_ERR_INVALID, "seb_get_option: unknown option %s", name);

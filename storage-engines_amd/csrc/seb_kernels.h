@@ -102,8 +102,8 @@ struct Options {
     int multiget_pass_kib = 0;    // MultiGet: filter bytes per pass (0 = one pass; passes measured slower)
     uint64_t varlen_sort_min_keys = INT64_MAX;  // length-bucketed order (measured slower; off by default)
     uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys
-    uint32_t varlen_hash_keys = 512;  // keys per pre-hash workgroup (256, 512)
-    uint32_t varlen_hash_win = 72;    // pre-hash LDS window bytes per key (64, 72, 80)
+    uint32_t varlen_hash_keys = 448;  // keys per pre-hash workgroup (256, 448 + split chains, 512, 1024)
+    uint32_t varlen_hash_win = 64;    // pre-hash LDS window bytes per key (48 .. 80)
     uint32_t apply_threads = 1024;    // radix-partitioned build: apply workgroup size (256, 512, 1024)
     int varlen_prehash_packed = 1;    // pre-hash to packed residues where k == 7, m < 2^29 (0/1)
     int build_prepack = 0;            // fixed-width bucketed build: pack residues first (full-occupancy hash), 0/1
@@ -127,6 +127,7 @@ struct Options {
     int probe_phases = 0;         // phased probe: number of phases (0 = one per 4 MiB of filter)
     int probe_mode = 8;           // k == 7 probe: 8 = phased (one launch per filter range, default); 0-6 k_probe_sliced MODE, 7 k_probe_compact
     unsigned grid_cap = 1u << 20;
+    unsigned probe_phase_grid = 0;  // > 0: grid cap of the later probe phases (grid-stride over 4-key groups)
 };
 Options &options();
 

@@ -1227,7 +1227,7 @@ hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *w
         if (e != hipSuccess) return e;
         p0 = 1;
     }
-    const unsigned g = grid_for((n + 3) / 4, 256, o.grid_cap);
+    const unsigned g = grid_for((n + 3) / 4, 256, o.probe_phase_grid ? o.probe_phase_grid : o.grid_cap);
     for (uint64_t p = p0; p < np; ++p) {
         const uint32_t first = p == 0 ? 1u : 0u;
         if (o.probe_kpt == 4)

@@ -116,6 +116,52 @@ struct Funnel {
     }
 };
 
+// One FNV chain (A: FNV-1a = hash1, else FNV-1 = hash2) in FnvSplit's form, for the split tail
+// waves of k_hash_varlen: the same bits as the matching half of FnvSplit / fnv_word_part.
+template <bool A>
+struct FnvOne {
+    uint32_t lo = (uint32_t)kFnvOffset;
+    uint64_t acc = kFnvOffset >> 32;
+    __device__ __forceinline__ void word(uint32_t w) {
+        uint32_t d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t b = (w >> (8 * j)) & 0xffu;
+            const uint32_t x = A ? lo ^ b : lo;
+            const uint64_t p = (uint64_t)x * 435u;
+            d[j] = (uint32_t)(p >> 32) + (x << 8);
+            lo = A ? (uint32_t)p : (uint32_t)p ^ b;
+        }
+        const uint64_t t = mad_lo(d[0], pow435(3), mad_lo(d[1], pow435(2), mad_lo(d[2], 435u, d[3])));
+        acc = mad_lo((uint32_t)acc, pow435(4), t);
+    }
+    // bytes [0, r) of w (r < 4) with the plain 64-bit step; returns the chain's hash
+    __device__ __forceinline__ uint64_t finish(uint32_t w, uint32_t r) const {
+        uint64_t h = (acc << 32) | lo;
+#pragma unroll
+        for (uint32_t j = 0; j < 3; ++j) {
+            const uint64_t b = (w >> (8 * j)) & 0xffu;
+            const uint64_t nh = A ? (h ^ b) * kFnvPrime : (h * kFnvPrime) ^ b;
+            h = j < r ? nh : h;
+        }
+        return h;
+    }
+};
+
+template <bool A>
+__device__ __forceinline__ uint64_t funnel_one(const uint32_t *lds, uint32_t b, uint32_t n) {
+    uint32_t wi = b >> 2;
+    const uint32_t sh = b & 3u;
+    uint32_t cur = lds[wi];
+    FnvOne<A> f;
+    for (uint32_t j = 0; j < n >> 2; ++j) {
+        const uint32_t nxt = lds[++wi];
+        f.word(__builtin_amdgcn_alignbyte(nxt, cur, sh));
+        cur = nxt;
+    }
+    return f.finish(__builtin_amdgcn_alignbyte(lds[wi + 1], cur, sh), n & 3u);
+}
+
 // A workgroup owns KEYS consecutive keys and an LDS window of WIN bytes per key (C4 keys average
 // 40 B).  It copies the keys' byte span into LDS, counting-sorts the keys by dword length so each
 // wave walks keys of about one length, and lane t hashes sorted key t with the funnel walk.  The
@@ -132,8 +178,13 @@ __device__ __forceinline__ void put_hash(void *out, uint64_t i, uint64_t h1, uin
         ((uint4 *)out)[i] = make_uint4((uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32));
 }
 
-template <uint32_t KEYS, uint32_t WIN, bool PACK>
-__global__ __launch_bounds__(KEYS) void k_hash_varlen(const uint8_t *__restrict__ data,
+// SPLIT (KEYS = 448, 512 threads): a full workgroup's 64 longest keys (the last slots of the
+// length order, which otherwise set the workgroup's lifetime and hold its LDS after the other
+// waves are done) are hashed by the last two waves, one per FNV chain: each runs half the
+// instructions.  The FNV-1 wave hands its hashes to the FNV-1a wave through LDS for the packed
+// output; the 16-B output is written in halves.
+template <uint32_t KEYS, uint32_t WIN, bool PACK, bool SPLIT = false>
+__global__ __launch_bounds__(SPLIT ? KEYS + 64 : KEYS) void k_hash_varlen(const uint8_t *__restrict__ data,
                                                       const uint64_t *__restrict__ off, uint64_t n,
                                                       void *__restrict__ hashes, ModArg md) {
     constexpr uint32_t kHashLds = KEYS * WIN;
@@ -142,6 +193,8 @@ __global__ __launch_bounds__(KEYS) void k_hash_varlen(const uint8_t *__restrict_
     __shared__ uint32_t cur[kLenBuckets];
     __shared__ uint32_t slot_key[KEYS];  // sorted slot -> start byte in the window << 16 | length
     __shared__ uint16_t slot_idx[KEYS];  // sorted slot -> key within the workgroup
+    __shared__ uint64_t xh2[SPLIT ? 64 : 1];  // SPLIT: the FNV-1 wave's hashes for the FNV-1a wave
+    __shared__ uint32_t xflag;
     const uint32_t t = threadIdx.x;
     const uint64_t k0 = (uint64_t)blockIdx.x * KEYS;
     const uint64_t k1 = k0 + KEYS < n ? k0 + KEYS : n;
@@ -161,7 +214,8 @@ __global__ __launch_bounds__(KEYS) void k_hash_varlen(const uint8_t *__restrict_
         return;
     }
     if (t < kLenBuckets) cur[t] = 0u;
-    for (uint32_t c = t; c < (uint32_t)chunks; c += KEYS) stage[c] = ((const uint4 *)base)[c];
+    if (t == 0) xflag = 0u;
+    for (uint32_t c = t; c < (uint32_t)chunks; c += blockDim.x) stage[c] = ((const uint4 *)base)[c];
     const uint32_t len = (uint32_t)(ke - ks);
     const uint32_t dw = (len + 3) >> 2;
     const uint32_t bk = dw > 64 ? 64u : dw;
@@ -196,9 +250,37 @@ __global__ __launch_bounds__(KEYS) void k_hash_varlen(const uint8_t *__restrict_
         slot_idx[q] = (uint16_t)t;
     }
     __syncthreads();
+    const uint32_t *lds = (const uint32_t *)stage;
+    if constexpr (SPLIT) {
+        if (cnt == KEYS && t >= KEYS - 64) {  // the 64 longest keys: one wave per FNV chain
+            const uint32_t lane = t & 63, q = KEYS - 64 + lane;
+            const uint32_t sk = slot_key[q];
+            const uint64_t i = k0 + slot_idx[q];
+            if (t < KEYS) {  // FNV-1a (hash1)
+                const uint64_t h1 = funnel_one<true>(lds, sk >> 16, sk & 0xffffu);
+                if constexpr (PACK) {
+                    while (__hip_atomic_load(&xflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+                        __builtin_amdgcn_s_sleep(1);
+                    put_hash<PACK>(hashes, i, h1, xh2[lane], md);
+                } else {
+                    ((uint2 *)hashes)[2 * i] = make_uint2((uint32_t)h1, (uint32_t)(h1 >> 32));
+                }
+            } else {  // FNV-1 (hash2)
+                const uint64_t h2 = funnel_one<false>(lds, sk >> 16, sk & 0xffffu);
+                if constexpr (PACK) {
+                    xh2[lane] = h2;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane == 0) __hip_atomic_store(&xflag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    ((uint2 *)hashes)[2 * i + 1] = make_uint2((uint32_t)h2, (uint32_t)(h2 >> 32));
+                }
+            }
+            return;
+        }
+    }
     if (!mine) return;  // cnt lanes hash the cnt sorted slots
     const uint32_t sk = slot_key[t];
-    const uint32_t *lds = (const uint32_t *)stage;
     Funnel f;
     f.init(lds, sk >> 16, sk & 0xffffu);
     for (uint32_t j = 0; j < f.len >> 2; ++j) f.step(lds);
@@ -213,16 +295,21 @@ static hipError_t launch_hash_varlen_keys(const KeyBatch &kb, void *out, const M
     // 1024-key workgroups: the window is at most 56 B per key (16-bit window offsets); two such
     // workgroups (55 KB of LDS each) share a CU
     void (*k)(const uint8_t *, const uint64_t *, uint64_t, void *, ModArg);
+    constexpr bool split = KEYS == 448;  // 7 waves of keys, the top 64 split over two chain waves
     if constexpr (KEYS == 1024)
         k = win <= 48 ? k_hash_varlen<1024, 48, PACK> : k_hash_varlen<1024, 56, PACK>;
+    else if constexpr (split)
+        k = win <= 64 ? k_hash_varlen<448, 64, PACK, true>
+            : win == 72 ? k_hash_varlen<448, 72, PACK, true>
+                        : k_hash_varlen<448, 80, PACK, true>;
     else
         k = win == 48   ? k_hash_varlen<KEYS, 48, PACK>
             : win == 56 ? k_hash_varlen<KEYS, 56, PACK>
             : win == 64 ? k_hash_varlen<KEYS, 64, PACK>
             : win == 72 ? k_hash_varlen<KEYS, 72, PACK>
                         : k_hash_varlen<KEYS, 80, PACK>;
-    hipLaunchKernelGGL(k, dim3((unsigned)((kb.n + KEYS - 1) / KEYS)), dim3(KEYS), 0, s, kb.data, kb.offsets, kb.n, out,
-                       md);
+    hipLaunchKernelGGL(k, dim3((unsigned)((kb.n + KEYS - 1) / KEYS)), dim3(split ? KEYS + 64 : KEYS), 0, s, kb.data,
+                       kb.offsets, kb.n, out, md);
     return hipGetLastError();
 }
 
@@ -232,6 +319,7 @@ static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const Mo
     const Options &o = options();
     if (o.varlen_hash_keys == 256) return launch_hash_varlen_keys<256, PACK>(kb, out, md, o.varlen_hash_win, s);
     if (o.varlen_hash_keys == 1024) return launch_hash_varlen_keys<1024, PACK>(kb, out, md, o.varlen_hash_win, s);
+    if (o.varlen_hash_keys == 448) return launch_hash_varlen_keys<448, PACK>(kb, out, md, o.varlen_hash_win, s);
     return launch_hash_varlen_keys<512, PACK>(kb, out, md, o.varlen_hash_win, s);
 }
 

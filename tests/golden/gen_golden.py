@@ -80,9 +80,10 @@ def fixed_case(n: int, p: float, check_np: bool) -> dict:
 def varlen_case(n: int, p: float, check_np: bool) -> dict:
     m, k = oc.params(n, p)
     data, off = kg.varlen_keys(np.arange(n))
-    bits = oc.build(m, k, data, n, offsets=off)
+    threads = 8 if n > 1_000_000 else 1  # the 10M (BASELINE C4) row: the oracle's threaded build/probe
+    bits = oc.build(m, k, data, n, offsets=off, threads=threads)
     pdata, poff = kg.varlen_keys(kg.probe_indices(n))
-    ans = oc.probe(bits, m, k, pdata, n, offsets=poff)
+    ans = oc.probe(bits, m, k, pdata, n, offsets=poff, threads=threads)
     if check_np:
         h1, h2 = bn.fnv_varlen(data, off)
         assert np.array_equal(bn.build(h1, h2, m, k), bits)
@@ -223,13 +224,17 @@ def wal_case(lay=kg.WAL_LAYOUT) -> dict:
             "crc_sha256": sha(crc.astype("<u4").tobytes())}
 
 
+def VARLEN() -> list:
+    return [varlen_case(n, 0.01, check_np=n <= 100000) for n in [1000, 100000, 1000000, 10000000]]
+
+
 def main():
     if len(sys.argv) > 2 and sys.argv[1] == "--add":  # refresh only the named entries
         with open(OUT) as f:
             out = json.load(f)
         for name in sys.argv[2].split(","):
             out[name] = {"route": route_case, "wal": wal_case, "lsm": lsm_case, "c5": c5_case,
-                         "lsm_wide": lsm_wide_case}[name]()
+                         "lsm_wide": lsm_wide_case, "varlen": VARLEN}[name]()
             print(name, out[name], flush=True)
         with open(OUT, "w") as f:
             json.dump(out, f, indent=1)
@@ -278,7 +283,7 @@ def main():
         fixed.append(fixed_case(100000, p, check_np=True))
     out["fixed16"] = fixed
 
-    out["varlen"] = [varlen_case(n, 0.01, check_np=n <= 100000) for n in [1000, 100000, 1000000]]
+    out["varlen"] = VARLEN()
     print("varlen done", flush=True)
     out["multi"] = [multi_case(8, 10000, 160000, 0.01), multi_case(64, 2000, 256000, 0.01)]
     out["c5"] = c5_case()

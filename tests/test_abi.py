@@ -114,7 +114,7 @@ OPTION_NAMES = ["build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "
                 "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases",
                 "probe_pack_first", "multi_phases", "many_splits", "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys",
                 "varlen_hash_win", "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
-                "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order", "lds_min_keys"]
+                "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order", "lds_min_keys", "probe_phase_grid"]
 
 
 def test_options_round_trip_and_reject_bad_values(seb):
@@ -143,4 +143,4 @@ def test_options_from_environment(seb):
     out = subprocess.run(["python", "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
     apply, win, phases = map(int, out.stdout.split())
     assert apply == 512 and phases == 5
-    assert win == 72  # 13 is not a valid window: the default stays
+    assert win == 64  # 13 is not a valid window: the default stays

@@ -382,6 +382,29 @@ def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
     assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
+@pytest.mark.parametrize("packed", [0, 1])
+@pytest.mark.parametrize("keys,win", [(512, 72), (448, 64), (448, 72), (448, 80), (256, 64), (1024, 56)])
+def test_c4_prehash_geometries_golden(seb, golden, torch_cuda, keys, win, packed):
+    """C4's zipf lengths (the spans fit the LDS window, so the sorted and split-chain hashing
+    paths run rather than the overflow fallback): every pre-hash geometry, to 16-B hashes and to
+    packed residues, reproduces the C4 golden digests."""
+    torch = torch_cuda
+    n = 100000
+    row = next(r for r in golden["varlen"] if r["n"] == n)
+    m, k = row["m"], row["k"]
+    data, off = kg.varlen_keys(np.arange(n))
+    pdata, poff = kg.varlen_keys(kg.probe_indices(n))
+    with seb.option("varlen_hash_keys", keys), seb.option("varlen_hash_win", win), \
+            seb.option("varlen_prehash_min_keys", 0), seb.option("varlen_prehash_packed", packed):
+        kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
+        words, bits = dev_build_bits(seb, torch, kd, m, k)
+        assert sha(bn.encode(bits, m, k)) == row["encode_sha256"]
+        out = torch.empty(n, dtype=torch.uint8, device="cuda")
+        seb.dev_probe(seb.dev_keys(to_dev(torch, pdata), to_dev(torch, poff)), words, m, k, out)
+        torch.cuda.synchronize()
+        assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
+
+
 @pytest.mark.parametrize("mode", [(0, 1 << 40), (1 << 40, 0), (1 << 40, 1 << 40)],
                          ids=["prehash", "length-bucketed", "direct"])
 def test_varlen_processing_order_invisible(seb, torch_cuda, mode, build_algo):
@@ -412,7 +435,7 @@ def test_varlen_processing_order_invisible(seb, torch_cuda, mode, build_algo):
 
 
 @pytest.mark.parametrize("keys,win", [(256, 64), (256, 80), (512, 48), (512, 64), (512, 72), (512, 80), (1024, 48),
-                                      (1024, 56)])
+                                      (1024, 56), (448, 64), (448, 72), (448, 80)])
 def test_varlen_prehash_geometries(seb, torch_cuda, keys, win):
     """Every pre-hash workgroup size and LDS window hashes like the oracle, over
     lengths that mix empty, sub-word, bucket-edge and window-overflowing keys, and a ragged
@@ -503,20 +526,26 @@ def test_varlen_bucketed_build_chunks(seb, torch_cuda, packed):
         assert np.array_equal(bits, ref)
 
 
-def test_c4_varlen_10m_properties(seb, torch_cuda):
-    """Full C4 size: no false negatives, and the bit array equals the oracle's."""
+def test_c4_varlen_10m_properties(seb, golden, torch_cuda):
+    """Full C4 size: the filter and the 10M answers match the golden digests (tests/golden varlen
+    n = 10M, the oracle's), and every built key answers true."""
     torch = torch_cuda
     n = 10_000_000
+    row = next(r for r in golden["varlen"] if r["n"] == n)
     m, k = oc.params(n, 0.01)
+    assert (m, k) == (row["m"], row["k"])
     data, off = kg.varlen_keys(np.arange(n))
     kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
     words, bits = dev_build_bits(seb, torch, kd, m, k)
-    ref = oc.build(m, k, data, n, offsets=off, threads=16)
-    assert np.array_equal(bits, ref)
+    assert sha(bn.encode(bits, m, k)) == row["encode_sha256"]
     out = torch.empty(n, dtype=torch.uint8, device="cuda")
     seb.dev_probe(kd, words, m, k, out)  # every built key must answer true
     torch.cuda.synchronize()
     assert bool(out.all())
+    pdata, poff = kg.varlen_keys(kg.probe_indices(n))
+    seb.dev_probe(seb.dev_keys(to_dev(torch, pdata), to_dev(torch, poff)), words, m, k, out)
+    torch.cuda.synchronize()
+    assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
 @pytest.mark.parametrize("stride", [0, 1, 3, 13, 16, 24, 33, 64])

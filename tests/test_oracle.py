@@ -161,3 +161,7 @@ def test_bench_golden_digests_match_fixtures():
     consts = dict(re.findall(r'^(GOLDEN_[A-Z_0-9]+) = "([0-9a-f]{64})"', src, re.M))
     assert consts["GOLDEN_LSM"] == gold["lsm"]["mask_sha256"]
     assert consts["GOLDEN_LSM_WIDE"] == gold["lsm_wide"]["rows_sha256"]
+    c4 = next(r for r in gold["varlen"] if r["n"] == 10_000_000)
+    assert consts["GOLDEN_C4"] == c4["encode_sha256"] and consts["GOLDEN_C4_PROBE"] == c4["probe_sha256"]
+    c2 = next(r for r in gold["fixed16"] if r["n"] == 10_000_000 and r["p"] == 0.01)
+    assert consts["GOLDEN_C2"] == c2["encode_sha256"] and consts["GOLDEN_C3"] == c2["probe_sha256"]
