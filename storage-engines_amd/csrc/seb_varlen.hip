@@ -93,26 +93,31 @@ __global__ __launch_bounds__(kPermThreads) void k_len_scatter(const uint64_t *__
 // is hashed straight from HBM in input order.  Build and probe then read 16 B per key
 // (KeysHashed), exactly like the fixed 16-B path.
 // Funnel walk of one key staged in LDS: every 4 key bytes come from two aligned LDS dwords
-// (v_alignbyte), so all full words take the same path whatever the key's alignment.
+// (v_alignbyte), so all full words take the same path whatever the key's alignment.  The dword
+// after next is read one step ahead, so a step's LDS latency overlaps the previous word's hashing
+// (it reads no further than finish() reads: one dword past the key).
 struct Funnel {
-    uint32_t wi, cur, sh, len;
+    uint32_t wi, cur, nxt, sh, len;
     FnvSplit f;
     __device__ __forceinline__ void init(const uint32_t *lds, uint32_t b, uint32_t n) {
         wi = b >> 2;
         sh = b & 3u;
         len = n;
         cur = lds[wi];
+        nxt = lds[wi + 1];
     }
     __device__ __forceinline__ void step(const uint32_t *lds) {  // the next 4 bytes
-        const uint32_t nxt = lds[++wi];
+        const uint32_t ahead = lds[wi + 2];
+        ++wi;
         f.word(__builtin_amdgcn_alignbyte(nxt, cur, sh));
         cur = nxt;
+        nxt = ahead;
     }
     // the last len % 4 bytes; returns the key's (h1, h2)
-    __device__ __forceinline__ void finish(const uint32_t *lds, uint64_t &h1, uint64_t &h2) {
+    __device__ __forceinline__ void finish(const uint32_t *, uint64_t &h1, uint64_t &h2) {
         f.get(h1, h2);
         const uint32_t r = len & 3u;
-        if (r) fnv_word_part(__builtin_amdgcn_alignbyte(lds[wi + 1], cur, sh), 0u, r, h1, h2);
+        if (r) fnv_word_part(__builtin_amdgcn_alignbyte(nxt, cur, sh), 0u, r, h1, h2);
     }
 };
 
@@ -152,14 +157,16 @@ template <bool A>
 __device__ __forceinline__ uint64_t funnel_one(const uint32_t *lds, uint32_t b, uint32_t n) {
     uint32_t wi = b >> 2;
     const uint32_t sh = b & 3u;
-    uint32_t cur = lds[wi];
+    uint32_t cur = lds[wi], nxt = lds[wi + 1];
     FnvOne<A> f;
-    for (uint32_t j = 0; j < n >> 2; ++j) {
-        const uint32_t nxt = lds[++wi];
+    for (uint32_t j = 0; j < n >> 2; ++j) {  // one dword read ahead, as Funnel::step
+        const uint32_t ahead = lds[wi + 2];
+        ++wi;
         f.word(__builtin_amdgcn_alignbyte(nxt, cur, sh));
         cur = nxt;
+        nxt = ahead;
     }
-    return f.finish(__builtin_amdgcn_alignbyte(lds[wi + 1], cur, sh), n & 3u);
+    return f.finish(__builtin_amdgcn_alignbyte(nxt, cur, sh), n & 3u);
 }
 
 // A workgroup owns KEYS consecutive keys and an LDS window of WIN bytes per key (C4 keys average
