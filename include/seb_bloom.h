@@ -95,8 +95,8 @@ int seb_abi_version(void);
  *   "stream_nt"       non-temporal loads of 16-B key batches (0/1)
  *   "varlen_prehash_min_keys", "varlen_sort_min_keys"  variable-length batches: LDS pre-hash and
  *                     global length-sort thresholds
- *   "varlen_hash_keys", "varlen_hash_win"  LDS pre-hash: keys per workgroup (256, 448, 512, 1024;
- *                     448: 512 threads, the 64 longest keys hashed one FNV chain per wave) and
+ *   "varlen_hash_keys", "varlen_hash_win"  LDS pre-hash: keys per workgroup (256, 384, 448, 512, 1024;
+ *                     384 / 448: 512 threads, the 128 / 64 longest keys hashed one FNV chain per wave) and
  *                     window bytes per key (48, 56, 64, 72, 80; 1024-key workgroups use 48 or 56)
  *   "varlen_prehash_packed" LDS pre-hash writes packed residues (8 B/key) for k == 7, m < 2^29
  *   "probe_phase_grid"  > 0: workgroup cap of the later probe phases (0 = one 4-key group per thread)

@@ -129,7 +129,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "multiget_pass_kib") && value >= 0 && value <= (1 << 22)) o.multiget_pass_kib = (int)value;
     else if (!strcmp(name, "multiget_group") && (value == 0 || value == 1)) o.multiget_group = (int)value;
     else if (!strcmp(name, "multiget_order") && (value == 0 || value == 1)) o.multiget_order = (int)value;
-    else if (!strcmp(name, "varlen_hash_keys") && (value == 256 || value == 448 || value == 512 || value == 1024))
+    else if (!strcmp(name, "varlen_hash_keys") && (value == 256 || value == 384 || value == 448 || value == 512 || value == 1024))
         o.varlen_hash_keys = (uint32_t)value;
     else if (!strcmp(name, "varlen_hash_win") && (value == 48 || value == 56 || value == 64 || value == 72 || value == 80))
         o.varlen_hash_win = (uint32_t)value;

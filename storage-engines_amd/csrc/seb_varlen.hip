@@ -207,13 +207,13 @@ __device__ __forceinline__ void put_hash(void *out, uint64_t i, uint64_t h1, uin
         ((uint4 *)out)[i] = make_uint4((uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32));
 }
 
-// SPLIT (KEYS = 448, 512 threads): a full workgroup's 64 longest keys (the last slots of the
-// length order, which otherwise set the workgroup's lifetime and hold its LDS after the other
-// waves are done) are hashed by the last two waves, one per FNV chain: each runs half the
-// instructions.  The FNV-1 wave hands its hashes to the FNV-1a wave through LDS for the packed
-// output; the 16-B output is written in halves.
-template <uint32_t KEYS, uint32_t WIN, bool PACK, bool SPLIT = false>
-__global__ __launch_bounds__(SPLIT ? KEYS + 64 : KEYS) void k_hash_varlen(const uint8_t *__restrict__ data,
+// NS > 0 (KEYS = 512 - 64 * NS, 512 threads): a full workgroup's 64 * NS longest keys (the last
+// slots of the length order, which otherwise set the workgroup's lifetime and hold its LDS after
+// the other waves are done) are hashed by the last 2 * NS waves, a pair per 64 keys, one wave per
+// FNV chain: each runs half the instructions.  The FNV-1 wave hands its hashes to the FNV-1a
+// wave through LDS for the packed output; the 16-B output is written in halves.
+template <uint32_t KEYS, uint32_t WIN, bool PACK, uint32_t NS = 0>
+__global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *__restrict__ data,
                                                       const uint64_t *__restrict__ off, uint64_t n,
                                                       void *__restrict__ hashes, ModArg md) {
     constexpr uint32_t kHashLds = KEYS * WIN;
@@ -222,8 +222,8 @@ __global__ __launch_bounds__(SPLIT ? KEYS + 64 : KEYS) void k_hash_varlen(const 
     __shared__ uint32_t cur[kLenBuckets];
     __shared__ uint32_t slot_key[KEYS];  // sorted slot -> start byte in the window << 16 | length
     __shared__ uint16_t slot_idx[KEYS];  // sorted slot -> key within the workgroup
-    __shared__ uint64_t xh2[SPLIT ? 64 : 1];  // SPLIT: the FNV-1 wave's hashes for the FNV-1a wave
-    __shared__ uint32_t xflag;
+    __shared__ uint64_t xh2[NS ? 64 * NS : 1];  // the FNV-1 waves' hashes for the FNV-1a waves
+    __shared__ uint32_t xflag[NS ? NS : 1];
     const uint32_t t = threadIdx.x;
     const uint64_t k0 = (uint64_t)blockIdx.x * KEYS;
     const uint64_t k1 = k0 + KEYS < n ? k0 + KEYS : n;
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(SPLIT ? KEYS + 64 : KEYS) void k_hash_varlen(const 
         return;
     }
     if (t < kLenBuckets) cur[t] = 0u;
-    if (t == 0) xflag = 0u;
+    if (t < NS) xflag[t] = 0u;
     for (uint32_t c = t; c < (uint32_t)chunks; c += blockDim.x) stage[c] = ((const uint4 *)base)[c];
     const uint32_t len = (uint32_t)(ke - ks);
     const uint32_t dw = (len + 3) >> 2;
@@ -280,27 +280,29 @@ __global__ __launch_bounds__(SPLIT ? KEYS + 64 : KEYS) void k_hash_varlen(const 
     }
     __syncthreads();
     const uint32_t *lds = (const uint32_t *)stage;
-    if constexpr (SPLIT) {
-        if (cnt == KEYS && t >= KEYS - 64) {  // the 64 longest keys: one wave per FNV chain
-            const uint32_t lane = t & 63, q = KEYS - 64 + lane;
+    if constexpr (NS > 0) {
+        if (cnt == KEYS && t >= KEYS - 64 * NS) {  // the longest keys: a wave pair per 64, one per chain
+            const uint32_t w = (t - (KEYS - 64 * NS)) >> 6, c = w >> 1, lane = t & 63;
+            const uint32_t q = KEYS - 64 * NS + 64 * c + lane;
             const uint32_t sk = slot_key[q];
             const uint64_t i = k0 + slot_idx[q];
-            if (t < KEYS) {  // FNV-1a (hash1)
+            if ((w & 1u) == 0u) {  // FNV-1a (hash1)
                 const uint64_t h1 = funnel_one<true>(lds, sk >> 16, sk & 0xffffu);
                 if constexpr (PACK) {
-                    while (__hip_atomic_load(&xflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+                    while (__hip_atomic_load(&xflag[c], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
                         __builtin_amdgcn_s_sleep(1);
-                    put_hash<PACK>(hashes, i, h1, xh2[lane], md);
+                    put_hash<PACK>(hashes, i, h1, xh2[64 * c + lane], md);
                 } else {
                     ((uint2 *)hashes)[2 * i] = make_uint2((uint32_t)h1, (uint32_t)(h1 >> 32));
                 }
             } else {  // FNV-1 (hash2)
                 const uint64_t h2 = funnel_one<false>(lds, sk >> 16, sk & 0xffffu);
                 if constexpr (PACK) {
-                    xh2[lane] = h2;
+                    xh2[64 * c + lane] = h2;
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                     __builtin_amdgcn_wave_barrier();
-                    if (lane == 0) __hip_atomic_store(&xflag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (lane == 0)
+                        __hip_atomic_store(&xflag[c], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 } else {
                     ((uint2 *)hashes)[2 * i + 1] = make_uint2((uint32_t)h2, (uint32_t)(h2 >> 32));
                 }
@@ -324,21 +326,22 @@ static hipError_t launch_hash_varlen_keys(const KeyBatch &kb, void *out, const M
     // 1024-key workgroups: the window is at most 56 B per key (16-bit window offsets); two such
     // workgroups (55 KB of LDS each) share a CU
     void (*k)(const uint8_t *, const uint64_t *, uint64_t, void *, ModArg);
-    constexpr bool split = KEYS == 448;  // 7 waves of keys, the top 64 split over two chain waves
+    // 448 / 384 keys: 512 threads, the top 64 / 128 keys split over chain waves
+    constexpr uint32_t ns = KEYS == 448 ? 1u : KEYS == 384 ? 2u : 0u;
     if constexpr (KEYS == 1024)
         k = win <= 48 ? k_hash_varlen<1024, 48, PACK> : k_hash_varlen<1024, 56, PACK>;
-    else if constexpr (split)
-        k = win <= 64 ? k_hash_varlen<448, 64, PACK, true>
-            : win == 72 ? k_hash_varlen<448, 72, PACK, true>
-                        : k_hash_varlen<448, 80, PACK, true>;
+    else if constexpr (ns > 0)
+        k = win <= 64 ? k_hash_varlen<KEYS, 64, PACK, ns>
+            : win == 72 ? k_hash_varlen<KEYS, 72, PACK, ns>
+                        : k_hash_varlen<KEYS, 80, PACK, ns>;
     else
         k = win == 48   ? k_hash_varlen<KEYS, 48, PACK>
             : win == 56 ? k_hash_varlen<KEYS, 56, PACK>
             : win == 64 ? k_hash_varlen<KEYS, 64, PACK>
             : win == 72 ? k_hash_varlen<KEYS, 72, PACK>
                         : k_hash_varlen<KEYS, 80, PACK>;
-    hipLaunchKernelGGL(k, dim3((unsigned)((kb.n + KEYS - 1) / KEYS)), dim3(split ? KEYS + 64 : KEYS), 0, s, kb.data,
-                       kb.offsets, kb.n, out, md);
+    const uint64_t ntiles = (kb.n + KEYS - 1) / KEYS;
+    hipLaunchKernelGGL(k, dim3((unsigned)ntiles), dim3(KEYS + 64 * ns), 0, s, kb.data, kb.offsets, kb.n, out, md);
     return hipGetLastError();
 }
 
@@ -349,6 +352,7 @@ static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const Mo
     if (o.varlen_hash_keys == 256) return launch_hash_varlen_keys<256, PACK>(kb, out, md, o.varlen_hash_win, s);
     if (o.varlen_hash_keys == 1024) return launch_hash_varlen_keys<1024, PACK>(kb, out, md, o.varlen_hash_win, s);
     if (o.varlen_hash_keys == 448) return launch_hash_varlen_keys<448, PACK>(kb, out, md, o.varlen_hash_win, s);
+    if (o.varlen_hash_keys == 384) return launch_hash_varlen_keys<384, PACK>(kb, out, md, o.varlen_hash_win, s);
     return launch_hash_varlen_keys<512, PACK>(kb, out, md, o.varlen_hash_win, s);
 }
 

@@ -383,7 +383,8 @@ def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
 
 
 @pytest.mark.parametrize("packed", [0, 1])
-@pytest.mark.parametrize("keys,win", [(512, 72), (448, 64), (448, 72), (448, 80), (256, 64), (1024, 56)])
+@pytest.mark.parametrize("keys,win", [(512, 72), (448, 64), (448, 72), (448, 80), (384, 64), (384, 80), (256, 64),
+                                      (1024, 56)])
 def test_c4_prehash_geometries_golden(seb, golden, torch_cuda, keys, win, packed):
     """C4's zipf lengths (the spans fit the LDS window, so the sorted and split-chain hashing
     paths run rather than the overflow fallback): every pre-hash geometry, to 16-B hashes and to
@@ -435,7 +436,7 @@ def test_varlen_processing_order_invisible(seb, torch_cuda, mode, build_algo):
 
 
 @pytest.mark.parametrize("keys,win", [(256, 64), (256, 80), (512, 48), (512, 64), (512, 72), (512, 80), (1024, 48),
-                                      (1024, 56), (448, 64), (448, 72), (448, 80)])
+                                      (1024, 56), (448, 64), (448, 72), (448, 80), (384, 64), (384, 80)])
 def test_varlen_prehash_geometries(seb, torch_cuda, keys, win):
     """Every pre-hash workgroup size and LDS window hashes like the oracle, over
     lengths that mix empty, sub-word, bucket-edge and window-overflowing keys, and a ragged
