@@ -694,6 +694,16 @@ def main():
             "parity": parity,
             "options": {**{o: seb.get_option(o) for o in OPTIONS}, "overlap": int(overlap)},
         }
+        if args.config == "c2c3":
+            # SURVEY.md 8(d)'s secondary sector model: every bit touch one 64-B DRAM transaction (no
+            # early exit), the build also writing each touched sector back.  Most touches are L2 hits
+            # here (phased probe, bucketed build), so this can exceed the HBM peak; DESIGN.md 6.
+            spk = {"build": 16 + 2 * 64 * st.k, "probe": 16 + 64 * st.k}
+            result["roofline"]["sector_model"] = {
+                "S": 64, "bytes_per_key": spk,
+                "GB/s": {d: round(st.n * spk[d] / (kern_ms[d] * 1e-3) / 1e9, 1) for d in spk if d in kern_ms},
+                "frac": {d: round(st.n * spk[d] / (kern_ms[d] * 1e-3) / 1e9 / PEAK_HBM_GBS, 3) for d in spk
+                         if d in kern_ms}}
         if world == 1 and args.config == "c2c3" and not args.no_host_inclusive:
             result["host_inclusive"] = host_inclusive(seb, st.build_host, st.probe_host, st.m, st.k)
         if world == 1 and not args.no_cpu_baseline and args.config in ("c2c3", "c4"):
