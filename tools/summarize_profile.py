@@ -9,12 +9,14 @@ round; --pmc-json), which bench.py reports as roofline.traffic.
 
 HBM bytes per launch, per MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB and
 come from the L2's memory-side (EA) request counters (Infinity-Cache hits included).  gfx950's
-FETCH_SIZE counts exactly half the bytes of a wide (16 B/lane) coalesced streaming read; the only
-such stream in these kernels is the key batch (16 B per key, dwordx4 per lane), so
-    read  = FETCH_SIZE*1024 + key_bytes/2      (the streamed half FETCH_SIZE misses)
+FETCH_SIZE counts exactly half the bytes of a wide (16 B/lane) coalesced streaming read, so
+    read  = FETCH_SIZE*1024 + wide/2      (the streamed half FETCH_SIZE misses)
     write = WRITE_SIZE*1024
-The random 4-byte gathers of the probe are one 64-B EA request each (TCC_EA0_RDREQ), which
-FETCH_SIZE counts at 64 B; they need no correction.
+where `wide` is every 16-B-per-lane stream of the step (WIDE_STREAMS): the key batch (dwordx4 per
+lane; for variable-length keys the pre-hash's 16-B span copy), the bucketed build's u16 position
+runs read back by k_bkt_apply (uint4 loads, 2 B per position), and the packed residues (8 B per
+key) the later probe phases read as u32x4.  The random 4-byte gathers of the probe are one 64-B
+EA request each (TCC_EA0_RDREQ), which FETCH_SIZE counts at 64 B; they need no correction.
 """
 from __future__ import annotations
 
@@ -41,6 +43,14 @@ STEP_KERNELS = {  # per config: timed step name -> kernels launched by that step
     "c3_partitioned": {"partitioned_probe": ("k_probe",)},
 }
 
+
+# 16-B-per-lane streams per timed step (bytes), for the FETCH_SIZE correction; configs not listed
+# use --key-bytes.  n = 10M keys, k = 7; C4's key bytes are the golden varlen n=10M row's.
+N, K, C4_KEY_BYTES = 10_000_000, 7, 399_655_906
+WIDE_STREAMS = {
+    "c2c3": {"build": 16 * N + 2 * N * K, "probe": 16 * N + 2 * 8 * N},
+    "c4": {"build": C4_KEY_BYTES + 2 * N * K, "probe": C4_KEY_BYTES + 2 * 8 * N},
+}
 
 # kernels launched more than once per timed step (besides the phased probe's, weighted above)
 LAUNCHES_PER_STEP = {"many": {"k_build_many": 2}}  # 64 filters = two 32-filter launches
@@ -90,10 +100,12 @@ def main():
                 kernels.append(k)
             elif c == "WRITE_SIZE":
                 write += v
-        read = fetch * 1024 + a.key_bytes / 2
+        wide = WIDE_STREAMS.get(a.config, {}).get(step, a.key_bytes)
+        read = fetch * 1024 + wide / 2
         steps[step] = {"hbm_bytes_per_launch": int(read + write * 1024), "read_bytes": int(read),
                        "write_bytes": int(write * 1024), "fetch_size_kib": fetch, "write_size_kib": write,
-                       "kernels": sorted(set(kernels)), "source": f"profiles/{tag}_pmc.csv"}
+                       "wide_stream_bytes": int(wide), "kernels": sorted(set(kernels)),
+                       "source": f"profiles/{tag}_pmc.csv"}
     out = os.path.join(ROOT, "profiles", a.pmc_json)
     doc = json.load(open(out)) if os.path.exists(out) else {}
     doc[a.config] = steps
