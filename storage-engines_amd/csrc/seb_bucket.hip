@@ -64,8 +64,13 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *w
 // for hash-distributed keys: cap = mean + 8 sigma + 32) is OR-ed straight into the filter with
 // device-scope atomics instead, which k_bkt_apply's read-modify-write OR preserves.
 // LDS: sorted[THREADS*KPT7*7] u32 | cursor[nb] | fill[nb] | wsum[16] | ovf
+#ifdef SEB_SCATTER_WAVES  // diagnostic builds: cap the scatter's VGPRs so other kernels' waves fit beside it
+#define SEB_SCATTER_ATTR __attribute__((amdgpu_waves_per_eu(SEB_SCATTER_WAVES, 8)))
+#else
+#define SEB_SCATTER_ATTR
+#endif
 template <typename Src, int KFIX, int THREADS, int KPT7>
-__global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, ModArg md, uint32_t nb,
+__global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src src, uint64_t n, ModArg md, uint32_t nb,
                                                               uint32_t tile_keys, uint32_t ntiles, uint32_t cap,
                                                               uint16_t *__restrict__ regions,
                                                               uint32_t *__restrict__ counts,
