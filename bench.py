@@ -322,6 +322,7 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
     st.pk = [seb.dev_keys(b, n=n, stride=16) for b in st.pbufs]
     st.plane = torch.zeros(n, dtype=shard.plane_dtype(), device=dev)
     st.planes = [torch.empty_like(st.plane) for _ in range(world)]
+    plane_b, planes_b = dp.comm_view(st.plane), [dp.comm_view(p) for p in st.planes]  # byte views to communicate
     st.kernel_bytes = {"probe": 16.0 * n + shard.count * ((m + 7) // 8) + st.plane.element_size() * n}
     st.units_per_step = float(n)
     st.scaling = "strong"
@@ -353,7 +354,7 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
         elif shard.count:
             seb.dev_probe_multi(st.pk[j % 2], st.local, st.plane)
         if world > 1:  # only rank 0 assembles masks: gather the answer planes there
-            dist.gather(st.plane, gather_list=st.planes if rank == 0 else None, dst=0)
+            dist.gather(plane_b, gather_list=planes_b if rank == 0 else None, dst=0)
 
     def parity(j):
         if n != 10_000_000 or rank != 0:

@@ -77,9 +77,15 @@ def broadcast_keys(keys: torch.Tensor, src: int = 0, group=None, async_op: bool 
     return dist.broadcast(keys, src=src, group=group, async_op=async_op)
 
 
+def comm_view(plane: torch.Tensor) -> torch.Tensor:
+    """The plane as bytes for a collective: RCCL (torch's nccl backend) and gloo have no 16-bit
+    integer type, and 9-16 filters per rank give an int16 plane (64 filters over 4 ranks)."""
+    return plane.view(torch.uint8)
+
+
 def gather_planes(plane: torch.Tensor, world: int, group=None) -> list[torch.Tensor]:
     out = [torch.empty_like(plane) for _ in range(world)]
-    dist.all_gather(out, plane, group=group)
+    dist.all_gather([comm_view(o) for o in out], comm_view(plane), group=group)
     return out
 
 

@@ -54,7 +54,8 @@ def _worker(rank, world, port, nf, per, nprobe, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,nf", [(2, 5), (2, 2), (3, 8), (2, 1)])
+# (2, 24) and (3, 40): 12 / 14 filters per rank, an int16 plane (gathered as bytes)
+@pytest.mark.parametrize("world,nf", [(2, 5), (2, 2), (3, 8), (2, 1), (2, 24), (3, 40)])
 def test_sharded_probe_matches_single_process(world, nf):
     per, nprobe = 3000, 4000
     ctx = mp.get_context("spawn")
