@@ -58,6 +58,18 @@ OPTIONS = ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe
            "stream_nt", "probe_persistent", "scatter_kpt", "probe_mode", "wal_lds_kib", "probe_phases", "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win", "varlen_prehash_packed", "apply_threads", "probe_pack_first", "multi_phases", "many_splits", "build_prepack", "multiget_group", "multiget_order")
 
 
+def gather_ceiling():
+    """L2-resident gather ceiling measured on MI355X: 7 dependent 4-B gathers per thread from a
+    4 MiB table (tools/ubench/stream_gather.hip mode 1, profiles/r02_ubench_stream_gather.jsonl)."""
+    path = os.path.join(ROOT, "profiles", "r02_ubench_stream_gather.jsonl")
+    with open(path) as f:
+        for line in f:
+            d = json.loads(line)
+            if d.get("mode") == 1:
+                return d["Ggathers_s"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def sha(b) -> str:
     return hashlib.sha256(bytes(b)).hexdigest()
 
@@ -713,6 +725,19 @@ def main():
                 "GB/s": {d: round(st.n * spk[d] / (kern_ms[d] * 1e-3) / 1e9, 1) for d in spk if d in kern_ms},
                 "frac": {d: round(st.n * spk[d] / (kern_ms[d] * 1e-3) / 1e9 / PEAK_HBM_GBS, 3) for d in spk
                          if d in kern_ms}}
+            # The probe's real bound: filter-word gathers, counted offline per call
+            # with the oracle (tools/gather_count.py), against the measured L2-resident ceiling.
+            gpath = os.path.join(ROOT, "profiles", "gathers_c2c3.json")
+            ceil, csrc = gather_ceiling()
+            if world == 1 and "probe" in kern_ms and ceil and os.path.exists(gpath):
+                with open(gpath) as f:
+                    gc = json.load(f).get("c2c3", {}).get("probe")
+                if gc and gc["n"] == st.n:
+                    rate = gc["gathers_phased"] / (kern_ms["probe"] * 1e-3) / 1e9
+                    result["roofline"]["gather_model"] = {
+                        "gathers_per_call": gc["gathers_phased"], "Ggathers_s": round(rate, 1),
+                        "ceiling_Ggathers_s": ceil, "frac": round(rate / ceil, 3),
+                        "count_source": "profiles/gathers_c2c3.json", "ceiling_source": csrc}
         if world == 1 and args.config == "c2c3" and not args.no_host_inclusive:
             result["host_inclusive"] = host_inclusive(seb, st.build_host, st.probe_host, st.m, st.k)
         if world == 1 and not args.no_cpu_baseline and args.config in ("c2c3", "c4"):

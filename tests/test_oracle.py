@@ -5,6 +5,7 @@ The oracle is the checker of the GPU path, so it is pinned first: public FNV kno
 digests of SURVEY.md §8(c).  Reference: lsm/bloom.go:19-120.
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -165,3 +166,23 @@ def test_bench_golden_digests_match_fixtures():
     assert consts["GOLDEN_C4"] == c4["encode_sha256"] and consts["GOLDEN_C4_PROBE"] == c4["probe_sha256"]
     c2 = next(r for r in gold["fixed16"] if r["n"] == 10_000_000 and r["p"] == 0.01)
     assert consts["GOLDEN_C2"] == c2["encode_sha256"] and consts["GOLDEN_C3"] == c2["probe_sha256"]
+
+
+def test_gather_count_tool(tmp_path):
+    """tools/gather_count.py (the probe's gather count in the bench's gather_model): the phased
+    walk answers as MayContain does and the positives equal the C1 golden count; the committed
+    10M count is the one the bench reads."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "g.json"
+    subprocess.run([sys.executable, os.path.join(root, "tools", "gather_count.py"), "--n", "100000", "--out", str(out)],
+                   check=True, capture_output=True)
+    r = json.loads(out.read_text())["c2c3"]["probe"]
+    assert r["positives"] == 51233 and r["ranges"] == 1
+    assert r["gathers_phased"] == r["gathers_reference_order"]  # one range: the same order
+    with open(os.path.join(root, "profiles", "gathers_c2c3.json")) as f:
+        full = json.load(f)["c2c3"]["probe"]
+    assert full["n"] == 10_000_000 and full["positives"] == 5_233_107 and full["ranges"] == 3
