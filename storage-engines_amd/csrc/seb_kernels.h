@@ -105,6 +105,7 @@ struct Options {
     uint32_t varlen_hash_keys = 448;  // keys per pre-hash workgroup (256, 448 + split chains, 512, 1024)
     uint32_t varlen_hash_win = 64;    // pre-hash LDS window bytes per key (48 .. 80)
     uint32_t apply_threads = 1024;    // radix-partitioned build: apply workgroup size (256, 512, 1024)
+    int clear_kernel = 1;             // seb_dev_clear: 16-B store kernel (1) or hipMemsetAsync (0)
     int varlen_prehash_packed = 1;    // pre-hash to packed residues where k == 7, m < 2^29 (0/1)
     int build_prepack = 0;            // fixed-width bucketed build: pack residues first (full-occupancy hash), 0/1
     int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)
@@ -132,6 +133,8 @@ struct Options {
 Options &options();
 
 hipError_t launch_build(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s);
+// Zero `bytes` (a multiple of 16) of filter words.
+hipError_t launch_clear_words(uint32_t *words, uint64_t bytes, hipStream_t s);
 bool bucketed_supported(uint64_t m, uint32_t k);
 uint64_t bucketed_workspace_bytes(uint64_t n, uint64_t m, uint32_t k);
 // Build from packed residues (k == 7, m < 2^kPackBits); same workspace as launch_build_bucketed.

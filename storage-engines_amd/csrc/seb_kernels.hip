@@ -998,6 +998,21 @@ static hipError_t launch_probe7(const Src &src, uint64_t n, const uint32_t *word
     }
 }
 
+// Filter clear: one 16-B store per lane, 4 per thread (hipMemsetAsync's fill kernel took 7.0 us
+// for the 12 MB C2 filter, profiles/r02_kernel_stats.csv).
+__global__ __launch_bounds__(256) void k_clear_words(uint4 *__restrict__ w, uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) w[i] = make_uint4(0, 0, 0, 0);
+}
+
+hipError_t launch_clear_words(uint32_t *words, uint64_t bytes, hipStream_t s) {
+    const uint64_t n16 = bytes / 16;
+    if (n16 == 0) return hipSuccess;
+    const unsigned g = grid_for((n16 + 3) / 4, 256, options().grid_cap);
+    hipLaunchKernelGGL(k_clear_words, dim3(g), dim3(256), 0, s, (uint4 *)words, n16);
+    return hipGetLastError();
+}
+
 hipError_t launch_build(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s) {
     if (kb.n == 0 || md.k == 0) return hipSuccess;
     const bool m32 = md.m < kM32Limit;

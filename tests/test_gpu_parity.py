@@ -1456,3 +1456,26 @@ def test_partitioned_probe_one_rank(seb, golden, torch_cuda):
     ans = pp.probe(kd, words, m, k, db.gpu_probe_fn(seb))
     torch.cuda.synchronize()
     assert sha(ans.cpu().numpy().tobytes()) == row["probe_sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", [1, 0])
+def test_dev_clear(seb, torch_cuda, kernel):
+    """seb_dev_clear zeroes exactly seb_words_bytes(m) (the 16-B store kernel and hipMemsetAsync),
+    and leaves the words past it alone; a pointer that is not 16-B aligned takes the memset."""
+    torch = torch_cuda
+    seb.set_option("clear_kernel", kernel)
+    try:
+        for m in (1, 127, 128, 129, 958_506, 95_850_584):
+            nw = seb.words_bytes(m) // 4
+            buf = torch.full((nw + 8,), -1, dtype=torch.int32, device="cuda")
+            seb.dev_clear(buf, m)
+            torch.cuda.synchronize()
+            assert int(buf[:nw].abs().sum()) == 0 and bool((buf[nw:] == -1).all()), m
+            view = buf[1:]  # 4-B aligned only
+            buf.fill_(-1)
+            seb.dev_clear(view, m)
+            torch.cuda.synchronize()
+            assert int(buf[0]) == -1 and int(buf[1:nw + 1].abs().sum()) == 0 and bool((buf[nw + 1:] == -1).all()), m
+    finally:
+        seb.set_option("clear_kernel", 1)
