@@ -136,9 +136,6 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "apply_threads") && (value == 256 || value == 512 || value == 1024))
         o.apply_threads = (uint32_t)value;
     else if (!strcmp(name, "clear_kernel") && (value == 0 || value == 1)) o.clear_kernel = (int)value;
-    else if (!strcmp(name, "probe_fused") && value >= 0 && value <= 4) o.probe_fused = (int)value;
-    else if (!strcmp(name, "probe_fused_kpl") && (value == 0 || value == 16 || value == 40))
-        o.probe_fused_kpl = (int)value;
     else if (!strcmp(name, "varlen_prehash_packed") && (value == 0 || value == 1))
         o.varlen_prehash_packed = (int)value;
     else if (!strcmp(name, "build_prepack") && (value == 0 || value == 1)) o.build_prepack = (int)value;
@@ -160,7 +157,7 @@ static const char *const kOptionNames[] = {
     "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
     "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
     "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order",
-    "lds_min_keys", "probe_phase_grid", "clear_kernel", "probe_fused", "probe_fused_kpl"};
+    "lds_min_keys", "probe_phase_grid", "clear_kernel"};
 
 static std::once_flag g_env_once;
 static void load_env() {
@@ -213,8 +210,6 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "build_prepack")) *value = o.build_prepack;
     else if (!strcmp(name, "apply_threads")) *value = o.apply_threads;
     else if (!strcmp(name, "clear_kernel")) *value = o.clear_kernel;
-    else if (!strcmp(name, "probe_fused")) *value = o.probe_fused;
-    else if (!strcmp(name, "probe_fused_kpl")) *value = o.probe_fused_kpl;
     else if (!strcmp(name, "wal_lds_kib")) *value = o.wal_lds_kib;
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;
@@ -474,22 +469,14 @@ static bool want_phased(uint64_t n, const ModArg &md, const uint8_t *out) {
 static int probe_dispatch(KeyBatch kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s) {
     void *ws;
     int rc;
-    const bool fused = options().probe_fused != 0;
     if (want_phased(kb.n, md, out) && want_prehash_packed(kb, md)) {  // pre-hash to packed, all phases from it
         void *packed;
         if ((rc = cached_workspace(s, kb.n * 8, &packed, 1))) return rc;
         HIP_OR_FAIL(launch_hash_varlen_packed(kb, md, (uint64_t *)packed, s));
-        if (fused)
-            HIP_OR_FAIL(launch_probe_fused(nullptr, (const uint64_t *)packed, kb.n, words, md, out, s));
-        else
-            HIP_OR_FAIL(launch_probe_phased(nullptr, kb.n, words, md, out, (uint64_t *)packed, s));
+        HIP_OR_FAIL(launch_probe_phased(nullptr, kb.n, words, md, out, (uint64_t *)packed, s));
         return SEB_OK;
     }
     if ((rc = prepare_probe_keys(kb, s, 0, &ws))) return rc;
-    if (want_phased(kb.n, md, out) && fused && fused_keys_supported(kb)) {  // no scratch: residues in registers
-        HIP_OR_FAIL(launch_probe_fused(&kb, nullptr, kb.n, words, md, out, s));
-        return SEB_OK;
-    }
     if (want_phased(kb.n, md, out)) {  // packed residues in their own scratch (tag 1)
         void *packed;
         if ((rc = cached_workspace(s, kb.n * 8, &packed, 1))) return rc;

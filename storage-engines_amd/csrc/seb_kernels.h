@@ -106,8 +106,6 @@ struct Options {
     uint32_t varlen_hash_win = 64;    // pre-hash LDS window bytes per key (48 .. 80)
     uint32_t apply_threads = 1024;    // radix-partitioned build: apply workgroup size (256, 512, 1024)
     int clear_kernel = 1;             // seb_dev_clear: 16-B store kernel (1) or hipMemsetAsync (0)
-    int probe_fused = 0;              // phased-probe batches through the one-launch fused probe (0/1)
-    int probe_fused_kpl = 0;          // fused probe keys per lane (0 = auto, 16, 40)
     int varlen_prehash_packed = 1;    // pre-hash to packed residues where k == 7, m < 2^29 (0/1)
     int build_prepack = 0;            // fixed-width bucketed build: pack residues first (full-occupancy hash), 0/1
     int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)
@@ -184,11 +182,6 @@ hipError_t launch_probe_packed(const uint64_t *packed, uint64_t n, const uint32_
 // range of the filter (probe_phase_count of them); `packed` is 8*n bytes of scratch.
 uint64_t probe_phase_count(uint64_t m);
 // kb == nullptr: probe the packed words themselves (no phase 0 hashing).
-constexpr uint32_t kMaxFusedRanges = 8;
-// One-launch probe of the phased probe's ranges (k == 7, m < 2^29): from keys (kb) or packed words.
-hipError_t launch_probe_fused(const KeyBatch *kb, const uint64_t *packed, uint64_t n, const uint32_t *words,
-                              const ModArg &md, uint8_t *out, hipStream_t s);
-bool fused_keys_supported(const KeyBatch &kb);
 hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
                                uint64_t *packed, hipStream_t s);
 // Probe from keys that also writes the batch's packed residues.

@@ -18,7 +18,6 @@
 #include <algorithm>
 
 #include <type_traits>
-#include <utility>
 
 #include "seb_device.h"
 #include "seb_kernels.h"
@@ -516,172 +515,6 @@ __global__ __launch_bounds__(256) void k_probe_phase(const uint64_t *__restrict_
                 *(uint32_t *)(out + i0) = na;
             else
                 for (uint32_t r = 0; i0 + r < n; ++r) out[i0 + r] = (uint8_t)(na >> (8 * r));
-        }
-    }
-}
-
-// ---- fused probe (k == 7, m < 2^29; option probe_fused).  The phased probe's ranges in ONE
-// launch: a grid sized to what the chip holds at once keeps KPL keys per lane, and their packed
-// residues stay in registers from the hash to the last range.  So the batch is read once and the
-// answers written once, where the phased probe writes 80 MB of packed words, reads them back
-// twice and moves the answer bytes three times (a stream adds its whole time to the
-// gathers).  Every wave hashes its keys, then walks the ranges in order, testing the positions
-// in range p of its keys still alive (each gather only while the key's bits so far are set, as
-// MayContain's early exit).  The waves start together and carry equal work, so the chip still
-// gathers from about one range at a time.  Answers equal the reference's whatever the schedule.
-struct RangeArg {
-    uint32_t np;
-    uint32_t bound[kMaxFusedRanges + 1];
-};
-
-// One key's walk over the positions in words [lo, hi), each gather only while its bits so far are set.
-__device__ __forceinline__ uint32_t fused_chain(uint64_t v, const uint32_t *__restrict__ words, uint32_t m, uint32_t c,
-                                                uint32_t lo, uint32_t hi) {
-    constexpr uint64_t kMask = (1ull << kPackBits) - 1;
-    uint32_t live = 1u;
-    uint32_t x = (uint32_t)(v & kMask);
-    const uint32_t b = (uint32_t)((v >> kPackBits) & kMask), f = (uint32_t)(v >> (2 * kPackBits));
-    const uint32_t nb = m - b, bc = b >= c ? b - c : b + (m - c), nd = m - bc;
-#pragma unroll
-    for (int q = 0; q < 7; ++q) {
-        if (q > 0) {
-            const uint32_t d = (f >> (q - 1)) & 1u ? nd : nb;
-            const uint32_t t = x - d;
-            x = x >= d ? t : t + m;
-        }
-        const uint32_t w = x >> 5;
-        if (live && w >= lo && w < hi) live &= words[w] >> (x & 31);
-    }
-    return live;
-}
-
-// Four keys' walks position-major: the four gathers of a step are in flight together.
-__device__ __forceinline__ void fused_chain4(const uint64_t *v, uint64_t &alive, int j0,
-                                             const uint32_t *__restrict__ words, uint32_t m, uint32_t c, uint32_t lo,
-                                             uint32_t hi) {
-    constexpr uint64_t kMask = (1ull << kPackBits) - 1;
-    uint32_t live[4], x[4], nb[4], nd[4], f[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        live[r] = (uint32_t)(alive >> (j0 + r)) & 1u;
-        x[r] = (uint32_t)(v[r] & kMask);
-        const uint32_t b = (uint32_t)((v[r] >> kPackBits) & kMask);
-        f[r] = (uint32_t)(v[r] >> (2 * kPackBits));
-        nb[r] = m - b;
-        nd[r] = m - (b >= c ? b - c : b + (m - c));
-    }
-#pragma unroll
-    for (int q = 0; q < 7; ++q) {
-        uint32_t g[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (q > 0) {
-                const uint32_t d = (f[r] >> (q - 1)) & 1u ? nd[r] : nb[r];
-                const uint32_t t = x[r] - d;
-                x[r] = x[r] >= d ? t : t + m;
-            }
-            const uint32_t w = x[r] >> 5;
-            g[r] = ~0u;
-            if (live[r] && w >= lo && w < hi) g[r] = words[w];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) live[r] &= g[r] >> (x[r] & 31);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) alive &= ~((uint64_t)(live[r] ^ 1u) << (j0 + r));
-}
-
-// Key J of the lane: hash (or load) it, keep its packed residues, and test its positions in
-// range 0 right away, so the hashing of later keys overlaps the gathers in flight.
-template <typename Src, int KPL, int J>
-__device__ __forceinline__ void fused_load(const Src &src, uint64_t n, uint64_t base, uint64_t lanes, uint64_t gt,
-                                           const ModArg &md, uint64_t (&pv)[KPL], uint64_t &alive,
-                                           const uint32_t *__restrict__ words, uint32_t hi0) {
-    const uint64_t i = base + (uint64_t)J * lanes + gt;
-    pv[J] = 0;
-    if (i < n) {
-        if constexpr (IsPacked<Src>::value) {
-            const uint4 v = src.load(i);
-            pv[J] = (uint64_t)v.x | ((uint64_t)v.y << 32);
-        } else {
-            uint64_t h1, h2;
-            src.hash(i, h1, h2);
-            pv[J] = pack_residue(h1, h2, md);
-        }
-        alive |= (uint64_t)fused_chain(pv[J], words, (uint32_t)md.m, (uint32_t)md.c, 0u, hi0) << J;
-    }
-}
-
-template <typename Src, int KPL, int... J>
-__device__ __forceinline__ void fused_load_all(const Src &src, uint64_t n, uint64_t base, uint64_t lanes, uint64_t gt,
-                                               const ModArg &md, uint64_t (&pv)[KPL], uint64_t &alive,
-                                               const uint32_t *__restrict__ words, uint32_t hi0,
-                                               std::integer_sequence<int, J...>) {
-    (fused_load<Src, KPL, J>(src, n, base, lanes, gt, md, pv, alive, words, hi0), ...);
-}
-
-// Grid-wide barrier of a cooperative launch (every workgroup resident).  bar[0] counts arrivals
-// and is reset by the last one, bar[1] is a release generation that only grows, so no reset can
-// race a waiter and the pair is ready for the next barrier and the next launch.
-__device__ __forceinline__ void fused_grid_sync(uint32_t *bar) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t snap = __hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-            __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            while (__hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == snap)
-                __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    __syncthreads();
-}
-
-// MODE bit 0: later ranges four keys at a time (fused_chain4); bit 1: a grid barrier before each
-// later range (cooperative launch), so every wave gathers from the same range.
-// WPE waves per SIMD: caps the VGPRs (512 / WPE) so the compiler cannot hoist every key's load and
-// positions; KPL keys' residues (2 VGPRs each) stay resident.
-template <typename Src, int KPL, int WPE, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_probe_fused(
-    Src src, uint64_t n, const uint32_t *__restrict__ words, ModArg md, uint8_t *__restrict__ out, RangeArg ra,
-    uint32_t *bar) {
-    static_assert(KPL <= 64 && KPL % 4 == 0, "alive mask is one u64; groups of 4 keys");
-    const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
-    const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (uint64_t base = 0; base < n; base += lanes * KPL) {
-        uint64_t pv[KPL];
-        uint64_t alive = 0;
-        // key j of every lane at base + j * lanes + gt: coalesced.  A fold, not a loop: a loop this
-        // long is not unrolled, and pv[j] with a run-time j would live in scratch memory.
-        fused_load_all<Src, KPL>(src, n, base, lanes, gt, md, pv, alive, words, ra.bound[1],
-                                 std::make_integer_sequence<int, KPL>{});
-        for (uint32_t p = 1; p < ra.np; ++p) {
-            if constexpr (MODE & 2) fused_grid_sync(bar);
-            const uint32_t lo = ra.bound[p], hi = ra.bound[p + 1];
-            // The positions do not depend on p: without this the compiler hoists all KPL x 7 of them
-            // out of the range loop (~500 VGPRs).  Regenerating them per range costs 3 VALU a step.
-#pragma unroll
-            for (int j = 0; j < KPL; ++j) asm volatile("" : "+v"(pv[j]));
-            if constexpr (MODE & 1) {
-#pragma unroll
-                for (int j = 0; j < KPL; j += 4)
-                    if ((alive >> j) & 15ull) fused_chain4(pv + j, alive, j, words, m, c, lo, hi);
-            } else {
-#pragma unroll
-                for (int j = 0; j < KPL; ++j)
-                    if ((alive >> j) & 1ull && !fused_chain(pv[j], words, m, c, lo, hi)) alive &= ~(1ull << j);
-            }
-        }
-        if constexpr (MODE & 2) fused_grid_sync(bar);  // the next pass starts in range 0 together
-        // recomputed, not kept: CSE with the load loop's indices would hold KPL u64s across the ranges
-        uint64_t g2 = base + gt;
-        asm volatile("" : "+v"(g2));
-#pragma unroll
-        for (int j = 0; j < KPL; ++j) {
-            const uint64_t i = g2 + (uint64_t)j * lanes;
-            if (i < n) out[i] = (uint8_t)((alive >> j) & 1ull);
         }
     }
 }
@@ -1421,73 +1254,6 @@ hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *w
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
-}
-
-// Fused probe launch.  Two shapes: 16 keys per lane at 6 waves per SIMD (small batches), and 40 at
-// 4 waves per SIMD, so that one pass of the grid the chip holds at once (256 CUs x 16 waves x 64
-// lanes x 40 = 10.5M keys) covers a 10M-key batch.  Larger batches loop over passes of that size.
-// probe_fused 1..4 picks MODE 0..3 for the 40-key shape of 16-B keys (the experiment); the other
-// shapes run MODE 0.
-__device__ uint32_t g_fused_bar[2];  // zero at load; fused_grid_sync leaves it ready for reuse
-
-template <typename Src, int KPL, int WPE, int MODE>
-static hipError_t fused_t(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
-                          const RangeArg &ra, hipStream_t s) {
-    int dev = 0, cus = 0, per_cu = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_probe_fused<Src, KPL, WPE, MODE>, 256, 0);
-    if (e != hipSuccess) return e;
-    const uint64_t resident = (uint64_t)std::max(per_cu, 1) * (uint64_t)std::max(cus, 1);
-    const unsigned g = (unsigned)std::min<uint64_t>(resident, (n + 256ull * KPL - 1) / (256ull * KPL));
-    if constexpr (MODE & 2) {
-        uint32_t *bar = nullptr;
-        if ((e = hipGetSymbolAddress((void **)&bar, HIP_SYMBOL(g_fused_bar))) != hipSuccess) return e;
-        void *args[] = {(void *)&src, (void *)&n, (void *)&words, (void *)&md, (void *)&out, (void *)&ra, (void *)&bar};
-        return hipLaunchCooperativeKernel((const void *)k_probe_fused<Src, KPL, WPE, MODE>, dim3(g), dim3(256), args, 0, s);
-    } else {
-        hipLaunchKernelGGL((k_probe_fused<Src, KPL, WPE, MODE>), dim3(g), dim3(256), 0, s, src, n, words, md, out, ra,
-                           (uint32_t *)nullptr);
-        return hipGetLastError();
-    }
-}
-
-template <typename Src>
-static hipError_t fused_src(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
-                            const RangeArg &ra, hipStream_t s) {
-    const int want = options().probe_fused_kpl;
-    if (want == 16 || (want == 0 && n <= (4ull << 20))) return fused_t<Src, 16, 6, 0>(src, n, words, md, out, ra, s);
-    if constexpr (std::is_same<Src, Keys16NT>::value) {
-        switch (options().probe_fused) {
-            case 2: return fused_t<Src, 40, 4, 1>(src, n, words, md, out, ra, s);
-            case 3: return fused_t<Src, 40, 4, 2>(src, n, words, md, out, ra, s);
-            case 4: return fused_t<Src, 40, 4, 3>(src, n, words, md, out, ra, s);
-            default: break;
-        }
-    }
-    return fused_t<Src, 40, 4, 0>(src, n, words, md, out, ra, s);
-}
-
-hipError_t launch_probe_fused(const KeyBatch *kb, const uint64_t *packed, uint64_t n, const uint32_t *words,
-                              const ModArg &md, uint8_t *out, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    if (md.k != 7 || md.m >= (1ull << kPackBits)) return hipErrorInvalidValue;
-    const uint64_t nwords = (md.m + 31) / 32;
-    RangeArg ra{};
-    const uint64_t np = std::min<uint64_t>(probe_phase_count(md.m), kMaxFusedRanges);
-    ra.np = (uint32_t)np;
-    for (uint64_t p = 0; p <= np; ++p) ra.bound[p] = (uint32_t)(nwords * p / np);
-    if (!kb) return fused_src(KeysPacked{packed}, n, words, md, out, ra, s);
-    if (kb->hashes) return fused_src(KeysHashed{kb->hashes}, n, words, md, out, ra, s);
-    if (!fused_keys_supported(*kb)) return hipErrorNotSupported;
-    return fused_src(Keys16NT{(const uint4 *)kb->data}, n, words, md, out, ra, s);
-}
-
-// Fixed 16-B aligned keys or pre-hashed ones: the sources the fused probe is instantiated for.
-bool fused_keys_supported(const KeyBatch &kb) {
-    if (kb.hashes) return true;
-    return !kb.offsets && kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0;
 }
 
 // Phases of the phased probe: probe_phases, or one per 4 MiB of filter (one XCD's L2).

@@ -1479,45 +1479,3 @@ def test_dev_clear(seb, torch_cuda, kernel):
             assert int(buf[0]) == -1 and int(buf[1:nw + 1].abs().sum()) == 0 and bool((buf[nw + 1:] == -1).all()), m
     finally:
         seb.set_option("clear_kernel", 1)
-
-
-def test_fused_probe(seb, golden, torch_cuda):
-    """The one-launch fused probe (probe_fused, k_probe_fused): the C3 digest with 16 and 40 keys
-    per lane (16 keys take two passes of the resident grid at 10M keys) and 1-8 ranges, a ragged
-    batch whose last lanes are empty, and variable-length batches through both pre-hash sources
-    (packed residues and 16-B hashes) on a small filter cut into 3 ranges."""
-    torch = torch_cuda
-    row = next(r for r in golden["fixed16"] if r["n"] == 10_000_000)
-    n, m, k = row["n"], row["m"], row["k"]
-    kd = seb.dev_keys(to_dev(torch, kg.key16(np.arange(n))), n=n, stride=16)
-    words, bits = dev_build_bits(seb, torch, kd, m, k)
-    pk = to_dev(torch, kg.key16(kg.probe_indices(n)))
-    ragged = 999_983
-    ref_ragged = oc.probe(bits, m, k, kg.key16(kg.probe_indices(n)[:ragged]), ragged, stride=16)
-    for kpl in (0, 16, 40):
-        for ph in (0, 2, 5, 8):
-            with seb.option("probe_fused", 1), seb.option("probe_fused_kpl", kpl), seb.option("probe_phases", ph):
-                out = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
-                seb.dev_probe(seb.dev_keys(pk, n=n, stride=16), words, m, k, out)
-                torch.cuda.synchronize()
-                assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"], (kpl, ph)
-        with seb.option("probe_fused", 1), seb.option("probe_fused_kpl", kpl):
-            outr = torch.full((ragged + 1,), 7, dtype=torch.uint8, device="cuda")
-            seb.dev_probe(seb.dev_keys(pk[:ragged], n=ragged, stride=16), words, m, k, outr)
-            torch.cuda.synchronize()
-            got = outr.cpu().numpy()
-            assert np.array_equal(got[:ragged], ref_ragged), kpl
-            assert got[ragged] == 7, kpl  # nothing written past the batch
-    nv = 100000
-    vrow = next(r for r in golden["varlen"] if r["n"] == nv)
-    vm, vk = vrow["m"], vrow["k"]
-    data, off = kg.varlen_keys(np.arange(nv))
-    pdata, poff = kg.varlen_keys(kg.probe_indices(nv))
-    vwords, _ = dev_build_bits(seb, torch, seb.dev_keys(to_dev(torch, data), to_dev(torch, off)), vm, vk)
-    for packed in (1, 0):
-        with seb.option("probe_fused", 1), seb.option("probe_phases", 3), seb.option("varlen_prehash_min_keys", 0), \
-                seb.option("varlen_prehash_packed", packed):
-            out = torch.empty(nv, dtype=torch.uint8, device="cuda")
-            seb.dev_probe(seb.dev_keys(to_dev(torch, pdata), to_dev(torch, poff)), vwords, vm, vk, out)
-            torch.cuda.synchronize()
-            assert sha(out.cpu().numpy().tobytes()) == vrow["probe_sha256"], packed
