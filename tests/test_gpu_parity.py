@@ -1408,9 +1408,10 @@ def test_sharded_build_emulated_on_one_gpu(seb, torch_cuda, world):
 
 
 def test_sharded_build_nccl_one_rank(seb, golden, torch_cuda):
-    """The nccl (RCCL) backend carries the int32 collectives dist_build uses (all-to-all single,
-    all-gather into a tensor, gather), on a one-rank group in this process; ShardedBuild at world 1
-    gives the C2 filter (golden digest)."""
+    """The nccl (RCCL) backend carries the collectives of the multi-GPU paths (dist_build's int32
+    all-to-all single, all-gather into a tensor and gather; dist_probe's answer planes as byte
+    views; the broadcast batch dtypes), on a one-rank group in this process; ShardedBuild at
+    world 1 gives the C2 filter (golden digest)."""
     import socket
     import torch.distributed as dist
     import dist_build as db
@@ -1431,6 +1432,21 @@ def test_sharded_build_nccl_one_rank(seb, golden, torch_cuda):
         dist.gather(x, gather_list=g, dst=0)
         torch.cuda.synchronize()
         assert torch.equal(y, x) and torch.equal(z, x) and torch.equal(g[0], x)
+        # dist_probe / bench c5: answer planes of every width travel as byte views (an int16 plane,
+        # 9-16 filters per rank, has no RCCL type), packed batches as int64, keys as uint8
+        import dist_probe as dp
+        for dt in (torch.uint8, torch.int16, torch.int32, torch.int64):
+            plane = torch.arange(1000, device="cuda").to(dt)
+            got = dp.gather_planes(plane, 1)
+            gl = [torch.empty_like(plane)]
+            dist.gather(dp.comm_view(plane), gather_list=[dp.comm_view(t) for t in gl], dst=0)
+            torch.cuda.synchronize()
+            assert got[0].dtype == dt and torch.equal(got[0], plane) and torch.equal(gl[0], plane), dt
+        for dt in (torch.int64, torch.uint8):
+            b = torch.arange(64, device="cuda").to(dt)
+            dist.broadcast(b, src=0, async_op=True).wait()
+            torch.cuda.synchronize()
+            assert torch.equal(b, torch.arange(64, device="cuda").to(dt))
     finally:
         dist.destroy_process_group()
     row = next(r for r in golden["fixed16"] if r["n"] == 10_000_000)
