@@ -55,7 +55,7 @@ GOLDEN_WAL = "7d661e321c2804cebf541abd9c1a34463b70fe27fce3c5459a71408ac91b3e01" 
 OPTIONS = ("build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "bucket_min_keys",
            "lds_min_keys", "probe_phase_grid", "grid_cap",
            "multi_interleave", "varlen_prehash_min_keys", "varlen_sort_min_keys", "scatter_threads",
-           "stream_nt", "probe_persistent", "scatter_kpt", "probe_mode", "wal_lds_kib", "probe_phases", "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win", "varlen_prehash_packed", "apply_threads", "probe_pack_first", "multi_phases", "many_splits", "build_prepack", "multiget_group", "multiget_order", "clear_kernel")
+           "stream_nt", "probe_persistent", "scatter_kpt", "probe_mode", "wal_lds_kib", "probe_phases", "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win", "varlen_prehash_packed", "apply_threads", "probe_pack_first", "multi_phases", "many_splits", "build_prepack", "multiget_group", "multiget_order", "clear_kernel", "scatter_xcd")
 
 
 def gather_ceiling():

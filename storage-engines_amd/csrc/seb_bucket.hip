@@ -69,12 +69,18 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *w
 #else
 #define SEB_SCATTER_ATTR
 #endif
+// ngrp > 0 (option scatter_xcd): one region per (bucket, tile group) instead of per (bucket, tile),
+// group = blockIdx % ngrp, i.e. the workgroups of one XCD (round-robin dispatch); each round claims
+// its run in the group's region with one device atomic on counts[region].  A region's partly
+// written tail line is then shared by every tile of the XCD and stays in that XCD's L2, where
+// per-tile regions leave 32 x nb partial lines per XCD, more than its L2 holds.  counts must be
+// zero at launch; it ends holding each region's claimed length (apply clamps it to cap).
 template <typename Src, int KFIX, int THREADS, int KPT7>
 __global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src src, uint64_t n, ModArg md, uint32_t nb,
                                                               uint32_t tile_keys, uint32_t ntiles, uint32_t cap,
                                                               uint16_t *__restrict__ regions,
                                                               uint32_t *__restrict__ counts,
-                                                              uint32_t *__restrict__ words) {
+                                                              uint32_t *__restrict__ words, uint32_t ngrp) {
     extern __shared__ uint32_t smem[];
     constexpr uint32_t kPos = (uint32_t)THREADS * KPT7 * 7;  // positions sorted per round
     uint32_t *sorted = smem;
@@ -83,6 +89,8 @@ __global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src sr
     uint32_t *wsum = fill + nb;
     uint32_t *ovf = wsum + 16;
     const uint32_t t = blockIdx.x;
+    // region of bucket b: (b * rstride + rsel) * cap
+    const uint32_t rstride = ngrp ? ngrp : ntiles, rsel = ngrp ? t % ngrp : t;
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
         cursor[b] = 0u;
         fill[b] = 0u;
@@ -198,10 +206,11 @@ __global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src sr
         // Turn fill[b] into the region element index of sorted[0] (mod 2^32), so that sorted[idx]
         // belongs at regions[fill[b] + idx], and flag a run that would overflow its region.
         for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
-            const uint32_t start = b ? cursor[b - 1] : 0u;
-            const uint32_t fb = fill[b];
-            if (fb + (cursor[b] - start) > cap) *ovf = 1u;
-            fill[b] = (b * ntiles + t) * cap + fb - start;
+            const uint32_t start = b ? cursor[b - 1] : 0u, c = cursor[b] - start;
+            const uint32_t reg = b * rstride + rsel;
+            const uint32_t fb = ngrp ? (c ? atomicAdd(&counts[reg], c) : 0u) : fill[b];
+            if (fb + c > cap) *ovf = 1u;
+            fill[b] = reg * cap + fb - start;
         }
         __syncthreads();
         const uint32_t cnt = (uint32_t)(k1 - k0) * md.k;
@@ -216,7 +225,7 @@ __global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src sr
                 const uint32_t p = sorted[idx];
                 const uint32_t b = p >> kBktShift;
                 const uint32_t e = fill[b] + idx;
-                if (e - (b * ntiles + t) * cap < cap)
+                if (e - (b * rstride + rsel) * cap < cap)
                     regions[e] = (uint16_t)p;
                 else
                     __hip_atomic_fetch_or(words + (p >> 5), 1u << (p & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -224,13 +233,14 @@ __global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src sr
         }
         __syncthreads();
         for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
-            fill[b] += cursor[b] - (b * ntiles + t) * cap;  // fill + this round's count
+            fill[b] += cursor[b] - (b * rstride + rsel) * cap;  // fill + this round's count (per-tile regions)
             cursor[b] = 0u;
         }
         if (threadIdx.x == 0) *ovf = 0u;
         __syncthreads();
     }
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) counts[(uint64_t)b * ntiles + t] = min(fill[b], cap);
+    if (!ngrp)
+        for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) counts[(uint64_t)b * ntiles + t] = min(fill[b], cap);
 }
 
 // ---- apply: one workgroup per bucket; stream its ntiles regions (16-B loads, 8 positions per
@@ -243,7 +253,7 @@ __global__ __launch_bounds__(THREADS) void k_bkt_apply(const uint16_t *__restric
     __shared__ uint32_t cnt[kMaxTiles];
     const uint32_t b = blockIdx.x;
     for (uint32_t j = threadIdx.x; j < kBktWords; j += blockDim.x) img[j] = 0u;
-    for (uint32_t t = threadIdx.x; t < ntiles; t += blockDim.x) cnt[t] = counts[(uint64_t)b * ntiles + t];
+    for (uint32_t t = threadIdx.x; t < ntiles; t += blockDim.x) cnt[t] = min(counts[(uint64_t)b * ntiles + t], cap);
     __syncthreads();
     const uint32_t chunks = cap / 8;  // cap is a multiple of 8: regions are 16-B aligned
     const uint32_t pairs = ntiles * chunks;
@@ -275,6 +285,8 @@ __global__ __launch_bounds__(THREADS) void k_bkt_apply(const uint16_t *__restric
 
 struct BktPlan {
     uint32_t nb, tile_keys, ntiles, cap;
+    uint32_t ngrp;     // 0: a region per (bucket, tile); > 0: per (bucket, tile group) (scatter_xcd)
+    uint32_t nregion;  // regions per bucket: ntiles or ngrp
     uint64_t off_regions, off_counts, bytes;
 };
 
@@ -301,16 +313,20 @@ static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k) {
     if (rounds_per_tile < 1) rounds_per_tile = 1;
     p.tile_keys = (uint32_t)(rounds_per_tile * round_keys);
     p.ntiles = (uint32_t)((n + p.tile_keys - 1) / p.tile_keys);
-    // positions of one tile landing in one (full) bucket: mean + 8 sigma + 32, 8-aligned
-    const double mu = (double)p.tile_keys * k * (double)(1u << kBktShift) / (double)m;
+    const uint32_t g = (uint32_t)options().scatter_xcd;
+    p.ngrp = g && p.ntiles >= 4 * g ? g : 0u;
+    p.nregion = p.ngrp ? p.ngrp : p.ntiles;
+    // positions of one region's tiles landing in one (full) bucket: mean + 8 sigma + 32, 8-aligned
+    const double rkeys = p.ngrp ? (double)p.tile_keys * ((p.ntiles + p.ngrp - 1) / p.ngrp) : (double)p.tile_keys;
+    const double mu = rkeys * k * (double)(1u << kBktShift) / (double)m;
     double c = mu + 8.0 * sqrt(mu > 1 ? mu : 1) + 32.0;
-    const double most = (double)p.tile_keys * k;  // never more than every position of the tile
+    const double most = rkeys * k;  // never more than every position of the region's tiles
     if (c > most) c = most;
     p.cap = ((uint32_t)c + 7) & ~7u;
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
     p.off_regions = 0;
-    p.off_counts = al((uint64_t)p.nb * p.ntiles * p.cap * 2);
-    p.bytes = al(p.off_counts + (uint64_t)p.nb * p.ntiles * 4);
+    p.off_counts = al((uint64_t)p.nb * p.nregion * p.cap * 2);
+    p.bytes = al(p.off_counts + (uint64_t)p.nb * p.nregion * 4);
     return p;
 }
 
@@ -339,7 +355,7 @@ static hipError_t run_bucketed(uint64_t n, const ModArg &md, uint32_t *words, vo
         const uint64_t sn = n - k0 < maxk ? n - k0 : maxk;
         const BktPlan p = plan_bucketed(sn, md.m, md.k);
         if (p.bytes > ws_bytes || p.ntiles > kMaxTiles) return hipErrorInvalidValue;
-        if ((uint64_t)p.nb * p.ntiles * p.cap >= (1ull << 31)) return hipErrorInvalidValue;  // u32 region index
+        if ((uint64_t)p.nb * p.nregion * p.cap >= (1ull << 31)) return hipErrorInvalidValue;  // u32 region index
         uint8_t *w = (uint8_t *)ws;
         uint16_t *regions = (uint16_t *)(w + p.off_regions);
         uint32_t *counts = (uint32_t *)(w + p.off_counts);
@@ -355,11 +371,12 @@ static hipError_t run_bucketed(uint64_t n, const ModArg &md, uint32_t *words, vo
                                    : (md.k == 7 ? k_bkt_scatter<S, 7, 1024, 4> : k_bkt_scatter<S, K0, 1024, 4>);
             hipError_t a = hipFuncSetAttribute((const void *)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (a != hipSuccess) return a;
+            if (p.ngrp && (a = hipMemsetAsync(counts, 0, (size_t)p.nb * p.nregion * 4, s)) != hipSuccess) return a;
             hipLaunchKernelGGL(scat, dim3(p.ntiles), dim3(thr), lds, s, src, sn, md, p.nb, p.tile_keys, p.ntiles,
-                               p.cap, regions, counts, words);
+                               p.cap, regions, counts, words, p.ngrp);
             const uint32_t at = options().apply_threads;
             auto apply = at == 1024 ? k_bkt_apply<1024> : at == 512 ? k_bkt_apply<512> : k_bkt_apply<256>;
-            hipLaunchKernelGGL(apply, dim3(p.nb), dim3(at), 0, s, regions, counts, p.ntiles, p.cap, words, nwords);
+            hipLaunchKernelGGL(apply, dim3(p.nb), dim3(at), 0, s, regions, counts, p.nregion, p.cap, words, nwords);
             return hipGetLastError();
         });
         if (e != hipSuccess) return e;

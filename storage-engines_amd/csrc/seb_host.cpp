@@ -136,6 +136,7 @@ static bool set_opt(Options &o, const char *name, int64_t value) {
     else if (!strcmp(name, "apply_threads") && (value == 256 || value == 512 || value == 1024))
         o.apply_threads = (uint32_t)value;
     else if (!strcmp(name, "clear_kernel") && (value == 0 || value == 1)) o.clear_kernel = (int)value;
+    else if (!strcmp(name, "scatter_xcd") && (value == 0 || value == 8 || value == 16 || value == 32)) o.scatter_xcd = (int)value;
     else if (!strcmp(name, "varlen_prehash_packed") && (value == 0 || value == 1))
         o.varlen_prehash_packed = (int)value;
     else if (!strcmp(name, "build_prepack") && (value == 0 || value == 1)) o.build_prepack = (int)value;
@@ -157,7 +158,7 @@ static const char *const kOptionNames[] = {
     "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
     "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
     "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order",
-    "lds_min_keys", "probe_phase_grid", "clear_kernel"};
+    "lds_min_keys", "probe_phase_grid", "clear_kernel", "scatter_xcd"};
 
 static std::once_flag g_env_once;
 static void load_env() {
@@ -210,6 +211,7 @@ extern "C" int seb_get_option(const char *name, int64_t *value) {
     else if (!strcmp(name, "build_prepack")) *value = o.build_prepack;
     else if (!strcmp(name, "apply_threads")) *value = o.apply_threads;
     else if (!strcmp(name, "clear_kernel")) *value = o.clear_kernel;
+    else if (!strcmp(name, "scatter_xcd")) *value = o.scatter_xcd;
     else if (!strcmp(name, "wal_lds_kib")) *value = o.wal_lds_kib;
     else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
     else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;

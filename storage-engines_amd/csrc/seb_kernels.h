@@ -106,6 +106,7 @@ struct Options {
     uint32_t varlen_hash_win = 64;    // pre-hash LDS window bytes per key (48 .. 80)
     uint32_t apply_threads = 1024;    // radix-partitioned build: apply workgroup size (256, 512, 1024)
     int clear_kernel = 1;             // seb_dev_clear: 16-B store kernel (1) or hipMemsetAsync (0)
+    int scatter_xcd = 0;              // bucketed build: regions per (bucket, tile group of this size; 8 = per XCD), 0 = per tile
     int varlen_prehash_packed = 1;    // pre-hash to packed residues where k == 7, m < 2^29 (0/1)
     int build_prepack = 0;            // fixed-width bucketed build: pack residues first (full-occupancy hash), 0/1
     int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)

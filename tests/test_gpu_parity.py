@@ -165,15 +165,18 @@ def test_host_api_chunked_pipeline(seb, monkeypatch, torch_cuda):
 
 # --------------------------------------------------------- device-resident API --------------
 
-@pytest.fixture(params=[(1, 1024, 4, 1024, 0), (2, 1024, 4, 256, 0), (2, 512, 4, 512, 0), (2, 1024, 5, 1024, 0),
-                        (2, 1024, 5, 1024, 1), (3, 1024, 5, 1024, 0)],
-                ids=["atomic", "bucketed", "bucketed512", "bucketed-kpt5", "bucketed-prepack", "lds"])
+@pytest.fixture(params=[(1, 1024, 4, 1024, 0, 0), (2, 1024, 4, 256, 0, 0), (2, 512, 4, 512, 0, 0),
+                        (2, 1024, 5, 1024, 0, 0), (2, 1024, 5, 1024, 1, 0), (3, 1024, 5, 1024, 0, 0),
+                        (2, 1024, 5, 1024, 0, 8), (2, 512, 4, 256, 1, 16)],
+                ids=["atomic", "bucketed", "bucketed512", "bucketed-kpt5", "bucketed-prepack", "lds",
+                     "bucketed-xcd8", "bucketed512-prepack-grp16"])
 def build_algo(request, seb):
-    """Build paths: device-scope atomics, radix-partitioned (several geometries), and the
-    LDS-resident filter (algo 3; a filter over 160 KiB falls back to atomics)."""
-    algo, thr, kpt, apply, prepack = request.param
+    """Build paths: device-scope atomics, radix-partitioned (several geometries, regions per tile
+    or per tile group), and the LDS-resident filter (algo 3; a filter over 160 KiB falls back to
+    atomics)."""
+    algo, thr, kpt, apply, prepack, grp = request.param
     with seb.option("build_algo", algo), seb.option("scatter_threads", thr), seb.option("scatter_kpt", kpt), \
-            seb.option("apply_threads", apply), seb.option("build_prepack", prepack):
+            seb.option("apply_threads", apply), seb.option("build_prepack", prepack), seb.option("scatter_xcd", grp):
         yield algo
 
 
@@ -1334,8 +1337,9 @@ def test_registry_full_capacity(seb, torch_cuda, multiget_group):
     reg.close()
 
 
+@pytest.mark.parametrize("grp", [0, 8])
 @pytest.mark.parametrize("case", ["duplicates", "skewed", "large_m"])
-def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
+def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case, grp):
     """Radix-partitioned build paths a hash-distributed batch never takes: runs that overflow
     their fixed-capacity region (identical keys put a tile's positions into 7 buckets; skewed: a
     few distinct keys repeated) fall back to device-scope atomic OR, and a filter with more
@@ -1343,6 +1347,7 @@ def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
     The bit array must equal the oracle's either way."""
     torch = torch_cuda
     seb.set_option("build_algo", 2)
+    seb.set_option("scatter_xcd", grp)  # regions per tile, or per group of 8 tiles (shared claims)
     try:
         rng = np.random.default_rng(5)
         if case == "duplicates":
@@ -1361,6 +1366,7 @@ def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
         assert np.array_equal(bits, ref)
     finally:
         seb.set_option("build_algo", 0)
+        seb.set_option("scatter_xcd", 0)
 
 
 # ------------------------------------------------ sharded build of one filter (§8(e)) ----
