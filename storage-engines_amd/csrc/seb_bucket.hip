@@ -218,7 +218,11 @@ __global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src sr
 #pragma unroll 5
             for (uint32_t idx = threadIdx.x; idx < cnt; idx += blockDim.x) {
                 const uint32_t p = sorted[idx];
+#ifdef SEB_DIAG_SCATTER_NT  // diagnostic builds (tools/diag_lib.sh): streaming stores for the runs
+                __builtin_nontemporal_store((uint16_t)p, regions + fill[p >> kBktShift] + idx);
+#else
                 regions[fill[p >> kBktShift] + idx] = (uint16_t)p;
+#endif
             }
         } else {
             for (uint32_t idx = threadIdx.x; idx < cnt; idx += blockDim.x) {
@@ -263,7 +267,13 @@ __global__ __launch_bounds__(THREADS) void k_bkt_apply(const uint16_t *__restric
         const uint32_t t = q / chunks, c = q - t * chunks;
         const uint32_t valid = cnt[t];
         if (c * 8 < valid) {
+#ifdef SEB_DIAG_APPLY_NT  // diagnostic builds: streaming loads of the runs
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 vv = __builtin_nontemporal_load((const u32x4 *)(reg + q));
+            const uint4 v = make_uint4(vv.x, vv.y, vv.z, vv.w);
+#else
             const uint4 v = reg[q];
+#endif
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (uint32_t e = 0; e < 8; ++e)
