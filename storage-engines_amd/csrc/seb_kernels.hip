@@ -404,6 +404,9 @@ __global__ __launch_bounds__(256) void k_probe_phase0(Src src, uint64_t n, const
                                             packed + i);
             }
         }
+#ifdef SEB_DIAG_GATHER_PRIO  // diagnostic builds: the dependent gather chain issues ahead of hashing waves
+        __builtin_amdgcn_s_setprio(3);
+#endif
 #pragma unroll
         for (int r = 0; r < KPT; ++r)
 #pragma unroll
@@ -411,6 +414,9 @@ __global__ __launch_bounds__(256) void k_probe_phase0(Src src, uint64_t n, const
                 const uint32_t w = pos[r][q] >> 5;
                 if ((acc[r] & 1u) && w < hi) acc[r] &= words[w] >> (pos[r][q] & 31);
             }
+#ifdef SEB_DIAG_GATHER_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
 #pragma unroll
         for (int r = 0; r < KPT; ++r) {
             const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
