@@ -376,8 +376,11 @@ __global__ __launch_bounds__(256) void k_probe_sliced_emit(Src src, uint64_t n, 
 // while the key's bits so far are all set (MODE 0's early exit; sampling liveness once per phase
 // so a key's gathers overlap was measured slower: more gathers).  The answer is the AND of the k
 // bits, as MayContain (lsm/bloom.go:82-92) returns.
+#ifndef SEB_PHASE_BLOCK  // diagnostic builds may change the phased probe's workgroup size
+#define SEB_PHASE_BLOCK 256
+#endif
 template <typename Src, int KPT>
-__global__ __launch_bounds__(256) void k_probe_phase0(Src src, uint64_t n, const uint32_t *__restrict__ words,
+__global__ __launch_bounds__(SEB_PHASE_BLOCK) void k_probe_phase0(Src src, uint64_t n, const uint32_t *__restrict__ words,
                                                       ModArg md, uint8_t *__restrict__ out,
                                                       uint64_t *__restrict__ packed, uint32_t hi) {
     const uint64_t span = (uint64_t)blockDim.x * KPT;
@@ -429,7 +432,7 @@ __global__ __launch_bounds__(256) void k_probe_phase0(Src src, uint64_t n, const
 // loads of packed words); `out` is 4-byte aligned (the host checks).  PMAJOR: walk the 7
 // positions of the 4 keys position-major (4 independent gathers per step) instead of key by key.
 template <bool PMAJOR>
-__global__ __launch_bounds__(256) void k_probe_phase(const uint64_t *__restrict__ packed, uint64_t n,
+__global__ __launch_bounds__(SEB_PHASE_BLOCK) void k_probe_phase(const uint64_t *__restrict__ packed, uint64_t n,
                                                      const uint32_t *__restrict__ words, ModArg md,
                                                      uint8_t *__restrict__ out, uint32_t lo, uint32_t hi,
                                                      uint32_t first) {
@@ -1238,24 +1241,24 @@ hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *w
     }
     if (kb) {
         const uint32_t kpt0 = o.probe_phase0_kpt == 1 || o.probe_phase0_kpt == 4 ? (uint32_t)o.probe_phase0_kpt : 2u;
-        const unsigned g0 = grid_for((n + kpt0 - 1) / kpt0, 256, o.grid_cap);
+        const unsigned g0 = grid_for((n + kpt0 - 1) / kpt0, SEB_PHASE_BLOCK, o.grid_cap);
         e = with_src(*kb, [&](auto src) {
             using S = decltype(src);
             auto k0 = kpt0 == 1 ? k_probe_phase0<S, 1> : kpt0 == 4 ? k_probe_phase0<S, 4> : k_probe_phase0<S, 2>;
-            hipLaunchKernelGGL(k0, dim3(g0), dim3(256), 0, s, src, n, words, md, out, packed, bound(1));
+            hipLaunchKernelGGL(k0, dim3(g0), dim3(SEB_PHASE_BLOCK), 0, s, src, n, words, md, out, packed, bound(1));
             return hipGetLastError();
         });
         if (e != hipSuccess) return e;
         p0 = 1;
     }
-    const unsigned g = grid_for((n + 3) / 4, 256, o.probe_phase_grid ? o.probe_phase_grid : o.grid_cap);
+    const unsigned g = grid_for((n + 3) / 4, SEB_PHASE_BLOCK, o.probe_phase_grid ? o.probe_phase_grid : o.grid_cap);
     for (uint64_t p = p0; p < np; ++p) {
         const uint32_t first = p == 0 ? 1u : 0u;
         if (o.probe_kpt == 4)
-            hipLaunchKernelGGL(k_probe_phase<true>, dim3(g), dim3(256), 0, s, packed, n, words, md, out, bound(p),
+            hipLaunchKernelGGL(k_probe_phase<true>, dim3(g), dim3(SEB_PHASE_BLOCK), 0, s, packed, n, words, md, out, bound(p),
                                bound(p + 1), first);
         else
-            hipLaunchKernelGGL(k_probe_phase<false>, dim3(g), dim3(256), 0, s, packed, n, words, md, out, bound(p),
+            hipLaunchKernelGGL(k_probe_phase<false>, dim3(g), dim3(SEB_PHASE_BLOCK), 0, s, packed, n, words, md, out, bound(p),
                                bound(p + 1), first);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
