@@ -1,7 +1,10 @@
 """Bloom build + probe benchmark (BASELINE.json metric), one process per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2c3|c4|c5|...]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...   (RCCL over xGMI)
+
+`--gpus N` with N > 1 and no launcher environment spawns the N rank processes itself
+(launch_ranks: the parent never touches the GPU); under torchrun WORLD_SIZE must equal --gpus.
 
 c2c3 (default, the metric's config): one step on every GPU = clear + build one SSTable filter
 from 10M x 16-B keys @1% FPR (BASELINE C2; m = 95,850,584, k = 7) and probe a 10M-key batch
@@ -76,7 +79,11 @@ def sha(b) -> str:
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default 1, or WORLD_SIZE under a launcher); N > 1 without a "
+                         "launcher spawns the N rank processes itself (launch_ranks)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="spawn/join the ranks and check the process group only (gloo, no GPU); CPU tests")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--time-every", type=int, default=4,
                     help="record the build/probe launch timers on every Nth timed step (and the last)")
@@ -145,7 +152,8 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
     # Every rank still tests all 10M keys against its own filter in every step.
     packed = world > 1 and args.bcast == "packed" and k == 7 and m < (1 << 29)
     st.workload = ("C2+C3: per GPU build one filter from 10M x 16B keys @1% FPR (m=95,850,584, k=7) "
-                   "+ probe a 10M-key batch (50% present) RCCL-broadcast from rank 0")
+                   "+ probe a 10M-key batch (50% present)" +
+                   (", RCCL-broadcast from rank 0" if world > 1 else ", resident in HBM (one GPU: no broadcast)"))
     if packed:
         st.bcast_lead = 2
         st.packed = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(st.bcast_lead + 1)]
@@ -156,7 +164,8 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
         st.bcast_prologue = lambda b, buf: seb.dev_pack_residues(st.pk[0], m, k, buf)
     else:
         st.broadcast_bufs = st.pbufs if world > 1 else None
-    st.parallelism = f"filter-per-gpu x{world}, probe batch broadcast (RCCL)"
+    st.parallelism = (f"filter-per-gpu x{world}, probe batch broadcast (RCCL)" if world > 1
+                      else "filter-per-gpu x1")
 
     def build(j):
         w = st.wbufs[j % len(st.wbufs)]
@@ -550,25 +559,117 @@ def setup_wal(args, seb, kg, torch, dev, rank, world, dist):
     return st
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(world: int, port: int, base=None) -> list:
+    """The environment of each of `world` rank processes on this node, as torchrun sets it."""
+    base = dict(os.environ if base is None else base)
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL needs it)
+    envs = []
+    for r in range(world):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(args, argv) -> int:
+    """`bench.py --gpus N` (N > 1) run directly: this process is only the launcher.  It never
+    initialises the GPU (torch.cuda.device_count() does not, on this image), checks that the node
+    has N GPUs for the RCCL backend, then starts N child processes of this same script, one per
+    GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N), and exits with the first failing child's status.
+    Rank 0 prints the JSON line.  gloo (a rehearsal) may put several ranks on one GPU."""
+    import subprocess
+
+    n = args.gpus
+    if not args.launch_check:
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < 1 or (args.dist_backend == "nccl" and have < n):
+            print(f"bench.py: --gpus {n} needs {n} GPUs for the {args.dist_backend} backend; this node has {have}",
+                  file=sys.stderr)
+            return 3
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=e)
+             for e in rank_envs(n, free_port())]
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                r = p.poll()
+                if r is None:
+                    continue
+                live.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in live:  # a rank that failed leaves its peers blocked in a collective
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
+def launch_check(args, world, rank):
+    """--launch-check: the rank processes' group as the bench forms it, on gloo and without a GPU."""
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    assert dist.get_world_size() == world and dist.get_rank() == rank
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": dist.get_world_size(), "rank_sum": int(t.item()),
+                          "master": f"{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}"}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    in_launcher = "WORLD_SIZE" in os.environ
+    if not in_launcher and args.gpus is not None and args.gpus > 1:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if args.launch_check:
+        launch_check(args, world, rank)
+        return
+
     import torch
     import torch.distributed as dist
 
     import keygen as kg
     import seb_bloom as seb
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dev = torch.device("cuda", local % torch.cuda.device_count())
+        if args.dist_backend == "nccl" and ndev < world:
+            print(f"bench.py: rank {rank}: {world} RCCL ranks need {world} GPUs; {ndev} visible", file=sys.stderr)
+            sys.exit(3)
+        dev = torch.device("cuda", local % ndev)
         torch.cuda.set_device(dev)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
     else:
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
@@ -697,7 +798,7 @@ def main():
             "metric": METRIC if args.config in ("c2c3", "c4", "c5", "lsm", "lsm_wide", "c2_sharded",
                                                              "c3_partitioned")
             else f"{args.config} {st.unit}",
-            "value": round(value, 2), "unit": st.unit, "n_gpus": world,
+            "value": round(value, 2), "unit": st.unit, "n_gpus": world, "devices": min(world, ndev),
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),
             "higher_is_better": True, "scaling": st.scaling, "vs_baseline": None, "dtype": st.dtype,
             "data": "synthetic (reference key format user%010d+2B, common/benchmark/keygen.go:89-109)",
@@ -718,13 +819,13 @@ def main():
         if args.config == "c2c3":
             # SURVEY.md 8(d)'s secondary sector model: every bit touch one 64-B DRAM transaction (no
             # early exit), the build also writing each touched sector back.  Most touches are L2 hits
-            # here (phased probe, bucketed build), so this can exceed the HBM peak; DESIGN.md 6.
+            # here (phased probe, bucketed build), so these rates exceed the HBM peak and are not a
+            # fraction of it; the probe's bound is the gather model below.
             spk = {"build": 16 + 2 * 64 * st.k, "probe": 16 + 64 * st.k}
             result["roofline"]["sector_model"] = {
                 "S": 64, "bytes_per_key": spk,
                 "GB/s": {d: round(st.n * spk[d] / (kern_ms[d] * 1e-3) / 1e9, 1) for d in spk if d in kern_ms},
-                "frac": {d: round(st.n * spk[d] / (kern_ms[d] * 1e-3) / 1e9 / PEAK_HBM_GBS, 3) for d in spk
-                         if d in kern_ms}}
+                "note": "modelled bytes, most of them L2 hits; not comparable to the HBM peak"}
             # The probe's real bound: filter-word gathers, counted offline per call
             # with the oracle (tools/gather_count.py), against the measured L2-resident ceiling.
             gpath = os.path.join(ROOT, "profiles", "gathers_c2c3.json")
@@ -826,7 +927,7 @@ def cpu_baseline(args, n, m, k):
     except OSError:
         pass
     res = {"value": round(2.0 * sample / (t2 - t0) / 1e6, 3), "unit": "Mkeys/s", "cores": args.cpu_threads,
-           "kind": "port",
+           "host_cpus": os.cpu_count(), "kind": "port",
            "sample": f"{sample} build + {sample} probe keys ({args.config}), oracle/bloom_oracle.c "
                      f"(C restatement of lsm/bloom.go; Go toolchain absent), {args.cpu_threads} thread(s), {model}",
            "build_mkeys_s": round(sample / (t1 - t0) / 1e6, 3), "probe_mkeys_s": round(sample / (t2 - t1) / 1e6, 3)}

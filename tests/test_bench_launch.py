@@ -1,0 +1,68 @@
+"""bench.py's rank launcher (`--gpus N` without torchrun): the driver runs `bench.py --gpus N`, so
+the script itself must start N rank processes and report n_gpus = N.
+CPU only: --launch-check forms the process group on gloo without touching a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**extra):
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    e.update(extra)
+    return e
+
+
+def _run(args, env=None, timeout=120):
+    return subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout,
+                          env=env or _env())
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_n_spawns_n_ranks(n):
+    r = _run(["--gpus", str(n), "--launch-check"])
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 alone prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n
+    assert d["rank_sum"] == n * (n + 1) // 2
+    assert d["master"].startswith("127.0.0.1:")
+
+
+def test_world_size_must_match_gpus():
+    r = _run(["--gpus", "2", "--launch-check"], env=_env(WORLD_SIZE="3", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode == 2
+    assert "WORLD_SIZE=3" in r.stderr
+
+
+def test_rccl_needs_n_gpus(monkeypatch):
+    import importlib.util
+
+    import torch
+
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    args = type("A", (), {"gpus": 4, "launch_check": False, "dist_backend": "nccl"})()
+    assert bench.launch_ranks(args, []) == 3  # refuses before starting any rank
+
+
+def test_rank_envs():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    envs = bench.rank_envs(4, 12345, base={"X": "1"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert all(e["WORLD_SIZE"] == "4" and e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "12345"
+               and e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e["X"] == "1" for e in envs)
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
