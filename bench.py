@@ -89,7 +89,7 @@ def parse():
                     help="record the build/probe launch timers on every Nth timed step (and the last)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "lsm", "lsm_wide", "route", "wal",
-                                                           "many", "c2_sharded", "c3_partitioned"])
+                                                           "many", "c2_sharded", "c3_partitioned", "flush"])
     ap.add_argument("--keys", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
@@ -637,8 +637,80 @@ def launch_check(args, world, rank):
     dist.destroy_process_group()
 
 
+def run_flush(args):
+    """--config flush: the drop-in ABI (include/seb_bloom.h's Go API mirror) at the sizes the
+    unchanged callers use, through harness/flush_bench.c, which calls it as the cgo shim would:
+    New -> Add per key -> Encode for a memtable flush (expectedKeys = len(entries), lsm/lsm.go:356;
+    ~50K) and a compaction output file (100000, lsm/compaction.go:286), both through
+    lsm/sstable_builder.go:30,53,217; then Decode -> single-key MayContain (lsm/sstable.go:129,206)
+    on 1 and 8 threads at once on one filter.  Host memory in, host memory out: every number
+    includes the arena, the H2D copy, the build launch and the D2H copy.  value = flush-size
+    filter builds, in keys per second end to end.  The oracle's C restatement is timed beside each
+    (cpu_baseline), and every digest is checked against it."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "storage-engines_amd", "lib", "flush_bench")
+    sizes = [50_000, 100_000]
+    threads = 8
+    out = subprocess.run([exe, "--reps", str(max(3, args.steps)), "--threads", str(threads), *map(str, sizes)],
+                         capture_output=True, text=True, timeout=600)
+    if out.returncode != 0:
+        print(out.stdout + out.stderr, file=sys.stderr)
+        sys.exit(out.returncode or 1)
+    res = json.loads(out.stdout)
+    by_n = {r["n"]: r for r in res["sizes"]}
+    flush = by_n[50_000]
+    result = {
+        "metric": "drop-in ABI flush build: New+Add x n+Encode keys/s (n=50K, host memory in and out)",
+        "value": round(flush["build_keys_per_s"] / 1e6, 3), "unit": "Mkeys/s", "n_gpus": 1,
+        "steps": max(3, args.steps), "warmup": 1, "ms_per_step": round(flush["build_us"]["total"] / 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (reference key format user%010d+2B, common/benchmark/keygen.go:89-109)",
+        "config": {"workload": "SSTableBuilder bloom at flush (50K keys) and compaction (100K keys) size, "
+                               "then per-Get single-key MayContain on 1 and 8 threads (harness/flush_bench.c)",
+                   "sizes": sizes, "threads": threads, "fpr": 0.01},
+        "sizes": res["sizes"],
+    }
+    if not args.no_cpu_baseline:
+        from oracle import oracle_c as oc
+
+        import keygen as kg
+
+        cpu, parity = {}, []
+        for n in sizes:
+            m, k = oc.params(n, 0.01)
+            bk, pk = kg.key16(np.arange(n)), kg.key16(kg.probe_indices(n))
+            tb, tp = [], []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                bits = oc.build(m, k, bk, n, stride=16)
+                t1 = time.perf_counter()
+                ans = oc.probe(bits, m, k, pk, n, stride=16)
+                t2 = time.perf_counter()
+                tb.append(t1 - t0)
+                tp.append(t2 - t1)
+            enc = m.to_bytes(8, "little") + k.to_bytes(4, "little") + bits.tobytes()
+            r = by_n[n]
+            parity.append(sha(enc) == r["encode_sha256"] and sha(ans.tobytes()) == r["probe_sha256"])
+            cpu[str(n)] = {"build_us": round(np.median(tb) * 1e6, 2),
+                           "build_keys_per_s": round(n / np.median(tb)),
+                           "may_contain_ns_per_key": round(np.median(tp) * 1e9 / n, 2)}
+        result["parity"] = ("bit-exact (Encode() and the single-key answers equal the oracle's at 50K and 100K)"
+                            if all(parity) else f"MISMATCH {parity}")
+        result["cpu_baseline"] = {
+            "value": round(cpu["50000"]["build_keys_per_s"] / 1e6, 3), "unit": "Mkeys/s", "cores": 1,
+            "host_cpus": os.cpu_count(), "kind": "port",
+            "sample": "oracle/bloom_oracle.c (C restatement of lsm/bloom.go; Go toolchain absent), 1 thread: "
+                      "build of the same 50K and 100K keys (no Encode copy) and MayContain per key",
+            "per_size": cpu}
+    print(json.dumps(result), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == "flush":
+        run_flush(args)
+        return
     in_launcher = "WORLD_SIZE" in os.environ
     if not in_launcher and args.gpus is not None and args.gpus > 1:
         sys.exit(launch_ranks(args, sys.argv[1:]))

@@ -1087,6 +1087,14 @@ struct CtxLease {  // borrow a context from the process pool (concurrent filters
     }
 };
 
+// A filter handle.  Writers (Add, flush, Encode's host sync) hold `mu`.  A single-key MayContain
+// does not: once the host copy reflects every Add (no pending keys, host_ok) and the filter is
+// usable, `readable` is published (release) and MayContain answers from `host` with no lock, as
+// the reference's MayContain runs lock-free from many goroutines (lsm/lsm.go:166 drops the RLock
+// before the SSTable loop).  `host` is sized once, at New/Decode, and never reallocated, so a
+// reader can never see freed memory; a reader racing an Add on the same filter sees bits of
+// either state, which is the reference's own contract (an unsynchronised Go Add/MayContain pair
+// is a data race there).
 struct seb_filter {
     std::mutex mu;
     uint64_t m = 0;
@@ -1095,12 +1103,50 @@ struct seb_filter {
     int device = 0;
     uint32_t *dwords = nullptr;  // HBM copy, authoritative once allocated
     uint64_t dbytes = 0;
-    std::vector<uint8_t> host;  // host copy (valid when host_ok)
+    std::vector<uint8_t> host;  // host copy (valid when host_ok); nbytes long for the handle's life
     bool host_ok = true;
+    std::atomic<bool> readable{false};  // host_ok, nothing pending, usable: lock-free MayContain
     std::vector<uint8_t> pend;       // deferred Add arena
     std::vector<uint64_t> pend_off;  // n+1 offsets into pend
     uint64_t pend_cap = 64ull << 20;
 };
+
+static bool usable_quiet(const seb_filter *f) {
+    return f->m != 0 && f->k <= 4096 && f->nbytes >= seb_num_bytes(f->m);
+}
+
+static void publish_locked(seb_filter *f) {
+    f->readable.store(f->host_ok && f->pend_off.size() <= 1 && usable_quiet(f), std::memory_order_release);
+}
+
+// lsm/bloom.go:82-92 for one key on the host copy: hash1 = FNV-1a 64, hash2 = FNV-1 64
+// (:44-54), positions (h1 + i*h2) mod m with u64 wraparound (:58-67), LSB-first bit test
+// (:87), false at the first clear bit.  The positions are stepped incrementally: with
+// r = (h1 + i*h2) mod m and b = h2 mod m, the next residue is r + b mod m, less 2^64 mod m when
+// the u64 sum h1 + (i+1)*h2 wrapped: two divisions per key instead of k.
+static int host_may_contain(const uint8_t *bits, uint64_t m, uint32_t k, const uint8_t *key, uint64_t len) {
+    uint64_t h1 = 0xcbf29ce484222325ull, h2 = 0xcbf29ce484222325ull;
+    const uint64_t P = 0x100000001b3ull;
+    for (uint64_t i = 0; i < len; ++i) {
+        h1 = (h1 ^ key[i]) * P;
+        h2 = (h2 * P) ^ key[i];
+    }
+    if (k == 0) return 1;  // no positions: the reference's loop never returns false
+    uint64_t r = h1 % m;
+    const uint64_t b = h2 % m, c = (0 - m) % m;  // 2^64 mod m
+    uint64_t s = h1;
+    for (uint32_t i = 0;;) {
+        if (!(bits[r >> 3] & (1u << (r & 7)))) return 0;
+        if (++i >= k) return 1;
+        const uint64_t s2 = s + h2;
+        const bool wrap = s2 < s;
+        s = s2;
+        uint64_t t = r + b;
+        if (t < r || t >= m) t -= m;  // r, b < m: one subtract, also when r + b overflowed
+        if (wrap) t = t >= c ? t - c : t + (m - c);
+        r = t;
+    }
+}
 
 static int ensure_device_copy(seb_filter *f) {
     if (f->dwords) return SEB_OK;
@@ -1137,11 +1183,12 @@ static int flush_locked(seb_filter *f) {
     seb_keys kb{f->pend.data(), f->pend_off.data(), f->pend_off.size() - 1, 0, 0};
     std::lock_guard<std::mutex> g(L.c->mu);
     HIP_OR_FAIL(hipSetDevice(f->device));
+    f->host_ok = false;  // the device copy is about to move ahead of the host copy
+    f->readable.store(false, std::memory_order_relaxed);
     if ((rc = build_device_from_host(L.c, &kb, f->dwords, mod_arg(f->m, f->k)))) return rc;
     HIP_OR_FAIL(hipStreamSynchronize(L.c->s_comp));
     f->pend.clear();
     f->pend_off.assign(1, 0);
-    f->host_ok = false;
     return SEB_OK;
 }
 
@@ -1157,6 +1204,7 @@ extern "C" seb_filter *seb_filter_new(int64_t n, double p) {
     f->device = default_device();
     f->host.assign(f->nbytes, 0);
     f->pend_off.assign(1, 0);
+    publish_locked(f);  // an empty filter answers false everywhere
     long cap;
     if (env_flag("SEB_PENDING_CAP", &cap) && cap > 0) f->pend_cap = (uint64_t)cap;
     return f;
@@ -1176,6 +1224,7 @@ extern "C" int seb_filter_add(seb_filter *f, const uint8_t *key, uint64_t len) {
     std::lock_guard<std::mutex> g(f->mu);
     int rc = usable(f, "BloomFilter.Add");
     if (rc) return rc;
+    f->readable.store(false, std::memory_order_relaxed);  // pending keys: MayContain must flush first
     f->pend.insert(f->pend.end(), key, key + len);
     f->pend_off.push_back(f->pend.size());
     if (f->pend.size() >= f->pend_cap) return flush_locked(f);
@@ -1194,9 +1243,10 @@ extern "C" int seb_filter_add_batch(seb_filter *f, const seb_keys *kb) {
     if (L.rc) return L.rc;
     std::lock_guard<std::mutex> g2(L.c->mu);
     HIP_OR_FAIL(hipSetDevice(f->device));
+    f->readable.store(false, std::memory_order_relaxed);
+    f->host_ok = false;
     if ((rc = build_device_from_host(L.c, kb, f->dwords, mod_arg(f->m, f->k)))) return rc;
     HIP_OR_FAIL(hipStreamSynchronize(L.c->s_comp));
-    f->host_ok = false;
     return SEB_OK;
 }
 
@@ -1218,22 +1268,31 @@ extern "C" int seb_filter_may_contain_batch(seb_filter *f, const seb_keys *kb, u
     return probe_device_to_host(L.c, kb, f->dwords, mod_arg(f->m, f->k), out);
 }
 
+static int sync_host_locked(seb_filter *f);
+
+// MayContain(key) (lsm/bloom.go:82-92), called once per Get per candidate SSTable
+// (lsm/sstable.go:206): answered on the host copy, lock-free once the filter is readable.  A GPU
+// launch costs microseconds against ~100 ns for this; batches go to the GPU
+// (seb_filter_may_contain_batch).
 extern "C" int seb_filter_may_contain(seb_filter *f, const uint8_t *key, uint64_t len) {
+    if (!f) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: null filter");
     if (!key && len) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: null key");
-    static const uint8_t empty = 0;
-    seb_keys kb{key ? key : &empty, nullptr, 1, (uint32_t)len, 0};
-    if (len > 0xffffffffull) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: key too long");
-    uint8_t ans = 0;
-    int rc = seb_filter_may_contain_batch(f, &kb, &ans);
-    return rc ? rc : (int)ans;
+    if (!f->readable.load(std::memory_order_acquire)) {
+        std::lock_guard<std::mutex> g(f->mu);
+        int rc;
+        if ((rc = usable(f, "BloomFilter.MayContain")) || (rc = flush_locked(f)) || (rc = sync_host_locked(f)))
+            return rc;
+        publish_locked(f);
+    }
+    return host_may_contain(f->host.data(), f->m, f->k, key, len);
 }
 
 static int sync_host_locked(seb_filter *f) {
     if (f->host_ok) return SEB_OK;
     HIP_OR_FAIL(hipSetDevice(f->device));
-    f->host.resize(f->nbytes);
     if (f->nbytes) HIP_OR_FAIL(hipMemcpy(f->host.data(), f->dwords, f->nbytes, hipMemcpyDeviceToHost));
     f->host_ok = true;
+    publish_locked(f);
     return SEB_OK;
 }
 
@@ -1264,6 +1323,7 @@ extern "C" seb_filter *seb_filter_decode(const uint8_t *data, uint64_t len) {
     f->device = default_device();
     f->host.assign(data + 12, data + len);
     f->pend_off.assign(1, 0);
+    publish_locked(f);  // immutable from here unless Add is called on it
     return f;
 }
 

@@ -1,0 +1,199 @@
+/*
+ * flush_bench.c — times the drop-in ABI at the sizes the unchanged Go callers use, calling it the
+ * way the cgo shim would (one C call per Go method call):
+ *
+ *   build   lsm/sstable_builder.go:30   NewBloomFilter(expectedKeys, 0.01)
+ *           lsm/sstable_builder.go:53   Add(key) per sorted entry
+ *           lsm/sstable_builder.go:217  Encode() at Finish
+ *           sizes: a memtable flush, expectedKeys = len(entries) (lsm/lsm.go:356, ~50K for a 4 MB
+ *           memtable of 16-B keys + 64-B values), and a compaction output file, expectedKeys =
+ *           100000 (lsm/compaction.go:286)
+ *   probe   lsm/sstable.go:129          DecodeBloomFilter(bloomData) at open
+ *           lsm/sstable.go:206          MayContain(key) per Get, from T threads at once on one
+ *                                       filter (lsm/lsm.go:166 releases the RLock before the loop)
+ *
+ * usage: flush_bench [--reps R] [--threads T] N...
+ * Prints one JSON line: per N, median microseconds of New / Add loop / Encode / Free, sha256 of
+ * Encode(), single-key MayContain ns per call on 1 and T threads, and the batched GPU MayContain.
+ * Keys are key16(i) (common/benchmark/keygen.go:89-109); probes q < N: even q -> key16(q), odd
+ * q -> key16(N + q).  Test/bench infrastructure; the cgo crossing itself (tens of ns per call in
+ * Go) is not included.
+ */
+#define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
+#include <stdlib.h>
+#include <time.h>
+
+#include "../../include/seb_bloom.h"
+#include "harness_common.h"
+
+static double now_us(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec * 1e6 + (double)t.tv_nsec * 1e-3;
+}
+
+static void die(const char *what) {
+    fprintf(stderr, "%s: %s\n", what, seb_last_error());
+    exit(2);
+}
+
+static int cmp_d(const void *a, const void *b) {
+    double x = *(const double *)a, y = *(const double *)b;
+    return (x > y) - (x < y);
+}
+
+static double median(double *v, int n) {
+    qsort(v, (size_t)n, sizeof *v, cmp_d);
+    return n % 2 ? v[n / 2] : 0.5 * (v[n / 2 - 1] + v[n / 2]);
+}
+
+typedef struct {
+    seb_filter *f;
+    const uint8_t *keys;
+    uint64_t n, start, calls;
+    uint8_t *ans;  /* per key answers (thread 0 only) */
+    uint64_t positives;
+    pthread_barrier_t *bar;
+    double us;
+} reader_arg;
+
+static void *reader(void *p) {
+    reader_arg *a = (reader_arg *)p;
+    pthread_barrier_wait(a->bar);
+    double t0 = now_us();
+    uint64_t pos = 0;
+    for (uint64_t c = 0; c < a->calls; c++) {
+        uint64_t q = (a->start + c) % a->n;
+        int r = seb_filter_may_contain(a->f, a->keys + 16 * q, 16);
+        if (r < 0) die("MayContain");
+        pos += (uint64_t)r;
+        if (a->ans) a->ans[q] = (uint8_t)r;
+    }
+    a->us = now_us() - t0;
+    a->positives = pos;
+    return NULL;
+}
+
+/* T threads each make `calls` MayContain calls on one filter; returns aggregate calls per second. */
+static double run_readers(seb_filter *f, const uint8_t *keys, uint64_t n, int T, uint64_t calls, uint8_t *ans,
+                          double *ns_per_call) {
+    pthread_t th[64];
+    reader_arg args[64];
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, (unsigned)T);
+    for (int t = 0; t < T; t++) {
+        args[t] = (reader_arg){f, keys, n, (uint64_t)t * (n / (uint64_t)T), calls, t == 0 ? ans : NULL, 0, &bar, 0};
+        pthread_create(&th[t], NULL, reader, &args[t]);
+    }
+    double worst = 0, sum = 0;
+    for (int t = 0; t < T; t++) {
+        pthread_join(th[t], NULL);
+        if (args[t].us > worst) worst = args[t].us;
+        sum += args[t].us;
+    }
+    pthread_barrier_destroy(&bar);
+    *ns_per_call = sum * 1e3 / ((double)T * (double)calls);
+    return (double)T * (double)calls / (worst * 1e-6);
+}
+
+int main(int argc, char **argv) {
+    int reps = 7, threads = 8;
+    uint64_t ns[16];
+    int nn = 0;
+    for (int i = 1; i < argc; i++) {
+        if (!strcmp(argv[i], "--reps") && i + 1 < argc) reps = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--threads") && i + 1 < argc) threads = atoi(argv[++i]);
+        else if (nn < 16) ns[nn++] = strtoull(argv[i], 0, 10);
+    }
+    if (nn == 0 || reps < 1 || reps > 1000 || threads < 1 || threads > 64) {
+        fprintf(stderr, "usage: %s [--reps R] [--threads T] N...\n", argv[0]);
+        return 2;
+    }
+    printf("{\"reps\": %d, \"threads\": %d, \"sizes\": [", reps, threads);
+    for (int s = 0; s < nn; s++) {
+        const uint64_t n = ns[s];
+        uint8_t *keys = malloc(16 * n), *pk = malloc(16 * n);
+        uint8_t *ans1 = malloc(n), *ansb = malloc(n);
+        for (uint64_t i = 0; i < n; i++) {
+            key16(i, keys + 16 * i);
+            key16(i % 2 == 0 ? i : n + i, pk + 16 * i);
+        }
+        double t_new[1000], t_add[1000], t_enc[1000], t_free[1000], t_all[1000];
+        uint64_t esz = 0;
+        uint8_t *enc = NULL;
+        for (int r = -1; r < reps; r++) { /* r = -1: warm-up (context pool, first-touch allocations) */
+            double t0 = now_us();
+            seb_filter *f = seb_filter_new((int64_t)n, 0.01);
+            if (!f) die("NewBloomFilter");
+            double t1 = now_us();
+            for (uint64_t i = 0; i < n; i++)
+                if (seb_filter_add(f, keys + 16 * i, 16) != SEB_OK) die("Add");
+            double t2 = now_us();
+            if (!enc) {
+                esz = seb_filter_encoded_size(f);
+                enc = malloc(esz);
+            }
+            if (seb_filter_encode(f, enc, esz) != SEB_OK) die("Encode");
+            double t3 = now_us();
+            seb_filter_free(f);
+            double t4 = now_us();
+            if (r >= 0) {
+                t_new[r] = t1 - t0, t_add[r] = t2 - t1, t_enc[r] = t3 - t2, t_free[r] = t4 - t3, t_all[r] = t4 - t0;
+            }
+        }
+        char henc[65];
+        digest(enc, esz, henc);
+
+        seb_filter *g = seb_filter_decode(enc, esz);
+        if (!g) die("DecodeBloomFilter");
+        double ns1 = 0, nsT = 0, t_one[1000], t_b[1000];
+        double rate1 = 0, rateT = 0;
+        for (int r = -1; r < reps; r++) {
+            double npc;
+            double rate = run_readers(g, pk, n, 1, n, ans1, &npc);
+            if (r >= 0) t_one[r] = npc;
+            if (r == reps - 1) rate1 = rate;
+        }
+        ns1 = median(t_one, reps);
+        uint64_t positives = 0;
+        for (uint64_t q = 0; q < n; q++) positives += ans1[q];
+        for (int r = -1; r < reps; r++) {
+            double npc;
+            double rate = run_readers(g, pk, n, threads, n, NULL, &npc);
+            if (r >= 0) t_b[r] = rate;
+            if (r == reps - 1) nsT = npc;
+        }
+        rateT = median(t_b, reps);
+        seb_keys kb = {pk, NULL, n, 16, 0};
+        double t_batch[1000];
+        for (int r = -1; r < reps; r++) {
+            double t0 = now_us();
+            if (seb_filter_may_contain_batch(g, &kb, ansb) != SEB_OK) die("MayContainBatch");
+            if (r >= 0) t_batch[r] = now_us() - t0;
+        }
+        char hans[65];
+        digest(ans1, n, hans);
+        const int same = memcmp(ans1, ansb, n) == 0;
+        seb_filter_free(g);
+        printf("%s{\"n\": %" PRIu64 ", \"encode_len\": %" PRIu64 ", \"encode_sha256\": \"%s\", "
+               "\"build_us\": {\"new\": %.2f, \"add_loop\": %.2f, \"encode\": %.2f, \"free\": %.2f, \"total\": %.2f}, "
+               "\"add_ns_per_key\": %.2f, \"build_keys_per_s\": %.0f, "
+               "\"may_contain\": {\"ns_per_call_1t\": %.2f, \"calls_per_s_1t\": %.0f, \"threads\": %d, "
+               "\"ns_per_call_per_thread\": %.2f, \"calls_per_s\": %.0f}, "
+               "\"batch_us\": %.2f, \"probe_positives\": %" PRIu64 ", \"probe_sha256\": \"%s\", "
+               "\"batch_matches_single\": %s}",
+               s ? ", " : "", n, esz, henc, median(t_new, reps), median(t_add, reps), median(t_enc, reps),
+               median(t_free, reps), median(t_all, reps), median(t_add, reps) * 1e3 / (double)n,
+               (double)n / (median(t_all, reps) * 1e-6), ns1, rate1, threads, nsT, rateT, median(t_batch, reps),
+               positives, hans, same ? "true" : "false");
+        free(keys), free(pk), free(ans1), free(ansb), free(enc);
+        if (!same) {
+            printf("]}\n");
+            fprintf(stderr, "batched and single-key answers differ at n=%" PRIu64 "\n", n);
+            return 1;
+        }
+    }
+    printf("]}\n");
+    return 0;
+}

@@ -880,6 +880,32 @@ def test_c_harness_replays_sstable_sequence(seb, golden, n, expected):
         assert res["probe_sha256"] == row["probe_sha256"]
 
 
+def test_flush_bench_harness_parity(seb, golden):
+    """harness/flush_bench.c (bench.py --config flush): New -> Add per key -> Encode at flush and
+    compaction sizes, then Decode -> single-key MayContain on 1 and 8 threads at once and the
+    batched GPU MayContain; every digest against the oracle (and the C1 golden row at 100K)."""
+    import json
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(seb.LIB_PATH), "flush_bench")
+    out = subprocess.run([exe, "--reps", "2", "--threads", "8", "1", "1000", "50000", "100000"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    res = json.loads(out.stdout)
+    for r in res["sizes"]:
+        n = r["n"]
+        m, k = oc.params(n, 0.01)
+        bits = oc.build(m, k, kg.key16(np.arange(n)), n, stride=16)
+        assert r["encode_sha256"] == sha(bn.encode(bits, m, k)), n
+        ans = oc.probe(bits, m, k, kg.key16(kg.probe_indices(n)), n, stride=16)
+        assert r["probe_sha256"] == sha(ans.tobytes()), n
+        assert r["batch_matches_single"]
+        row = next((g for g in golden["fixed16"] if g["n"] == n and g["p"] == 0.01), None)
+        if row is not None:
+            assert r["encode_sha256"] == row["encode_sha256"] and r["probe_sha256"] == row["probe_sha256"]
+
+
 @pytest.mark.parametrize("n,expected", [(1000, 1000), (70000, 100000)])
 def test_c_harness_under_host_asan(seb, golden, n, expected):
     """The SSTable replay harness against libseb_bloom.so built with host-side AddressSanitizer +
