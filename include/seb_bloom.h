@@ -73,37 +73,18 @@ int seb_abi_version(void);
 /* Process-wide tuning knobs (results never change, only speed):
  *   "build_algo"      0 auto, 1 device-scope atomic OR, 2 radix-partitioned LDS build, 3 the whole
  *                     filter in one CU's LDS (word array <= 160 KiB), keys split over workgroups
- *   "probe_split"     k == 7 probes: words gathered before the first test (0 = all 7, 2, 3)
- *   "probe_kpt"       k == 7 probes: keys per thread (1, 2, 4) — gathers in flight per lane
  *   "bucket_min_keys" auto build_algo: radix-partitioned from this many keys on
  *   "lds_min_keys"    auto build_algo: LDS-resident filter (<= 160 KiB) from this many keys on
- *   "grid_cap"        maximum workgroups of the grid-stride kernels
- *   "probe_slice_shift" k == 7, m < 2^32 probes: slice of 2^shift words gathered per phase (0 = off)
- *   "probe_slice_grid"  sliced probe: workgroup cap (0 = grid_cap)
- *   "probe_mode"      k == 7 probe: 8 = phased, one launch per filter range (default); 0-7 sliced gather orders (k_probe_sliced)
- *   "probe_phases"    phased probe (probe_mode 8): phases, 0 = one per 4 MiB of filter
- *   "probe_phase0_pct", "probe_phase0_kpt"  phased probe: range 0's share of the filter (0 = even),
- *                     keys per thread in phase 0 (1, 2, 4)
- *   "probe_pack_first" phased probe: a streaming pack pass, then every range from packed words (0/1)
- *   "probe_persistent" sliced probe: persistent 1024-thread workgroups (0 = off)
+ *   "many_splits"     batched small-filter build: workgroups per filter (0 = auto)
+ *   "probe_phases"    k == 7, m < 2^29 probes: filter ranges of the phased probe, one launch each
+ *                     (0 = one per 4 MiB of filter; 1 = the single-launch sliced probe)
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
- *   "multi_phases"    interleaved multi-filter probe: 1 = in-kernel slices (default), 0 = one launch
- *                     per 4 MiB of table, n > 1 = n launches (phased, k == 7, m < 2^29)
- *   "multiget_pass_kib" registry MultiGet: filter bytes per pass (0 = one pass over all files)
- *   "scatter_threads", "scatter_kpt"  radix-partitioned build: workgroup size, keys per thread
- *   "apply_threads"   radix-partitioned build: apply workgroup size (256, 512, 1024)
- *   "stream_nt"       non-temporal loads of 16-B key batches (0/1)
- *   "varlen_prehash_min_keys", "varlen_sort_min_keys"  variable-length batches: LDS pre-hash and
- *                     global length-sort thresholds
- *   "varlen_hash_keys", "varlen_hash_win"  LDS pre-hash: keys per workgroup (256, 384, 448, 512, 1024;
- *                     384 / 448: 512 threads, the 128 / 64 longest keys hashed one FNV chain per wave) and
- *                     window bytes per key (48, 56, 64, 72, 80; 1024-key workgroups use 48 or 56)
- *   "varlen_prehash_packed" LDS pre-hash writes packed residues (8 B/key) for k == 7, m < 2^29
- *   "probe_phase_grid"  > 0: workgroup cap of the later probe phases (0 = one 4-key group per thread)
- *   "build_prepack"     fixed-width bucketed build hashes to packed residues first (0 off, 1 on)
- *   "multiget_group"    registry MultiGet tests k=7 filters 4 at a time (1) or one by one (0, default)
- *   "multiget_order"    registry MultiGet walks batches of >= 64K keys in key-range order (1, default) or batch order (0)
- *                     filters, read directly by the bucketed build and the phased probe (0/1)
+ *   "multiget_order"  registry MultiGet walks batches of >= 64K keys in key-range order (1, default)
+ *                     or batch order (0)
+ *   "varlen_prehash_min_keys"  variable-length batches of this many keys are pre-hashed in LDS
+ *   "grid_cap"        maximum workgroups of the grid-stride kernels
+ *   "workspace_limit_mib"  cap on library scratch (0 = none); a request above it fails with
+ *                     SEB_ERR_NOMEM (MultiGet's key-range order then falls back to batch order)
  * Environment variables SEB_<NAME> (upper case) set the initial values. */
 int seb_set_option(const char *name, int64_t value);
 int seb_get_option(const char *name, int64_t *value);

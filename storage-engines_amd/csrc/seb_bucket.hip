@@ -64,23 +64,11 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *w
 // for hash-distributed keys: cap = mean + 8 sigma + 32) is OR-ed straight into the filter with
 // device-scope atomics instead, which k_bkt_apply's read-modify-write OR preserves.
 // LDS: sorted[THREADS*KPT7*7] u32 | cursor[nb] | fill[nb] | wsum[16] | ovf
-#ifdef SEB_SCATTER_WAVES  // diagnostic builds: cap the scatter's VGPRs so other kernels' waves fit beside it
-#define SEB_SCATTER_ATTR __attribute__((amdgpu_waves_per_eu(SEB_SCATTER_WAVES, 8)))
-#else
-#define SEB_SCATTER_ATTR
-#endif
-// ngrp > 0 (option scatter_xcd): one region per (bucket, tile group) instead of per (bucket, tile),
-// group = blockIdx % ngrp, i.e. the workgroups of one XCD (round-robin dispatch); each round claims
-// its run in the group's region with one device atomic on counts[region].  A region's partly
-// written tail line is then shared by every tile of the XCD and stays in that XCD's L2, where
-// per-tile regions leave 32 x nb partial lines per XCD, more than its L2 holds.  counts must be
-// zero at launch; it ends holding each region's claimed length (apply clamps it to cap).
 template <typename Src, int KFIX, int THREADS, int KPT7>
-__global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src src, uint64_t n, ModArg md, uint32_t nb,
-                                                              uint32_t tile_keys, uint32_t ntiles, uint32_t cap,
-                                                              uint16_t *__restrict__ regions,
-                                                              uint32_t *__restrict__ counts,
-                                                              uint32_t *__restrict__ words, uint32_t ngrp) {
+__global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, ModArg md, uint32_t nb, uint32_t tile_keys,
+                                                             uint32_t ntiles, uint32_t cap, uint16_t *__restrict__ regions,
+                                                             uint32_t *__restrict__ counts,
+                                                             uint32_t *__restrict__ words) {
     extern __shared__ uint32_t smem[];
     constexpr uint32_t kPos = (uint32_t)THREADS * KPT7 * 7;  // positions sorted per round
     uint32_t *sorted = smem;
@@ -88,9 +76,7 @@ __global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src sr
     uint32_t *fill = cursor + nb;
     uint32_t *wsum = fill + nb;
     uint32_t *ovf = wsum + 16;
-    const uint32_t t = blockIdx.x;
-    // region of bucket b: (b * rstride + rsel) * cap
-    const uint32_t rstride = ngrp ? ngrp : ntiles, rsel = ngrp ? t % ngrp : t;
+    const uint32_t t = blockIdx.x;  // region of bucket b: (b * ntiles + t) * cap
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
         cursor[b] = 0u;
         fill[b] = 0u;
@@ -207,10 +193,9 @@ __global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src sr
         // belongs at regions[fill[b] + idx], and flag a run that would overflow its region.
         for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
             const uint32_t start = b ? cursor[b - 1] : 0u, c = cursor[b] - start;
-            const uint32_t reg = b * rstride + rsel;
-            const uint32_t fb = ngrp ? (c ? atomicAdd(&counts[reg], c) : 0u) : fill[b];
-            if (fb + c > cap) *ovf = 1u;
-            fill[b] = reg * cap + fb - start;
+            const uint32_t reg = b * ntiles + t;
+            if (fill[b] + c > cap) *ovf = 1u;
+            fill[b] = reg * cap + fill[b] - start;
         }
         __syncthreads();
         const uint32_t cnt = (uint32_t)(k1 - k0) * md.k;
@@ -218,18 +203,14 @@ __global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src sr
 #pragma unroll 5
             for (uint32_t idx = threadIdx.x; idx < cnt; idx += blockDim.x) {
                 const uint32_t p = sorted[idx];
-#ifdef SEB_DIAG_SCATTER_NT  // diagnostic builds (tools/diag_lib.sh): streaming stores for the runs
-                __builtin_nontemporal_store((uint16_t)p, regions + fill[p >> kBktShift] + idx);
-#else
                 regions[fill[p >> kBktShift] + idx] = (uint16_t)p;
-#endif
             }
         } else {
             for (uint32_t idx = threadIdx.x; idx < cnt; idx += blockDim.x) {
                 const uint32_t p = sorted[idx];
                 const uint32_t b = p >> kBktShift;
                 const uint32_t e = fill[b] + idx;
-                if (e - (b * rstride + rsel) * cap < cap)
+                if (e - (b * ntiles + t) * cap < cap)
                     regions[e] = (uint16_t)p;
                 else
                     __hip_atomic_fetch_or(words + (p >> 5), 1u << (p & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -237,14 +218,13 @@ __global__ __launch_bounds__(THREADS) SEB_SCATTER_ATTR void k_bkt_scatter(Src sr
         }
         __syncthreads();
         for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
-            fill[b] += cursor[b] - (b * rstride + rsel) * cap;  // fill + this round's count (per-tile regions)
+            fill[b] += cursor[b] - (b * ntiles + t) * cap;  // fill + this round's count
             cursor[b] = 0u;
         }
         if (threadIdx.x == 0) *ovf = 0u;
         __syncthreads();
     }
-    if (!ngrp)
-        for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) counts[(uint64_t)b * ntiles + t] = min(fill[b], cap);
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) counts[(uint64_t)b * ntiles + t] = min(fill[b], cap);
 }
 
 // ---- apply: one workgroup per bucket; stream its ntiles regions (16-B loads, 8 positions per
@@ -267,13 +247,7 @@ __global__ __launch_bounds__(THREADS) void k_bkt_apply(const uint16_t *__restric
         const uint32_t t = q / chunks, c = q - t * chunks;
         const uint32_t valid = cnt[t];
         if (c * 8 < valid) {
-#ifdef SEB_DIAG_APPLY_NT  // diagnostic builds: streaming loads of the runs
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 vv = __builtin_nontemporal_load((const u32x4 *)(reg + q));
-            const uint4 v = make_uint4(vv.x, vv.y, vv.z, vv.w);
-#else
             const uint4 v = reg[q];
-#endif
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (uint32_t e = 0; e < 8; ++e)
@@ -294,49 +268,43 @@ __global__ __launch_bounds__(THREADS) void k_bkt_apply(const uint16_t *__restric
 // ------------------------------------------------------------------ host side ---------------
 
 struct BktPlan {
-    uint32_t nb, tile_keys, ntiles, cap;
-    uint32_t ngrp;     // 0: a region per (bucket, tile); > 0: per (bucket, tile group) (scatter_xcd)
-    uint32_t nregion;  // regions per bucket: ntiles or ngrp
+    uint32_t nb, tile_keys, ntiles, cap;  // a region of cap u16 per (bucket, tile)
     uint64_t off_regions, off_counts, bytes;
 };
 
-static uint32_t scatter_threads() { return options().scatter_threads == 512 ? 512u : 1024u; }
+// One 1024-thread scatter workgroup per CU (two of 512 measured slower).
+constexpr uint32_t kScatterThreads = 1024;
 // 5 keys per thread per round only while its sort buffer and the two per-bucket arrays fit the
-// 160 KiB of LDS (nb <= 2551 at 1024 threads, m <= ~167M bits); 4 otherwise.
+// 160 KiB of LDS (nb <= 2551, m <= ~167M bits); 4 otherwise.
 static uint32_t scatter_kpt(uint32_t nb) {
-    const uint32_t thr = scatter_threads();
-    if (options().scatter_kpt == 5 && ((uint64_t)thr * 5 * 7 + 2 * nb + 17) * 4 <= 160u * 1024) return 5u;
-    return 4u;
+    return ((uint64_t)kScatterThreads * 5 * 7 + 2 * nb + 17) * 4 <= 160u * 1024 ? 5u : 4u;
 }
 
 static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k) {
     BktPlan p{};
     const uint64_t nwords = (m + 31) / 32;
     p.nb = (uint32_t)((nwords + kBktWords - 1) / kBktWords);
-    const uint32_t thr = scatter_threads();
+    const uint32_t thr = kScatterThreads;
     const uint32_t kpt = scatter_kpt(p.nb);
     const uint32_t pos = thr * kpt * 7;
     const uint32_t round_keys = k == 7 ? kpt * thr : pos / k;
-    const uint32_t target = kTargetTiles * (1024 / thr);
+    const uint32_t target = kTargetTiles;
     uint64_t rounds_total = (n + round_keys - 1) / round_keys;
     uint64_t rounds_per_tile = (rounds_total + target - 1) / target;
     if (rounds_per_tile < 1) rounds_per_tile = 1;
     p.tile_keys = (uint32_t)(rounds_per_tile * round_keys);
     p.ntiles = (uint32_t)((n + p.tile_keys - 1) / p.tile_keys);
-    const uint32_t g = (uint32_t)options().scatter_xcd;
-    p.ngrp = g && p.ntiles >= 4 * g ? g : 0u;
-    p.nregion = p.ngrp ? p.ngrp : p.ntiles;
-    // positions of one region's tiles landing in one (full) bucket: mean + 8 sigma + 32, 8-aligned
-    const double rkeys = p.ngrp ? (double)p.tile_keys * ((p.ntiles + p.ngrp - 1) / p.ngrp) : (double)p.tile_keys;
+    // positions of one tile landing in one (full) bucket: mean + 8 sigma + 32, 8-aligned
+    const double rkeys = (double)p.tile_keys;
     const double mu = rkeys * k * (double)(1u << kBktShift) / (double)m;
     double c = mu + 8.0 * sqrt(mu > 1 ? mu : 1) + 32.0;
-    const double most = rkeys * k;  // never more than every position of the region's tiles
+    const double most = rkeys * k;  // never more than every position of the tile
     if (c > most) c = most;
     p.cap = ((uint32_t)c + 7) & ~7u;
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
     p.off_regions = 0;
-    p.off_counts = al((uint64_t)p.nb * p.nregion * p.cap * 2);
-    p.bytes = al(p.off_counts + (uint64_t)p.nb * p.nregion * 4);
+    p.off_counts = al((uint64_t)p.nb * p.ntiles * p.cap * 2);
+    p.bytes = al(p.off_counts + (uint64_t)p.nb * p.ntiles * 4);
     return p;
 }
 
@@ -365,28 +333,25 @@ static hipError_t run_bucketed(uint64_t n, const ModArg &md, uint32_t *words, vo
         const uint64_t sn = n - k0 < maxk ? n - k0 : maxk;
         const BktPlan p = plan_bucketed(sn, md.m, md.k);
         if (p.bytes > ws_bytes || p.ntiles > kMaxTiles) return hipErrorInvalidValue;
-        if ((uint64_t)p.nb * p.nregion * p.cap >= (1ull << 31)) return hipErrorInvalidValue;  // u32 region index
+        if ((uint64_t)p.nb * p.ntiles * p.cap >= (1ull << 31)) return hipErrorInvalidValue;  // u32 region index
         uint8_t *w = (uint8_t *)ws;
         uint16_t *regions = (uint16_t *)(w + p.off_regions);
         uint32_t *counts = (uint32_t *)(w + p.off_counts);
         const uint64_t nwords = (md.m + 31) / 32;
-        const uint32_t thr = scatter_threads();
         const uint32_t kpt = scatter_kpt(p.nb);
-        const size_t lds = ((size_t)thr * kpt * 7 + 2 * p.nb + 17) * sizeof(uint32_t);
+        const size_t lds = ((size_t)kScatterThreads * kpt * 7 + 2 * p.nb + 17) * sizeof(uint32_t);
         hipError_t e = chunk(k0, sn, [&](auto src) -> hipError_t {
             using S = decltype(src);
             constexpr int K0 = IsPacked<S>::value ? 7 : 0;  // packed sources have no generic-k kernel
-            auto scat = thr == 512 ? (md.k == 7 ? k_bkt_scatter<S, 7, 512, 4> : k_bkt_scatter<S, K0, 512, 4>)
-                        : kpt == 5 ? (md.k == 7 ? k_bkt_scatter<S, 7, 1024, 5> : k_bkt_scatter<S, K0, 1024, 5>)
-                                   : (md.k == 7 ? k_bkt_scatter<S, 7, 1024, 4> : k_bkt_scatter<S, K0, 1024, 4>);
+            auto scat = kpt == 5 ? (md.k == 7 ? k_bkt_scatter<S, 7, kScatterThreads, 5> : k_bkt_scatter<S, K0, kScatterThreads, 5>)
+                                 : (md.k == 7 ? k_bkt_scatter<S, 7, kScatterThreads, 4> : k_bkt_scatter<S, K0, kScatterThreads, 4>);
             hipError_t a = hipFuncSetAttribute((const void *)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (a != hipSuccess) return a;
-            if (p.ngrp && (a = hipMemsetAsync(counts, 0, (size_t)p.nb * p.nregion * 4, s)) != hipSuccess) return a;
-            hipLaunchKernelGGL(scat, dim3(p.ntiles), dim3(thr), lds, s, src, sn, md, p.nb, p.tile_keys, p.ntiles,
-                               p.cap, regions, counts, words, p.ngrp);
-            const uint32_t at = options().apply_threads;
-            auto apply = at == 1024 ? k_bkt_apply<1024> : at == 512 ? k_bkt_apply<512> : k_bkt_apply<256>;
-            hipLaunchKernelGGL(apply, dim3(p.nb), dim3(at), 0, s, regions, counts, p.nregion, p.cap, words, nwords);
+            hipLaunchKernelGGL(scat, dim3(p.ntiles), dim3(kScatterThreads), lds, s, src, sn, md, p.nb, p.tile_keys,
+                               p.ntiles, p.cap, regions, counts, words);
+            // apply: 1024 threads per bucket (256 and 512 measured slower)
+            hipLaunchKernelGGL(k_bkt_apply<1024>, dim3(p.nb), dim3(1024), 0, s, regions, counts, p.ntiles, p.cap, words,
+                               nwords);
             return hipGetLastError();
         });
         if (e != hipSuccess) return e;
@@ -402,8 +367,6 @@ hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModA
         sub.n = sn;
         if (kb.hashes)
             sub.hashes = kb.hashes + k0;
-        else if (kb.perm)
-            sub.perm = kb.perm + k0;  // perm holds batch-wide key indices into the same offsets
         else if (kb.offsets)
             sub.offsets = kb.offsets + k0;
         else

@@ -401,10 +401,8 @@ hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mo
     if (n == 0) return hipSuccess;
     const uint64_t g = (n + kWalRecs - 1) / kWalRecs;
     if (g >= (1ull << 31)) return hipErrorInvalidValue;
-    if (options().wal_lds_kib != 48)  // 36 KiB: four workgroups per CU (measured 4% faster than 48)
-        hipLaunchKernelGGL(k_wal_crc<36 * 1024>, dim3((unsigned)g), dim3(kWalRecs), 0, s, data, off, n, mode, crc, ok);
-    else
-        hipLaunchKernelGGL(k_wal_crc<48 * 1024>, dim3((unsigned)g), dim3(kWalRecs), 0, s, data, off, n, mode, crc, ok);
+    // 36 KiB of staging: four workgroups per CU (measured 4% faster than 48 KiB)
+    hipLaunchKernelGGL(k_wal_crc<36 * 1024>, dim3((unsigned)g), dim3(kWalRecs), 0, s, data, off, n, mode, crc, ok);
     return hipGetLastError();
 }
 

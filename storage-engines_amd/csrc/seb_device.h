@@ -84,50 +84,6 @@ __device__ __forceinline__ void fnv_key16(const uint4 v, uint64_t &h1, uint64_t 
     h2 = (acc2 << 32) | lo2;
 }
 
-#ifdef SEB_UNIFORM_PREFIX
-// fnv_key16 from the state (s1, s2) after the key's first 4P bytes: the low words continue the
-// byte chain, the high words are 435^(16-4P) hi_4P + sum_j d_j 435^(15-j) over the rest.
-template <int P>
-__device__ __forceinline__ void fnv_key16_from(const uint4 v, uint64_t s1, uint64_t s2, uint64_t &h1, uint64_t &h2) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint32_t lo1 = (uint32_t)s1, lo2 = (uint32_t)s2;
-    uint64_t acc1 = (uint32_t)(s1 >> 32) * pow435(16 - 4 * P), acc2 = (uint32_t)(s2 >> 32) * pow435(16 - 4 * P);
-#pragma unroll
-    for (int j = 4 * P; j < 16; ++j) {
-        const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
-        const uint32_t x = lo1 ^ b;
-        const uint64_t p = (uint64_t)x * 435u;
-        lo1 = (uint32_t)p;
-        acc1 = mad_lo((uint32_t)(p >> 32) + (x << 8), pow435(15 - j), acc1);
-        const uint64_t q = (uint64_t)lo2 * 435u;
-        acc2 = mad_lo((uint32_t)(q >> 32) + (lo2 << 8), pow435(15 - j), acc2);
-        lo2 = (uint32_t)q ^ b;
-    }
-    h1 = (acc1 << 32) | lo1;
-    h2 = (acc2 << 32) | lo2;
-}
-
-// Diagnostic builds (tools/diag_lib.sh -DSEB_UNIFORM_PREFIX): the leading 4-byte words that are
-// equal on every active lane of the wave (a sorted flush batch shares its keys' prefixes) are
-// hashed once, on uniform (scalar) values; each lane hashes only the rest.
-__device__ __forceinline__ void fnv_key16_wave(const uint4 v, uint64_t &h1, uint64_t &h2) {
-    const uint64_t exec = __ballot(1);
-    const uint32_t u0 = __builtin_amdgcn_readfirstlane(v.x), u1 = __builtin_amdgcn_readfirstlane(v.y),
-                   u2 = __builtin_amdgcn_readfirstlane(v.z);
-    if (__ballot(v.x == u0) != exec) return fnv_key16(v, h1, h2);
-    uint64_t s1 = kFnvOffset, s2 = kFnvOffset;
-    fnv_word(u0, s1, s2);
-    if (__ballot(v.y == u1) != exec) return fnv_key16_from<1>(v, s1, s2, h1, h2);
-    fnv_word(u1, s1, s2);
-    if (__ballot(v.z == u2) != exec) return fnv_key16_from<2>(v, s1, s2, h1, h2);
-    fnv_word(u2, s1, s2);
-    return fnv_key16_from<3>(v, s1, s2, h1, h2);
-}
-#define SEB_FNV_KEY16 fnv_key16_wave
-#else
-#define SEB_FNV_KEY16 fnv_key16
-#endif
-
 // Both chains in the split form of fnv_key16, for walks of unknown length: the high words are
 // kept as u64 accumulators whose low 32 bits are the hash's high word, and each 4-byte word
 // folds its four d_j into them with constant weights (3 mads), then one mad scales the old value
@@ -161,16 +117,9 @@ struct FnvSplit {
 
 // Sources with kSplit = true also expose load(i) -> uint4 and hash_raw(raw, h1, h2), so a kernel
 // can issue the loads of its next batch of keys before it hashes them (software prefetch).
-struct Keys16 {  // fixed 16-B keys, 16-B aligned: one dwordx4 per lane, 1 KiB per wave, coalesced
-    static constexpr bool kSplit = true;
-    const uint4 *p;
-    __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
-    __device__ __forceinline__ uint4 load(uint64_t i) const { return p[i]; }
-    __device__ __forceinline__ static void hash_raw(const uint4 v, uint64_t &h1, uint64_t &h2) { SEB_FNV_KEY16(v, h1, h2); }
-    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const { SEB_FNV_KEY16(p[i], h1, h2); }
-};
-
-struct Keys16NT {  // Keys16 with non-temporal loads: the streamed batch does not evict filter lines from L2
+// Fixed 16-B keys, 16-B aligned: one dwordx4 per lane, 1 KiB per wave, coalesced; non-temporal, so
+// the streamed batch does not evict filter lines from L2 (+2% over plain loads).
+struct Keys16 {
     static constexpr bool kSplit = true;
     const uint4 *p;
     __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
@@ -179,8 +128,8 @@ struct Keys16NT {  // Keys16 with non-temporal loads: the streamed batch does no
         const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(p + i));
         return make_uint4(v.x, v.y, v.z, v.w);
     }
-    __device__ __forceinline__ static void hash_raw(const uint4 v, uint64_t &h1, uint64_t &h2) { SEB_FNV_KEY16(v, h1, h2); }
-    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const { SEB_FNV_KEY16(load(i), h1, h2); }
+    __device__ __forceinline__ static void hash_raw(const uint4 v, uint64_t &h1, uint64_t &h2) { fnv_key16(v, h1, h2); }
+    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const { fnv_key16(load(i), h1, h2); }
 };
 
 struct KeysStrideW {  // fixed stride, multiple of 4 bytes, 4-B aligned
@@ -232,17 +181,6 @@ struct KeysVar {  // variable length: key i = p[off[i], off[i+1])
     __device__ __forceinline__ uint64_t index(uint64_t i) const { return i; }
     __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
         fnv_range(p, off[i], off[i + 1], h1, h2);
-    }
-};
-
-struct KeysVarPerm {  // variable length, processed in length-bucketed order: i-th = key perm[i]
-    const uint8_t *p;
-    const uint64_t *off;
-    const uint32_t *perm;
-    __device__ __forceinline__ uint64_t index(uint64_t i) const { return perm[i]; }
-    __device__ __forceinline__ void hash(uint64_t i, uint64_t &h1, uint64_t &h2) const {
-        const uint64_t j = perm[i];
-        fnv_range(p, off[j], off[j + 1], h1, h2);
     }
 };
 
@@ -342,12 +280,8 @@ __device__ __forceinline__ void for_positions(uint64_t h1, uint64_t h2, const Mo
 template <typename Fn>
 static inline hipError_t with_src(const KeyBatch &kb, Fn &&fn) {
     if (kb.hashes) return fn(KeysHashed{kb.hashes});
-    if (kb.offsets && kb.perm) return fn(KeysVarPerm{kb.data, kb.offsets, kb.perm});
     if (kb.offsets) return fn(KeysVar{kb.data, kb.offsets});
-    if (kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0) {
-        if (options().stream_nt) return fn(Keys16NT{(const uint4 *)kb.data});
-        return fn(Keys16{(const uint4 *)kb.data});
-    }
+    if (kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0) return fn(Keys16{(const uint4 *)kb.data});
     if (kb.stride % 4 == 0 && ((uintptr_t)kb.data & 3) == 0)
         return fn(KeysStrideW{(const uint32_t *)kb.data, kb.stride / 4});
     return fn(KeysStrideB{kb.data, kb.stride});

@@ -13,6 +13,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/seb_bloom.h"
@@ -107,119 +108,76 @@ static bool env_flag(const char *name, long *out) {
     return true;
 }
 
-// Validated assignment of one knob; false for an unknown name or an out-of-range value.
-static bool set_opt(Options &o, const char *name, int64_t value) {
-    if (!strcmp(name, "build_algo") && value >= 0 && value <= 3) o.build_algo = (int)value;
-    else if (!strcmp(name, "probe_split") && (value == 0 || value == 2 || value == 3)) o.probe_split = (int)value;
-    else if (!strcmp(name, "probe_kpt") && (value == 1 || value == 2 || value == 4 || value == 6 || value == 8)) o.probe_kpt = (int)value;
-    else if (!strcmp(name, "probe_slice_shift") && value >= 0 && value <= 26) o.probe_slice_shift = (int)value;
-    else if (!strcmp(name, "probe_slice_grid") && value >= 0) o.probe_slice_grid = (unsigned)value;
-    else if (!strcmp(name, "multi_interleave") && (value == 0 || value == 1)) o.multi_interleave = (int)value;
-    else if (!strcmp(name, "scatter_threads") && (value == 512 || value == 1024)) o.scatter_threads = (int)value;
-    else if (!strcmp(name, "stream_nt") && (value == 0 || value == 1)) o.stream_nt = (int)value;
-    else if (!strcmp(name, "scatter_kpt") && (value == 4 || value == 5)) o.scatter_kpt = (int)value;
-    else if (!strcmp(name, "probe_persistent") && value >= 0 && value <= 65536) o.probe_persistent = (int)value;
-    else if (!strcmp(name, "probe_mode") && value >= 0 && value <= 8) o.probe_mode = (int)value;
-    else if (!strcmp(name, "probe_phases") && value >= 0 && value <= 64) o.probe_phases = (int)value;
-    else if (!strcmp(name, "probe_pack_first") && (value == 0 || value == 1)) o.probe_pack_first = (int)value;
-    else if (!strcmp(name, "multi_phases") && value >= 0 && value <= 64) o.multi_phases = (int)value;
-    else if (!strcmp(name, "many_splits") && value >= 0 && value <= 64) o.many_splits = (uint32_t)value;
-    else if (!strcmp(name, "probe_phase0_pct") && value >= 0 && value <= 90) o.probe_phase0_pct = (int)value;
-    else if (!strcmp(name, "probe_phase0_kpt") && (value == 1 || value == 2 || value == 4)) o.probe_phase0_kpt = (int)value;
-    else if (!strcmp(name, "multiget_pass_kib") && value >= 0 && value <= (1 << 22)) o.multiget_pass_kib = (int)value;
-    else if (!strcmp(name, "multiget_group") && (value == 0 || value == 1)) o.multiget_group = (int)value;
-    else if (!strcmp(name, "multiget_order") && (value == 0 || value == 1)) o.multiget_order = (int)value;
-    else if (!strcmp(name, "varlen_hash_keys") && (value == 256 || value == 384 || value == 448 || value == 512 || value == 1024))
-        o.varlen_hash_keys = (uint32_t)value;
-    else if (!strcmp(name, "varlen_hash_win") && (value == 48 || value == 56 || value == 64 || value == 72 || value == 80))
-        o.varlen_hash_win = (uint32_t)value;
-    else if (!strcmp(name, "apply_threads") && (value == 256 || value == 512 || value == 1024))
-        o.apply_threads = (uint32_t)value;
-    else if (!strcmp(name, "clear_kernel") && (value == 0 || value == 1)) o.clear_kernel = (int)value;
-    else if (!strcmp(name, "scatter_xcd") && (value == 0 || value == 8 || value == 16 || value == 32)) o.scatter_xcd = (int)value;
-    else if (!strcmp(name, "varlen_prehash_packed") && (value == 0 || value == 1))
-        o.varlen_prehash_packed = (int)value;
-    else if (!strcmp(name, "build_prepack") && (value == 0 || value == 1)) o.build_prepack = (int)value;
-    else if (!strcmp(name, "wal_lds_kib") && (value == 36 || value == 48)) o.wal_lds_kib = (int)value;
-    else if (!strcmp(name, "varlen_sort_min_keys") && value >= 0) o.varlen_sort_min_keys = (uint64_t)value;
-    else if (!strcmp(name, "varlen_prehash_min_keys") && value >= 0) o.varlen_prehash_min_keys = (uint64_t)value;
-    else if (!strcmp(name, "grid_cap") && value > 0 && value <= (1 << 30)) o.grid_cap = (unsigned)value;
-    else if (!strcmp(name, "probe_phase_grid") && value >= 0 && value <= (1 << 30)) o.probe_phase_grid = (unsigned)value;
-    else if (!strcmp(name, "bucket_min_keys") && value >= 0) o.bucket_min_keys = (uint64_t)value;
-    else if (!strcmp(name, "lds_min_keys") && value >= 0) o.lds_min_keys = (uint64_t)value;
-    else return false;
-    return true;
-}
+// Every knob of seb_set_option: name, field, accepted range.  SEB_<NAME> in the environment sets
+// its initial value.
+struct OptionDesc {
+    const char *name;
+    int64_t lo, hi;
+    int64_t (*get)(const Options &);
+    void (*set)(Options &, int64_t);
+};
+#define SEB_OPT(field, lo, hi)                                                              \
+    OptionDesc {                                                                            \
+        #field, lo, hi, [](const Options &o) { return (int64_t)o.field; },                   \
+            [](Options &o, int64_t v) { o.field = (decltype(o.field))v; }                    \
+    }
+static const OptionDesc kOptions[] = {
+    SEB_OPT(build_algo, 0, 3),
+    SEB_OPT(multi_interleave, 0, 1),
+    SEB_OPT(multiget_order, 0, 1),
+    SEB_OPT(varlen_prehash_min_keys, 0, INT64_MAX),
+    SEB_OPT(bucket_min_keys, 0, INT64_MAX),
+    SEB_OPT(lds_min_keys, 0, INT64_MAX),
+    SEB_OPT(many_splits, 0, 64),
+    SEB_OPT(probe_phases, 0, 64),
+    SEB_OPT(grid_cap, 1, 1 << 30),
+    SEB_OPT(workspace_limit_mib, 0, 1 << 30),
+};
+#undef SEB_OPT
 
-// Every knob of seb_set_option; SEB_<NAME> in the environment sets its initial value.
-static const char *const kOptionNames[] = {
-    "build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "multi_interleave",
-    "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases", "probe_pack_first", "multi_phases", "many_splits",
-    "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys", "varlen_hash_win",
-    "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
-    "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order",
-    "lds_min_keys", "probe_phase_grid", "clear_kernel", "scatter_xcd"};
+static const OptionDesc *find_option(const char *name) {
+    for (const OptionDesc &d : kOptions)
+        if (!strcmp(d.name, name)) return &d;
+    return nullptr;
+}
 
 static std::once_flag g_env_once;
 static void load_env() {
     Options &o = options();
-    for (const char *name : kOptionNames) {
+    for (const OptionDesc &d : kOptions) {
         char var[64] = "SEB_";
         size_t j = 4;
-        for (const char *c = name; *c && j + 1 < sizeof var; ++c) var[j++] = (char)toupper((unsigned char)*c);
+        for (const char *c = d.name; *c && j + 1 < sizeof var; ++c) var[j++] = (char)toupper((unsigned char)*c);
         var[j] = 0;
         long v;
-        if (env_flag(var, &v)) set_opt(o, name, v);
+        if (env_flag(var, &v) && v >= d.lo && v <= d.hi) d.set(o, v);
     }
+}
+
+// Entry of a call that launches kernels: the knobs are loaded, and HIP's last-error state is
+// cleared, so a failed HIP call made earlier on this thread (the caller's, or an allocation the
+// library recovered from) is not reported by this call's post-launch hipGetLastError.
+static void enter() {
+    std::call_once(g_env_once, load_env);
+    (void)hipGetLastError();
 }
 
 extern "C" int seb_set_option(const char *name, int64_t value) {
     std::call_once(g_env_once, load_env);
     if (!name) return fail(SEB_ERR_INVALID, "seb_set_option: null name");
-    if (!set_opt(options(), name, value))
+    const OptionDesc *d = find_option(name);
+    if (!d || value < d->lo || value > d->hi)
         return fail(SEB_ERR_INVALID, "seb_set_option: bad option %s=%lld", name, (long long)value);
+    d->set(options(), value);
     return SEB_OK;
 }
 
 extern "C" int seb_get_option(const char *name, int64_t *value) {
     std::call_once(g_env_once, load_env);
     if (!name || !value) return fail(SEB_ERR_INVALID, "seb_get_option: null argument");
-    const Options &o = options();
-    if (!strcmp(name, "build_algo")) *value = o.build_algo;
-    else if (!strcmp(name, "probe_split")) *value = o.probe_split;
-    else if (!strcmp(name, "probe_kpt")) *value = o.probe_kpt;
-    else if (!strcmp(name, "probe_slice_shift")) *value = o.probe_slice_shift;
-    else if (!strcmp(name, "probe_slice_grid")) *value = o.probe_slice_grid;
-    else if (!strcmp(name, "multi_interleave")) *value = o.multi_interleave;
-    else if (!strcmp(name, "scatter_threads")) *value = o.scatter_threads;
-    else if (!strcmp(name, "stream_nt")) *value = o.stream_nt;
-    else if (!strcmp(name, "scatter_kpt")) *value = o.scatter_kpt;
-    else if (!strcmp(name, "probe_persistent")) *value = o.probe_persistent;
-    else if (!strcmp(name, "probe_mode")) *value = o.probe_mode;
-    else if (!strcmp(name, "probe_phases")) *value = o.probe_phases;
-    else if (!strcmp(name, "probe_pack_first")) *value = o.probe_pack_first;
-    else if (!strcmp(name, "multi_phases")) *value = o.multi_phases;
-    else if (!strcmp(name, "many_splits")) *value = o.many_splits;
-    else if (!strcmp(name, "probe_phase0_pct")) *value = o.probe_phase0_pct;
-    else if (!strcmp(name, "probe_phase0_kpt")) *value = o.probe_phase0_kpt;
-    else if (!strcmp(name, "multiget_pass_kib")) *value = o.multiget_pass_kib;
-    else if (!strcmp(name, "multiget_group")) *value = o.multiget_group;
-    else if (!strcmp(name, "multiget_order")) *value = o.multiget_order;
-    else if (!strcmp(name, "varlen_hash_keys")) *value = o.varlen_hash_keys;
-    else if (!strcmp(name, "varlen_hash_win")) *value = o.varlen_hash_win;
-    else if (!strcmp(name, "varlen_prehash_packed")) *value = o.varlen_prehash_packed;
-    else if (!strcmp(name, "build_prepack")) *value = o.build_prepack;
-    else if (!strcmp(name, "apply_threads")) *value = o.apply_threads;
-    else if (!strcmp(name, "clear_kernel")) *value = o.clear_kernel;
-    else if (!strcmp(name, "scatter_xcd")) *value = o.scatter_xcd;
-    else if (!strcmp(name, "wal_lds_kib")) *value = o.wal_lds_kib;
-    else if (!strcmp(name, "varlen_sort_min_keys")) *value = (int64_t)o.varlen_sort_min_keys;
-    else if (!strcmp(name, "varlen_prehash_min_keys")) *value = (int64_t)o.varlen_prehash_min_keys;
-    else if (!strcmp(name, "grid_cap")) *value = o.grid_cap;
-    else if (!strcmp(name, "probe_phase_grid")) *value = o.probe_phase_grid;
-    else if (!strcmp(name, "bucket_min_keys")) *value = (int64_t)o.bucket_min_keys;
-    else if (!strcmp(name, "lds_min_keys")) *value = (int64_t)o.lds_min_keys;
-    else return fail(SEB_ERR_INVALID, "seb_get_option: unknown option %s", name);
+    const OptionDesc *d = find_option(name);
+    if (!d) return fail(SEB_ERR_INVALID, "seb_get_option: unknown option %s", name);
+    *value = d->get(options());
     return SEB_OK;
 }
 
@@ -240,9 +198,10 @@ extern "C" int seb_device_check(int device) {
 // ------------------------------------------------------- device-resident entry points --------
 
 extern "C" int seb_dev_clear(uint32_t *words, uint64_t m, void *stream) {
+    enter();
     if (!words && m) return fail(SEB_ERR_INVALID, "seb_dev_clear: null words");
     if (m == 0) return SEB_OK;
-    if (options().clear_kernel && ((uintptr_t)words & 15) == 0)
+    if (((uintptr_t)words & 15) == 0)
         HIP_OR_FAIL(launch_clear_words(words, seb_words_bytes(m), (hipStream_t)stream));
     else
         HIP_OR_FAIL(hipMemsetAsync(words, 0, seb_words_bytes(m), (hipStream_t)stream));
@@ -275,7 +234,9 @@ static thread_local std::vector<std::unique_lock<std::recursive_mutex>> t_ws_hel
 // the call returns (its last launch is enqueued by then).
 struct WsCall {
     size_t mark;
-    WsCall() : mark(t_ws_held.size()) { ++t_ws_depth; }
+    WsCall() : mark(t_ws_held.size()) {
+        if (t_ws_depth++ == 0) (void)hipGetLastError();  // as enter(): no stale error from before this call
+    }
     ~WsCall() {
         while (t_ws_held.size() > mark) t_ws_held.pop_back();
         --t_ws_depth;
@@ -294,6 +255,22 @@ static WsSlot *ws_slot(int dev, hipStream_t s) {
     return g_ws.back().get();
 }
 
+// A failed hipMalloc is answered with SEB_ERR_NOMEM and HIP's error state is cleared, so a caller
+// that falls back (MultiGet's batch order) does not find it again in a later hipGetLastError.
+static int ws_alloc(void **p, uint64_t bytes) {
+    const uint64_t lim = options().workspace_limit_mib;
+    if (lim && bytes > (lim << 20))
+        return fail(SEB_ERR_NOMEM, "workspace %llu B > workspace_limit_mib %llu", (unsigned long long)bytes,
+                    (unsigned long long)lim);
+    hipError_t a = hipMalloc(p, bytes);
+    if (a != hipSuccess) {
+        *p = nullptr;
+        (void)hipGetLastError();
+        return fail(SEB_ERR_NOMEM, "workspace hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(a));
+    }
+    return SEB_OK;
+}
+
 static int cached_workspace(hipStream_t s, uint64_t bytes, void **out, int tag = 0) {
     if (t_ws_depth == 0) return fail(SEB_ERR_INVALID, "internal: library scratch requested outside a WsCall scope");
     int dev = 0;
@@ -310,15 +287,15 @@ static int cached_workspace(hipStream_t s, uint64_t bytes, void **out, int tag =
             HIP_OR_FAIL(hipFree(e.p));
             e.p = nullptr;
             e.bytes = 0;
-            hipError_t a = hipMalloc(&e.p, bytes);
-            if (a != hipSuccess) return fail(SEB_ERR_NOMEM, "workspace hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(a));
+            int rc = ws_alloc(&e.p, bytes);
+            if (rc) return rc;
             e.bytes = bytes;
             *out = e.p;
             return SEB_OK;
         }
     void *p = nullptr;
-    hipError_t a = hipMalloc(&p, bytes);
-    if (a != hipSuccess) return fail(SEB_ERR_NOMEM, "workspace hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(a));
+    int rc = ws_alloc(&p, bytes);
+    if (rc) return rc;
     sl->bufs.push_back({tag, p, bytes});
     *out = p;
     return SEB_OK;
@@ -366,32 +343,24 @@ extern "C" int seb_workspace_release(void) {
 static bool want_prehash(const KeyBatch &kb) {
     return kb.offsets && !kb.hashes && kb.n >= options().varlen_prehash_min_keys;
 }
-static bool want_len_perm(const KeyBatch &kb) {
-    return kb.offsets && !kb.perm && !want_prehash(kb) && kb.n >= options().varlen_sort_min_keys &&
-           kb.n <= 0xffffffffull;
-}
 static uint64_t prehash_bytes(const KeyBatch &kb) { return want_prehash(kb) ? ((kb.n * 16 + 255) & ~255ull) : 0; }
 // Pre-hash straight to packed residues (8 B per key) when the filter allows them (k == 7,
 // m < 2^29): the bucketed build and the phased probe then read half the bytes per key and skip
 // re-deriving the residues.
 static bool want_prehash_packed(const KeyBatch &kb, const ModArg &md) {
-    return want_prehash(kb) && options().varlen_prehash_packed && md.k == 7 && md.m < (1ull << kPackBits);
+    return want_prehash(kb) && md.k == 7 && md.m < (1ull << kPackBits);
 }
 
-// Build dispatcher: bucketed (LDS, no global atomics) or device-scope atomics; variable-length
-// batches are first put in length-bucketed order.  Scratch layout: [perm | bucketed].  `ws` /
-// `ws_bytes` may be null/0, in which case `grow` supplies scratch.
+// Build dispatcher: bucketed (LDS, no global atomics), LDS-resident or device-scope atomics;
+// large variable-length batches are pre-hashed first.  `ws` / `ws_bytes` may be null/0, in which
+// case `grow` supplies scratch.
 template <typename Grow>
 static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStream_t s, void *ws, uint64_t ws_bytes,
                           Grow &&grow) {
     if (kb.n == 0 || md.k == 0) return SEB_OK;
     const int algo = choose_build_algo(kb.n, md.m, md.k);
     const bool bucketed = algo == 2;
-    // build_prepack: fixed-width keys hashed to packed residues by a full-occupancy kernel first,
-    // so the scatter (4 waves per SIMD) only derives positions from 8-byte words
-    const bool prepack = bucketed && !kb.offsets && !kb.hashes && options().build_prepack && md.k == 7 &&
-                         md.m < (1ull << kPackBits);
-    if (bucketed && (want_prehash_packed(kb, md) || prepack)) {  // scratch: [packed residues | bucketed]
+    if (bucketed && want_prehash_packed(kb, md)) {  // scratch: [packed residues | bucketed]
         const uint64_t pack_b = (kb.n * 8 + 255) & ~255ull;
         const uint64_t need = pack_b + bucketed_workspace_bytes(kb.n, md.m, md.k);
         if (need > ws_bytes) {
@@ -399,28 +368,22 @@ static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStr
             if (rc) return rc;
             ws_bytes = need;
         }
-        if (prepack)
-            HIP_OR_FAIL(launch_pack_residues(kb, md, (uint64_t *)ws, s));
-        else
-            HIP_OR_FAIL(launch_hash_varlen_packed(kb, md, (uint64_t *)ws, s));
+        HIP_OR_FAIL(launch_hash_varlen_packed(kb, md, (uint64_t *)ws, s));
         HIP_OR_FAIL(launch_build_bucketed_packed((const uint64_t *)ws, kb.n, words, md, (uint8_t *)ws + pack_b,
                                                  ws_bytes - pack_b, s));
         return SEB_OK;
     }
-    const uint64_t pre_b = prehash_bytes(kb);
-    const uint64_t perm_b = want_len_perm(kb) ? len_perm_workspace_bytes(kb.n) : 0;
-    const uint64_t head = pre_b + perm_b;
+    const uint64_t head = prehash_bytes(kb);
     const uint64_t need = head + (bucketed ? bucketed_workspace_bytes(kb.n, md.m, md.k) : 0);
     if (need > ws_bytes) {
         int rc = grow(need, &ws);
         if (rc) return rc;
         ws_bytes = need;
     }
-    if (pre_b) {
+    if (head) {
         HIP_OR_FAIL(launch_hash_varlen(kb, (uint4 *)ws, s));
         kb.hashes = (const uint4 *)ws;
     }
-    if (perm_b) HIP_OR_FAIL(launch_len_perm(kb, (uint8_t *)ws + pre_b, perm_b, s, &kb.perm));
     if (bucketed) {
         HIP_OR_FAIL(launch_build_bucketed(kb, words, md, (uint8_t *)ws + head, ws_bytes - head, s));
         return SEB_OK;
@@ -441,30 +404,27 @@ static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStr
     return SEB_OK;
 }
 
-// Variable-length probe batches: pre-hash (or length-bucketed order) into the per-(device,
-// stream) scratch cache first.  `extra` bytes at the front of the scratch are the caller's.
+// Variable-length probe batches: pre-hash into the per-(device, stream) scratch cache first.
+// `extra` bytes at the front of the scratch are the caller's.
 static int prepare_probe_keys(KeyBatch &kb, hipStream_t s, uint64_t extra, void **ws_out) {
     const uint64_t pre_b = prehash_bytes(kb);
-    const uint64_t perm_b = want_len_perm(kb) ? len_perm_workspace_bytes(kb.n) : 0;
     *ws_out = nullptr;
-    if (extra + pre_b + perm_b == 0) return SEB_OK;
+    if (extra + pre_b == 0) return SEB_OK;
     void *ws = nullptr;
-    int rc = cached_workspace(s, extra + pre_b + perm_b, &ws);
+    int rc = cached_workspace(s, extra + pre_b, &ws);
     if (rc) return rc;
     *ws_out = ws;
     if (pre_b) {
         HIP_OR_FAIL(launch_hash_varlen(kb, (uint4 *)((uint8_t *)ws + extra), s));
         kb.hashes = (const uint4 *)((uint8_t *)ws + extra);
     }
-    if (perm_b) HIP_OR_FAIL(launch_len_perm(kb, (uint8_t *)ws + extra + pre_b, perm_b, s, &kb.perm));
     return SEB_OK;
 }
 
 // The phased probe applies to k == 7, m < 2^29 filters spanning more than one phase, with a
 // 4-byte aligned answer array.
 static bool want_phased(uint64_t n, const ModArg &md, const uint8_t *out) {
-    const Options &o = options();
-    if (o.probe_mode != 8 || md.k != 7 || md.m >= (1ull << kPackBits)) return false;
+    if (md.k != 7 || md.m >= (1ull << kPackBits)) return false;
     return probe_phase_count(md.m) > 1 && ((uintptr_t)out & 3) == 0 && n > 0;
 }
 
@@ -490,19 +450,16 @@ static int probe_dispatch(KeyBatch kb, const uint32_t *words, const ModArg &md, 
 }
 
 extern "C" uint64_t seb_dev_build_workspace_size(uint64_t n, uint64_t m, uint32_t k) {
-    std::call_once(g_env_once, load_env);
+    enter();
     if (m == 0 || n == 0) return 0;
-    // conservative: assumes a variable-length batch (length-bucketed order) as well
-    const Options &o = options();
-    const uint64_t pre_b = n >= o.varlen_prehash_min_keys ? ((n * 16 + 255) & ~255ull) : 0;
-    const uint64_t perm_b = !pre_b && n >= o.varlen_sort_min_keys && n <= 0xffffffffull ? len_perm_workspace_bytes(n) : 0;
-    const uint64_t pack_b = o.build_prepack ? ((n * 8 + 255) & ~255ull) : 0;  // packed residues (build_prepack)
-    return std::max(pre_b + perm_b, pack_b) + (choose_build_algo(n, m, k) == 2 ? bucketed_workspace_bytes(n, m, k) : 0);
+    // conservative: assumes a variable-length batch (pre-hashed) as well
+    const uint64_t pre_b = n >= options().varlen_prehash_min_keys ? ((n * 16 + 255) & ~255ull) : 0;
+    return pre_b + (choose_build_algo(n, m, k) == 2 ? bucketed_workspace_bytes(n, m, k) : 0);
 }
 
 extern "C" int seb_dev_build_ws(const seb_keys *keys, uint32_t *words, uint64_t m, uint32_t k, void *ws,
                                 uint64_t ws_bytes, void *stream) {
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc;
     if ((rc = check_keys(keys, "seb_dev_build_ws")) || (rc = check_filter_args(m, k, "seb_dev_build_ws"))) return rc;
     if (!words) return fail(SEB_ERR_INVALID, "seb_dev_build_ws: null words");
@@ -515,7 +472,7 @@ extern "C" int seb_dev_build_ws(const seb_keys *keys, uint32_t *words, uint64_t 
 
 extern "C" int seb_dev_build(const seb_keys *keys, uint32_t *words, uint64_t m, uint32_t k, void *stream) {
     WsCall ws_call;
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc;
     if ((rc = check_keys(keys, "seb_dev_build")) || (rc = check_filter_args(m, k, "seb_dev_build"))) return rc;
     if (!words) return fail(SEB_ERR_INVALID, "seb_dev_build: null words");
@@ -527,7 +484,7 @@ extern "C" int seb_dev_build(const seb_keys *keys, uint32_t *words, uint64_t m, 
 extern "C" int seb_dev_probe(const seb_keys *keys, const uint32_t *words, uint64_t m, uint32_t k, uint8_t *out,
                              void *stream) {
     WsCall ws_call;
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc;
     if ((rc = check_keys(keys, "seb_dev_probe")) || (rc = check_filter_args(m, k, "seb_dev_probe"))) return rc;
     if (!words || (!out && keys->n)) return fail(SEB_ERR_INVALID, "seb_dev_probe: null words/out");
@@ -546,7 +503,7 @@ static int check_packed_args(uint64_t m, uint32_t k, const char *who) {
 
 extern "C" int seb_dev_pack_residues(const seb_keys *keys, uint64_t m, uint32_t k, uint64_t *packed, void *stream) {
     WsCall ws_call;
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc;
     if ((rc = check_keys(keys, "seb_dev_pack_residues")) || (rc = check_packed_args(m, k, "seb_dev_pack_residues")))
         return rc;
@@ -564,7 +521,7 @@ extern "C" int seb_dev_pack_residues(const seb_keys *keys, uint64_t m, uint32_t 
 
 extern "C" int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, uint64_t m, uint32_t k,
                                     uint8_t *out, void *stream) {
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc = check_packed_args(m, k, "seb_dev_probe_packed");
     if (rc) return rc;
     if (n && (!packed || !words || !out)) return fail(SEB_ERR_INVALID, "seb_dev_probe_packed: null pointer");
@@ -579,7 +536,7 @@ extern "C" int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const ui
 extern "C" int seb_dev_probe_emit_packed(const seb_keys *keys, const uint32_t *words, uint64_t m, uint32_t k,
                                          uint8_t *out, uint64_t *packed, void *stream) {
     WsCall ws_call;
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc;
     if ((rc = check_keys(keys, "seb_dev_probe_emit_packed")) ||
         (rc = check_packed_args(m, k, "seb_dev_probe_emit_packed")))
@@ -622,7 +579,7 @@ static int fill_multi(const seb_filter_ref *filters, uint32_t nf, uint32_t mask_
 extern "C" int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *filters, uint32_t nf, void *mask,
                                    uint32_t mask_bytes, void *stream) {
     WsCall ws_call;
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc;
     MultiArg ma;
     if ((rc = check_keys(keys, "seb_dev_probe_multi")) ||
@@ -635,12 +592,7 @@ extern "C" int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *f
     void *ws = nullptr;
     if ((rc = prepare_probe_keys(kb, s, (tb + 255) & ~255ull, &ws))) return rc;
     if (tb) {
-        const ModArg &md = ma.f[0].md;
-        void *packed = nullptr;  // phased: packed residues in their own scratch (tag 1)
-        if (md.m < (1ull << kPackBits) && multi_phase_count(md.m, mask_bytes) > 1 &&
-            (rc = cached_workspace(s, kb.n * 8, &packed, 1)))
-            return rc;
-        HIP_OR_FAIL(launch_probe_interleaved(kb, ma, mask, mask_bytes, ws, (uint64_t *)packed, s));
+        HIP_OR_FAIL(launch_probe_interleaved(kb, ma, mask, mask_bytes, ws, s));
         return SEB_OK;
     }
     HIP_OR_FAIL(launch_probe_multi(kb, ma, mask, mask_bytes, s));
@@ -650,7 +602,7 @@ extern "C" int seb_dev_probe_multi(const seb_keys *keys, const seb_filter_ref *f
 extern "C" int seb_dev_probe_multi_packed(const uint64_t *packed, uint64_t n, const seb_filter_ref *filters,
                                           uint32_t nf, void *mask, uint32_t mask_bytes, void *stream) {
     WsCall ws_call;
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc;
     MultiArg ma;
     if ((rc = fill_multi(filters, nf, mask_bytes, &ma, "seb_dev_probe_multi_packed"))) return rc;
@@ -670,7 +622,7 @@ extern "C" int seb_dev_probe_multi_packed(const uint64_t *packed, uint64_t n, co
 
 extern "C" int seb_dev_or_slices(const uint32_t *slices, uint32_t num_slices, uint64_t slice_words, uint32_t *out,
                                  void *stream) {
-    std::call_once(g_env_once, load_env);
+    enter();
     if (slice_words && num_slices && (!slices || !out)) return fail(SEB_ERR_INVALID, "seb_dev_or_slices: null pointer");
     HIP_OR_FAIL(launch_or_slices(slices, num_slices, slice_words, out, (hipStream_t)stream));
     return SEB_OK;
@@ -680,7 +632,7 @@ static const uint32_t kLdsMax = 160 * 1024;
 
 extern "C" int seb_dev_build_many(const seb_keys *keys, const uint64_t *key_begin, const seb_filter_ref *filters,
                                   uint32_t nf, void *stream) {
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc;
     if ((rc = check_keys(keys, "seb_dev_build_many"))) return rc;
     if (!key_begin || (!filters && nf)) return fail(SEB_ERR_INVALID, "seb_dev_build_many: null arrays");
@@ -1087,6 +1039,59 @@ struct CtxLease {  // borrow a context from the process pool (concurrent filters
     }
 };
 
+// A lock for the filter handle: one atomic exchange to take it uncontended (Add takes it once per
+// key, so a pthread mutex's call + fence pair showed in the per-key cost), a bounded spin, then
+// yields (a waiter may be waiting on a GPU build that takes milliseconds).
+struct FilterLock {
+    std::atomic<bool> held{false};
+    void lock() {
+        for (int spin = 0; held.exchange(true, std::memory_order_acquire); ++spin) {
+            while (held.load(std::memory_order_relaxed)) {
+                if (++spin > 64) std::this_thread::yield();
+                else __builtin_ia32_pause();
+            }
+        }
+    }
+    void unlock() { held.store(false, std::memory_order_release); }
+};
+using FilterGuard = std::lock_guard<FilterLock>;
+
+// Freed filters' device word arrays, kept per device for the next filter of a similar size
+// (flushes and compactions create filters of a few sizes over and over); at most 256 MiB.
+struct DevWordsPool {
+    std::mutex mu;
+    struct Buf {
+        int device;
+        void *p;
+        uint64_t bytes;
+    };
+    std::vector<Buf> free;
+    uint64_t total = 0;
+    static constexpr uint64_t kCap = 256ull << 20;
+    void *take(int device, uint64_t bytes, uint64_t *got) {
+        std::lock_guard<std::mutex> g(mu);
+        size_t best = free.size();
+        for (size_t i = 0; i < free.size(); ++i)
+            if (free[i].device == device && free[i].bytes >= bytes && free[i].bytes <= 2 * bytes &&
+                (best == free.size() || free[i].bytes < free[best].bytes))
+                best = i;
+        if (best == free.size()) return nullptr;
+        void *p = free[best].p;
+        *got = free[best].bytes;
+        total -= free[best].bytes;
+        free.erase(free.begin() + best);
+        return p;
+    }
+    bool give(int device, void *p, uint64_t bytes) {
+        std::lock_guard<std::mutex> g(mu);
+        if (total + bytes > kCap) return false;
+        free.push_back({device, p, bytes});
+        total += bytes;
+        return true;
+    }
+};
+static DevWordsPool g_words_pool;
+
 // A filter handle.  Writers (Add, flush, Encode's host sync) hold `mu`.  A single-key MayContain
 // does not: once the host copy reflects every Add (no pending keys, host_ok) and the filter is
 // usable, `readable` is published (release) and MayContain answers from `host` with no lock, as
@@ -1095,36 +1100,65 @@ struct CtxLease {  // borrow a context from the process pool (concurrent filters
 // reader can never see freed memory; a reader racing an Add on the same filter sees bits of
 // either state, which is the reference's own contract (an unsynchronised Go Add/MayContain pair
 // is a data race there).
+//
+// Deferred Adds go to a host arena.  While every key has one length (the reference's SSTable keys
+// usually do) the arena is a fixed-stride batch and no offsets are kept: the build reads it as
+// such (16-B keys take the vector path), and the H2D copy carries the key bytes only.  The first
+// key of another length materialises the offsets.
+constexpr uint64_t kNoLen = UINT64_MAX, kMixedLen = UINT64_MAX - 1;
 struct seb_filter {
-    std::mutex mu;
+    FilterLock mu;
     uint64_t m = 0;
     uint32_t k = 0;
+    uint64_t mu_m = 0, c_m = 0;  // floor((2^64-1)/m), 2^64 mod m: the host MayContain's reductions
     uint64_t nbytes = 0;  // len(bits): ceil(m/8) for New, len(data)-12 for Decode
     int device = 0;
     uint32_t *dwords = nullptr;  // HBM copy, authoritative once allocated
     uint64_t dbytes = 0;
     std::vector<uint8_t> host;  // host copy (valid when host_ok); nbytes long for the handle's life
     bool host_ok = true;
+    bool host_zero = false;     // New, nothing built yet: the device copy starts as a memset
     std::atomic<bool> readable{false};  // host_ok, nothing pending, usable: lock-free MayContain
     std::vector<uint8_t> pend;       // deferred Add arena
-    std::vector<uint64_t> pend_off;  // n+1 offsets into pend
+    std::vector<uint64_t> pend_off;  // n+1 offsets into pend, only once lengths differ
+    uint64_t pend_n = 0;
+    uint64_t pend_len = kNoLen;      // the common key length, or kMixedLen
     uint64_t pend_cap = 64ull << 20;
 };
+
+static void set_moduli(seb_filter *f) {
+    if (f->m) {
+        f->mu_m = UINT64_MAX / f->m;
+        f->c_m = (0 - f->m) % f->m;
+    }
+}
 
 static bool usable_quiet(const seb_filter *f) {
     return f->m != 0 && f->k <= 4096 && f->nbytes >= seb_num_bytes(f->m);
 }
 
 static void publish_locked(seb_filter *f) {
-    f->readable.store(f->host_ok && f->pend_off.size() <= 1 && usable_quiet(f), std::memory_order_release);
+    f->readable.store(f->host_ok && f->pend_n == 0 && usable_quiet(f), std::memory_order_release);
+}
+
+// x mod m with mu = floor((2^64-1)/m): the Barrett estimate is at most 2 low.
+static inline uint64_t host_mod(uint64_t x, uint64_t m, uint64_t mu) {
+    const uint64_t q = (uint64_t)(((unsigned __int128)x * mu) >> 64);
+    uint64_t r = x - q * m;
+    if (r >= m) r -= m;
+    if (r >= m) r -= m;
+    return r;
 }
 
 // lsm/bloom.go:82-92 for one key on the host copy: hash1 = FNV-1a 64, hash2 = FNV-1 64
 // (:44-54), positions (h1 + i*h2) mod m with u64 wraparound (:58-67), LSB-first bit test
 // (:87), false at the first clear bit.  The positions are stepped incrementally: with
 // r = (h1 + i*h2) mod m and b = h2 mod m, the next residue is r + b mod m, less 2^64 mod m when
-// the u64 sum h1 + (i+1)*h2 wrapped: two divisions per key instead of k.
-static int host_may_contain(const uint8_t *bits, uint64_t m, uint32_t k, const uint8_t *key, uint64_t len) {
+// the u64 sum h1 + (i+1)*h2 wrapped: two Barrett reductions per key instead of k divisions.
+static int host_may_contain(const seb_filter *f, const uint8_t *key, uint64_t len) {
+    const uint8_t *bits = f->host.data();
+    const uint64_t m = f->m, c = f->c_m;
+    const uint32_t k = f->k;
     uint64_t h1 = 0xcbf29ce484222325ull, h2 = 0xcbf29ce484222325ull;
     const uint64_t P = 0x100000001b3ull;
     for (uint64_t i = 0; i < len; ++i) {
@@ -1132,8 +1166,8 @@ static int host_may_contain(const uint8_t *bits, uint64_t m, uint32_t k, const u
         h2 = (h2 * P) ^ key[i];
     }
     if (k == 0) return 1;  // no positions: the reference's loop never returns false
-    uint64_t r = h1 % m;
-    const uint64_t b = h2 % m, c = (0 - m) % m;  // 2^64 mod m
+    uint64_t r = host_mod(h1, m, f->mu_m);
+    const uint64_t b = host_mod(h2, m, f->mu_m);
     uint64_t s = h1;
     for (uint32_t i = 0;;) {
         if (!(bits[r >> 3] & (1u << (r & 7)))) return 0;
@@ -1148,18 +1182,32 @@ static int host_may_contain(const uint8_t *bits, uint64_t m, uint32_t k, const u
     }
 }
 
-static int ensure_device_copy(seb_filter *f) {
+// The device word array, on `s`: a pooled or new buffer, zeroed, then the host bits unless the
+// filter is a fresh New (all zero).
+static int ensure_device_copy(seb_filter *f, hipStream_t s) {
     if (f->dwords) return SEB_OK;
     HIP_OR_FAIL(hipSetDevice(f->device));
-    f->dbytes = std::max<uint64_t>(seb_words_bytes(f->m), (f->nbytes + 15) / 16 * 16);
-    if (f->dbytes == 0) f->dbytes = 16;
-    hipError_t e = hipMalloc((void **)&f->dwords, f->dbytes);
-    if (e != hipSuccess) {
-        f->dwords = nullptr;
-        return fail(SEB_ERR_NOMEM, "filter: hipMalloc(%llu): %s", (unsigned long long)f->dbytes, hipGetErrorString(e));
+    uint64_t want = std::max<uint64_t>(seb_words_bytes(f->m), (f->nbytes + 15) / 16 * 16);
+    if (want == 0) want = 16;
+    uint64_t got = 0;
+    void *p = g_words_pool.take(f->device, want, &got);
+    if (!p) {
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(SEB_ERR_NOMEM, "filter: hipMalloc(%llu): %s", (unsigned long long)want, hipGetErrorString(e));
+        }
+        got = want;
     }
-    HIP_OR_FAIL(hipMemset(f->dwords, 0, f->dbytes));
-    if (f->nbytes) HIP_OR_FAIL(hipMemcpy(f->dwords, f->host.data(), f->nbytes, hipMemcpyHostToDevice));
+    f->dwords = (uint32_t *)p;
+    f->dbytes = got;
+    if (f->host_zero) {
+        HIP_OR_FAIL(hipMemsetAsync(f->dwords, 0, f->dbytes, s));
+    } else {
+        const uint64_t tail = f->nbytes & ~15ull;  // zero the padding past the copied bytes
+        HIP_OR_FAIL(hipMemsetAsync((uint8_t *)f->dwords + tail, 0, f->dbytes - tail, s));
+        if (f->nbytes) HIP_OR_FAIL(hipMemcpyAsync(f->dwords, f->host.data(), f->nbytes, hipMemcpyHostToDevice, s));
+    }
     return SEB_OK;
 }
 
@@ -1173,22 +1221,34 @@ static int usable(seb_filter *f, const char *who) {
     return SEB_OK;
 }
 
-static int flush_locked(seb_filter *f) {
-    if (f->pend_off.size() <= 1) return SEB_OK;
-    int rc = usable(f, "BloomFilter.Add");
-    if (rc) return rc;
-    if ((rc = ensure_device_copy(f))) return rc;
+// OR host keys into the filter's device words on a pooled context; returns when the build is done.
+static int build_into_filter(seb_filter *f, const seb_keys *kb) {
     CtxLease L(f->device);
     if (L.rc) return L.rc;
-    seb_keys kb{f->pend.data(), f->pend_off.data(), f->pend_off.size() - 1, 0, 0};
     std::lock_guard<std::mutex> g(L.c->mu);
     HIP_OR_FAIL(hipSetDevice(f->device));
+    int rc;
+    if ((rc = ensure_device_copy(f, L.c->s_comp))) return rc;
     f->host_ok = false;  // the device copy is about to move ahead of the host copy
+    f->host_zero = false;
     f->readable.store(false, std::memory_order_relaxed);
-    if ((rc = build_device_from_host(L.c, &kb, f->dwords, mod_arg(f->m, f->k)))) return rc;
+    if ((rc = build_device_from_host(L.c, kb, f->dwords, mod_arg(f->m, f->k)))) return rc;
     HIP_OR_FAIL(hipStreamSynchronize(L.c->s_comp));
+    return SEB_OK;
+}
+
+static int flush_locked(seb_filter *f) {
+    if (f->pend_n == 0) return SEB_OK;
+    int rc = usable(f, "BloomFilter.Add");
+    if (rc) return rc;
+    const bool uniform = f->pend_len != kMixedLen;
+    seb_keys kb{f->pend.data(), uniform ? nullptr : f->pend_off.data(), f->pend_n,
+                uniform ? (uint32_t)f->pend_len : 0u, 0};
+    if ((rc = build_into_filter(f, &kb))) return rc;
     f->pend.clear();
-    f->pend_off.assign(1, 0);
+    f->pend_off.clear();
+    f->pend_n = 0;
+    f->pend_len = kNoLen;
     return SEB_OK;
 }
 
@@ -1200,19 +1260,22 @@ extern "C" seb_filter *seb_filter_new(int64_t n, double p) {
     if (!f) return nullptr;
     f->m = m;
     f->k = k;
+    set_moduli(f);
     f->nbytes = seb_num_bytes(m);
     f->device = default_device();
     f->host.assign(f->nbytes, 0);
-    f->pend_off.assign(1, 0);
-    publish_locked(f);  // an empty filter answers false everywhere
+    f->host_zero = true;
     long cap;
     if (env_flag("SEB_PENDING_CAP", &cap) && cap > 0) f->pend_cap = (uint64_t)cap;
+    // the caller's expectedKeys: room for that many 16-B keys (the arena still grows past it)
+    if (n > 0) f->pend.reserve((size_t)std::min<uint64_t>((uint64_t)n * 16, f->pend_cap));
+    publish_locked(f);  // an empty filter answers false everywhere
     return f;
 }
 
 extern "C" void seb_filter_free(seb_filter *f) {
     if (!f) return;
-    if (f->dwords) {
+    if (f->dwords && !g_words_pool.give(f->device, f->dwords, f->dbytes)) {
         (void)hipSetDevice(f->device);
         (void)hipFree(f->dwords);
     }
@@ -1221,13 +1284,24 @@ extern "C" void seb_filter_free(seb_filter *f) {
 
 extern "C" int seb_filter_add(seb_filter *f, const uint8_t *key, uint64_t len) {
     if (!f || (!key && len)) return fail(SEB_ERR_INVALID, "BloomFilter.Add: null argument");
-    std::lock_guard<std::mutex> g(f->mu);
-    int rc = usable(f, "BloomFilter.Add");
-    if (rc) return rc;
+    FilterGuard g(f->mu);
+    if (__builtin_expect(!usable_quiet(f), 0)) return usable(f, "BloomFilter.Add");
     f->readable.store(false, std::memory_order_relaxed);  // pending keys: MayContain must flush first
-    f->pend.insert(f->pend.end(), key, key + len);
-    f->pend_off.push_back(f->pend.size());
-    if (f->pend.size() >= f->pend_cap) return flush_locked(f);
+    if (len != f->pend_len) {
+        if (f->pend_len == kNoLen && len <= 0xffffffffull) {
+            f->pend_len = len;
+        } else if (f->pend_len != kMixedLen) {  // the first key of another length: keep offsets from here
+            f->pend_off.resize(f->pend_n + 1);
+            for (uint64_t i = 0; i <= f->pend_n; ++i) f->pend_off[i] = i * f->pend_len;
+            f->pend_len = kMixedLen;
+        }
+    }
+    const size_t at = f->pend.size();
+    f->pend.resize(at + len);
+    if (len) memcpy(f->pend.data() + at, key, len);
+    ++f->pend_n;
+    if (f->pend_len == kMixedLen) f->pend_off.push_back(f->pend.size());
+    if (f->pend.size() >= f->pend_cap || f->pend_n >= (1ull << 32)) return flush_locked(f);
     return SEB_OK;
 }
 
@@ -1235,19 +1309,11 @@ extern "C" int seb_filter_add_batch(seb_filter *f, const seb_keys *kb) {
     if (!f) return fail(SEB_ERR_INVALID, "BloomFilter.Add: null filter");
     int rc;
     if ((rc = check_keys(kb, "BloomFilter.Add")) || (rc = validate_offsets(kb, "BloomFilter.Add"))) return rc;
-    std::lock_guard<std::mutex> g(f->mu);
+    FilterGuard g(f->mu);
     if ((rc = usable(f, "BloomFilter.Add"))) return rc;
     if ((rc = flush_locked(f))) return rc;  // keep Add order: earlier single Adds first
-    if ((rc = ensure_device_copy(f))) return rc;
-    CtxLease L(f->device);
-    if (L.rc) return L.rc;
-    std::lock_guard<std::mutex> g2(L.c->mu);
-    HIP_OR_FAIL(hipSetDevice(f->device));
-    f->readable.store(false, std::memory_order_relaxed);
-    f->host_ok = false;
-    if ((rc = build_device_from_host(L.c, kb, f->dwords, mod_arg(f->m, f->k)))) return rc;
-    HIP_OR_FAIL(hipStreamSynchronize(L.c->s_comp));
-    return SEB_OK;
+    if (kb->n == 0) return SEB_OK;
+    return build_into_filter(f, kb);
 }
 
 extern "C" int seb_filter_may_contain_batch(seb_filter *f, const seb_keys *kb, uint8_t *out) {
@@ -1257,14 +1323,14 @@ extern "C" int seb_filter_may_contain_batch(seb_filter *f, const seb_keys *kb, u
     if ((rc = check_keys(kb, "BloomFilter.MayContain")) || (rc = validate_offsets(kb, "BloomFilter.MayContain")))
         return rc;
     if (!out && kb->n) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: null out");
-    std::lock_guard<std::mutex> g(f->mu);
+    FilterGuard g(f->mu);
     if ((rc = usable(f, "BloomFilter.MayContain"))) return rc;
     if ((rc = flush_locked(f))) return rc;
-    if ((rc = ensure_device_copy(f))) return rc;
     CtxLease L(f->device);
     if (L.rc) return L.rc;
     std::lock_guard<std::mutex> g2(L.c->mu);
     HIP_OR_FAIL(hipSetDevice(f->device));
+    if ((rc = ensure_device_copy(f, L.c->s_comp))) return rc;
     return probe_device_to_host(L.c, kb, f->dwords, mod_arg(f->m, f->k), out);
 }
 
@@ -1278,13 +1344,13 @@ extern "C" int seb_filter_may_contain(seb_filter *f, const uint8_t *key, uint64_
     if (!f) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: null filter");
     if (!key && len) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: null key");
     if (!f->readable.load(std::memory_order_acquire)) {
-        std::lock_guard<std::mutex> g(f->mu);
+        FilterGuard g(f->mu);
         int rc;
         if ((rc = usable(f, "BloomFilter.MayContain")) || (rc = flush_locked(f)) || (rc = sync_host_locked(f)))
             return rc;
         publish_locked(f);
     }
-    return host_may_contain(f->host.data(), f->m, f->k, key, len);
+    return host_may_contain(f, key, len);
 }
 
 static int sync_host_locked(seb_filter *f) {
@@ -1300,7 +1366,7 @@ extern "C" uint64_t seb_filter_encoded_size(seb_filter *f) { return f ? 12 + f->
 
 extern "C" int seb_filter_encode(seb_filter *f, uint8_t *out, uint64_t cap) {
     if (!f || !out) return fail(SEB_ERR_INVALID, "BloomFilter.Encode: null argument");
-    std::lock_guard<std::mutex> g(f->mu);
+    FilterGuard g(f->mu);
     if (cap < 12 + f->nbytes) return fail(SEB_ERR_INVALID, "BloomFilter.Encode: buffer too small");
     int rc;
     if ((rc = flush_locked(f)) || (rc = sync_host_locked(f))) return rc;
@@ -1320,9 +1386,9 @@ extern "C" seb_filter *seb_filter_decode(const uint8_t *data, uint64_t len) {
     for (int b = 0; b < 8; ++b) f->m |= (uint64_t)data[b] << (8 * b);
     for (int b = 0; b < 4; ++b) f->k |= (uint32_t)data[8 + b] << (8 * b);
     f->nbytes = len - 12;
+    set_moduli(f);
     f->device = default_device();
     f->host.assign(data + 12, data + len);
-    f->pend_off.assign(1, 0);
     publish_locked(f);  // immutable from here unless Add is called on it
     return f;
 }
@@ -1331,12 +1397,12 @@ extern "C" uint64_t seb_filter_num_bits(const seb_filter *f) { return f ? f->m :
 extern "C" uint32_t seb_filter_num_hashes(const seb_filter *f) { return f ? f->k : 0; }
 extern "C" uint64_t seb_filter_pending(seb_filter *f) {
     if (!f) return 0;
-    std::lock_guard<std::mutex> g(f->mu);
-    return f->pend_off.size() - 1;
+    FilterGuard g(f->mu);
+    return f->pend_n;
 }
 extern "C" int seb_filter_flush(seb_filter *f) {
     if (!f) return fail(SEB_ERR_INVALID, "flush: null filter");
-    std::lock_guard<std::mutex> g(f->mu);
+    FilterGuard g(f->mu);
     return flush_locked(f);
 }
 
@@ -1370,8 +1436,6 @@ struct seb_registry {
     uint32_t max_slot = 0;         // 1 + the largest slot id in use (the mask form needs <= 64)
     uint32_t part_lo = 0, part_hi = 0;  // multiget_order's partition level: lookup-ordered slots [lo, hi)
     RegLayout layout{};
-    std::vector<uint32_t> passes;  // MultiGet pass bounds over the lookup-ordered slots
-    int pass_kib = -1;             // multiget_pass_kib the bounds were computed for
     seb_ctx *ctx = nullptr;
 };
 
@@ -1473,32 +1537,8 @@ static std::vector<const RegEntry *> lookup_order(const seb_registry *r) {
     return v;
 }
 
-// Group the lookup-ordered slots into MultiGet passes of at most multiget_pass_kib of filter
-// words each (a larger filter gets a pass of its own); 0 = one pass.
-static void plan_passes(seb_registry *r, const std::vector<uint64_t> &bytes) {
-    const uint64_t budget = (uint64_t)options().multiget_pass_kib * 1024;
-    r->passes.assign(1, 0u);
-    uint64_t acc = 0;
-    for (uint32_t i = 0; i < bytes.size(); ++i) {
-        if (budget && i > r->passes.back() && acc + bytes[i] > budget) {
-            r->passes.push_back(i);
-            acc = 0;
-        }
-        acc += bytes[i];
-    }
-    r->passes.push_back((uint32_t)bytes.size());
-    r->pass_kib = options().multiget_pass_kib;
-}
-
 static int sync_registry_locked(seb_registry *r) {
-    if (!r->dirty) {
-        if (r->pass_kib != options().multiget_pass_kib) {  // the knob changed since the last sync
-            std::vector<uint64_t> bytes;
-            for (const RegEntry *e : lookup_order(r)) bytes.push_back(seb_words_bytes(e->m));
-            plan_passes(r, bytes);
-        }
-        return SEB_OK;
-    }
+    if (!r->dirty) return SEB_OK;
     HIP_OR_FAIL(hipSetDevice(r->device));
     auto order = lookup_order(r);
     std::vector<RegSlot> slots;
@@ -1557,9 +1597,6 @@ static int sync_registry_locked(seb_registry *r) {
             r->part_lo = lay.lo[L];
             r->part_hi = lay.hi[L];
         }
-    std::vector<uint64_t> bytes;
-    for (const RegEntry *e : order) bytes.push_back(seb_words_bytes(e->m));
-    plan_passes(r, bytes);
     r->dirty = false;
     return SEB_OK;
 }
@@ -1617,7 +1654,7 @@ static int check_multiget_out(seb_registry *r, uint64_t *maybe, uint16_t *cand, 
 
 static int registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t *maybe, uint16_t *cand, uint32_t cap,
                                  void *stream, const char *who) {
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc;
     if (!r) return fail(SEB_ERR_INVALID, "%s: null registry", who);
     if ((rc = check_keys(keys, who))) return rc;
@@ -1631,7 +1668,7 @@ static int registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t
     bool order_keys = true;
     if ((rc = multiget_order(r, kb, (hipStream_t)stream, &order, &order_keys))) return rc;
     HIP_OR_FAIL(launch_multiget(kb, (const RegSlot *)r->dslots.p, r->nslots, r->layout, (const uint8_t *)r->dranges.p,
-                                maybe, cand, cap, r->passes.data(), (uint32_t)r->passes.size() - 1, (hipStream_t)stream,
+                                maybe, cand, cap, (hipStream_t)stream,
                                 order, order_keys));
     return SEB_OK;
 }
@@ -1672,8 +1709,7 @@ static int registry_multiget_host_locked(seb_registry *r, const seb_keys *kb, ui
         if ((rc = multiget_order(r, dk, c->s_comp, &order, &order_keys))) return rc;
         HIP_OR_FAIL(launch_multiget(dk, (const RegSlot *)r->dslots.p, r->nslots, r->layout,
                                     (const uint8_t *)r->dranges.p, maybe ? (uint64_t *)c->out[b].p : nullptr,
-                                    maybe ? nullptr : (uint16_t *)c->out[b].p, cap, r->passes.data(),
-                                    (uint32_t)r->passes.size() - 1, c->s_comp, order, order_keys));
+                                    maybe ? nullptr : (uint16_t *)c->out[b].p, cap, c->s_comp, order, order_keys));
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
         uint8_t *dst = maybe ? (uint8_t *)(maybe + chunks[j].i0) : (uint8_t *)(cand + chunks[j].i0 * cap);
@@ -1742,7 +1778,7 @@ extern "C" int seb_registry_multiget_list_dev(seb_registry *r, const seb_keys *k
 
 extern "C" int seb_dev_shard_route(const seb_keys *keys, uint32_t bits, uint16_t *shard, uint32_t *hash,
                                    void *stream) {
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc;
     if ((rc = check_keys(keys, "seb_dev_shard_route"))) return rc;
     if (bits > 16) return fail(SEB_ERR_INVALID, "seb_dev_shard_route: shard_bits %u > 16", bits);
@@ -1756,7 +1792,7 @@ extern "C" uint64_t seb_dev_shard_partition_workspace_size(uint64_t n, uint32_t 
 
 extern "C" int seb_dev_shard_partition(const seb_keys *keys, uint32_t bits, uint32_t *perm, uint64_t *shard_begin,
                                        uint16_t *shard, void *ws, uint64_t ws_bytes, void *stream) {
-    std::call_once(g_env_once, load_env);
+    enter();
     int rc;
     if ((rc = check_keys(keys, "seb_dev_shard_partition"))) return rc;
     if (bits > 12) return fail(SEB_ERR_INVALID, "seb_dev_shard_partition: shard_bits %u > 12", bits);
@@ -1772,7 +1808,7 @@ extern "C" int seb_dev_shard_partition(const seb_keys *keys, uint32_t bits, uint
 
 extern "C" int seb_dev_wal_crc(uint8_t *data, const uint64_t *rec_off, uint64_t n, int mode, uint32_t *crc,
                                uint8_t *ok, void *stream) {
-    std::call_once(g_env_once, load_env);
+    enter();
     if (mode < SEB_WAL_CRC || mode > SEB_WAL_VERIFY) return fail(SEB_ERR_INVALID, "seb_dev_wal_crc: bad mode %d", mode);
     if (n && (!data || !rec_off)) return fail(SEB_ERR_INVALID, "seb_dev_wal_crc: null data/offsets");
     if (n && mode == SEB_WAL_VERIFY && !ok) return fail(SEB_ERR_INVALID, "seb_dev_wal_crc: VERIFY needs ok[]");

@@ -22,7 +22,6 @@ struct KeyBatch {  // device pointers
     const uint64_t *offsets;  // n+1 or nullptr
     uint64_t n;
     uint32_t stride;
-    const uint32_t *perm = nullptr;  // variable-length only: processing order (length-bucketed)
     const uint4 *hashes = nullptr;   // pre-hashed batch: (h1 lo, h1 hi, h2 lo, h2 hi) per key
 };
 
@@ -73,15 +72,13 @@ hipError_t launch_route_partition(const KeyBatch &kb, uint32_t bits, uint32_t *p
                                   uint16_t *shard_out, void *ws, uint64_t ws_bytes, hipStream_t s);
 hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mode, uint32_t *crc, uint8_t *ok,
                           hipStream_t s);
-// Passes: slots [pass_bounds[p], pass_bounds[p+1]) per launch (npasses == 0: one pass, all slots).
-// cand != null: the list form (cap u16 slots per key, one pass, any nslots) instead of masks.
+// cand != null: the list form (cap u16 slots per key, any nslots) instead of masks.
 constexpr uint32_t kRegMaxFiles = 4096;  // registry capacity (u16 slot ids, 0xFFFF = none)
 // order != null: key j answers at index order[j]; order_keys: key j is read as key order[j] of kb
 // (else kb already holds the keys in that order).
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
-                           const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap,
-                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s, const uint32_t *order,
-                           bool order_keys);
+                           const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap, hipStream_t s,
+                           const uint32_t *order, bool order_keys);
 // Key-range order for MultiGet: buckets = files of slots [lo, hi) (a disjoint, MinKey-ordered
 // level) with MinKey <= key.  *order_out stays null when the level does not apply.
 constexpr uint32_t kMgMaxBuckets = 1025;
@@ -93,43 +90,20 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
                                  const uint8_t *ranges, void *ws, uint32_t **order_out, const uint8_t **keys_out,
                                  hipStream_t s);
 
-// Process-wide tuning knobs (seb_set_option).
+// Process-wide tuning knobs (seb_set_option): the auto-dispatch thresholds, the build algorithm,
+// and the few shape choices tests force to cover both paths.  Variants measured slower were
+// removed from the kernels (DESIGN.md 8 keeps their numbers).
 struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed), 3 LDS-resident filter
     int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
     int multiget_order = 1;       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
-    int multiget_group = 0;       // MultiGet (k = 7, m < 2^31): test filters 4 at a time (1; measured slower) or one by one (0)
-    int multiget_pass_kib = 0;    // MultiGet: filter bytes per pass (0 = one pass; passes measured slower)
-    uint64_t varlen_sort_min_keys = INT64_MAX;  // length-bucketed order (measured slower; off by default)
     uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys
-    uint32_t varlen_hash_keys = 448;  // keys per pre-hash workgroup (256, 448 + split chains, 512, 1024)
-    uint32_t varlen_hash_win = 64;    // pre-hash LDS window bytes per key (48 .. 80)
-    uint32_t apply_threads = 1024;    // radix-partitioned build: apply workgroup size (256, 512, 1024)
-    int clear_kernel = 1;             // seb_dev_clear: 16-B store kernel (1) or hipMemsetAsync (0)
-    int scatter_xcd = 0;              // bucketed build: regions per (bucket, tile group of this size; 8 = per XCD), 0 = per tile
-    int varlen_prehash_packed = 1;    // pre-hash to packed residues where k == 7, m < 2^29 (0/1)
-    int build_prepack = 0;            // fixed-width bucketed build: pack residues first (full-occupancy hash), 0/1
-    int probe_split = 3;          // k == 7 probes: gathers in the first round (0: all 7 at once)
-    int probe_kpt = 2;            // k == 7 probes: keys per thread (1, 2, 4)
-    int probe_slice_shift = 19;   // k == 7, m < 2^31: sliced probe with 2^shift-word (2 MiB) slices (0 = off)
-    unsigned probe_slice_grid = 0;  // workgroups of the sliced probe (0 = one thread per KPT keys)
     uint64_t bucket_min_keys = 100000;  // auto: bucketed build from this many keys on
     uint64_t lds_min_keys = 75000;      // auto: LDS-resident build (filter <= 160 KiB) from this many keys on
-    int scatter_threads = 1024;
-    int scatter_kpt = 5;          // bucketed build, k == 7: keys per thread per round (4: 112 KiB LDS, 5: 140 KiB)
-    int stream_nt = 1;            // non-temporal loads for 16-B key batches (keeps filter lines in L2)
-    int probe_persistent = 0;     // sliced probe: persistent 1024-thread workgroups, barrier per slice (0 = off)
-    int wal_lds_kib = 36;         // WAL CRC: LDS staging window per 256-record workgroup (36 or 48)
-    int probe_phase0_pct = 0;     // phased probe: share of the filter in range 0 (0 = even split)
-    int probe_phase0_kpt = 1;     // phased probe: keys per thread in phase 0 (1, 2, 4)
     uint32_t many_splits = 0;     // batched small-filter build: workgroups per filter (0 = auto, one per CU)
-    int multi_phases = 1;         // phased interleaved multi-filter probe: ranges (1 = off, the default: measured slower
-                                  // on C5; 0 = one per 4 MiB of table; n > 1 = n ranges)
-    int probe_pack_first = 0;     // phased probe: pack residues in a streaming pass instead of in phase 0
-    int probe_phases = 0;         // phased probe: number of phases (0 = one per 4 MiB of filter)
-    int probe_mode = 8;           // k == 7 probe: 8 = phased (one launch per filter range, default); 0-6 k_probe_sliced MODE, 7 k_probe_compact
-    unsigned grid_cap = 1u << 20;
-    unsigned probe_phase_grid = 0;  // > 0: grid cap of the later probe phases (grid-stride over 4-key groups)
+    int probe_phases = 0;         // phased probe: number of filter ranges (0 = one per 4 MiB of filter)
+    unsigned grid_cap = 1u << 20; // grid-stride kernels: most workgroups per launch
+    uint64_t workspace_limit_mib = 0;  // library scratch cap (0 = none); a larger request fails SEB_ERR_NOMEM
 };
 Options &options();
 
@@ -148,11 +122,6 @@ int choose_build_algo(uint64_t n, uint64_t m, uint32_t k);
 hipError_t launch_probe(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s);
 hipError_t launch_probe_multi(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes,
                               hipStream_t s);
-// Length-bucketed order for variable-length keys: perm[i] = the i-th key in order of
-// ceil(len/4) (capped at 64 dwords), so one wave hashes keys of one length.  Scratch bytes / launch.
-uint64_t len_perm_workspace_bytes(uint64_t n);
-hipError_t launch_len_perm(const KeyBatch &kb, void *ws, uint64_t ws_bytes, hipStream_t s, const uint32_t **perm_out);
-
 // Pre-hash a variable-length batch into one uint4 (h1, h2) per key (LDS-staged byte walk).
 hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s);
 // The same pre-hash writing packed residues for filter md (k == 7, m < 2^kPackBits) instead.
@@ -161,11 +130,8 @@ hipError_t launch_hash_varlen_packed(const KeyBatch &kb, const ModArg &md, uint6
 // Interleaved multi-filter probe (all filters share (m, k), k == 7, m < 2^31): scratch bytes
 // needed for the per-call table (0 = not applicable), and the launch (table in `ws`).
 uint64_t interleaved_bytes(const MultiArg &ma, uint32_t mask_bytes);
-// packed != nullptr: phased (multi_phase_count > 1), with n * 8 bytes of packed-residue scratch.
 hipError_t launch_probe_interleaved(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes, void *ws,
-                                    uint64_t *packed, hipStream_t s);
-// Table ranges of the phased interleaved probe for filters of m bits (0: not phased).
-uint32_t multi_phase_count(uint64_t m, uint32_t mask_bytes);
+                                    hipStream_t s);
 // The same over packed residues (all filters share (m, k), k == 7, m < 2^kPackBits); `ws` holds
 // the table (interleaved_table_bytes).
 hipError_t launch_probe_interleaved_packed(const uint64_t *packed, uint64_t n, const MultiArg &ma, void *mask,
@@ -179,7 +145,7 @@ hipError_t launch_pack_residues(const KeyBatch &kb, const ModArg &md, uint64_t *
 hipError_t launch_or_slices(const uint32_t *in, uint32_t nslices, uint64_t slice_words, uint32_t *out, hipStream_t s);
 hipError_t launch_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
                                uint8_t *out, hipStream_t s);
-// Phased probe (probe_mode 8; k == 7, m < 2^kPackBits, 4-byte aligned out): one launch per word
+// Phased probe (the default for k == 7, m < 2^kPackBits, 4-byte aligned out): one launch per word
 // range of the filter (probe_phase_count of them); `packed` is 8*n bytes of scratch.
 uint64_t probe_phase_count(uint64_t m);
 // kb == nullptr: probe the packed words themselves (no phase 0 hashing).

@@ -96,39 +96,14 @@ __global__ __launch_bounds__(256) void k_probe(Src src, uint64_t n, const uint32
     }
 }
 
-// Sliced probe (k == 7, m < 2^31): a filter larger than one XCD's 4 MiB L2 is probed in
-// phases.  Each thread keeps the 7 positions of its KPT keys in registers and, in phase s, gathers
-// only the words of slice s (2^slice_shift words).  Workgroups that progress at the same pace on
-// one XCD then share a single slice in that XCD's L2 instead of thrashing the whole filter; a
-// key whose bits so far include a clear one skips its remaining gathers.  Which slice a gather
-// belongs to changes only when it is issued, never the answer.
-// MODE selects how the gathers of one thread are ordered (the answers never change):
-//   0  per position, skipping the rest of a key once a clear bit is seen.  Every gather then
-//      depends on the previous one, so a wave has a single gather in flight.
-//   1  per slice: the key's liveness is sampled once at the start of each slice, so the gathers
-//      of one slice are independent and overlap; a dead key skips the later slices.
-//   2  no slices: the 7 positions are sorted ascending (16-comparator network) and all gathers
-//      are issued back to back, so lanes of a wave sweep the filter in the same direction.
-//   3  per slice without the liveness test (every position gathered once, all independent).
-//   4  no slices: positions sorted ascending, gathered in that order with mode 0's early exit, so
-//      a workgroup generation sweeps the filter low to high without per-slice tests.
-//   5  mode 0's gathers and early exit (the same gathers are issued), ordered position-major
-//      across the thread's KPT keys: the KPT gathers of one position step are independent, so a
-//      wave keeps up to KPT gathers in flight instead of one.
-//   6  mode 4 (sorted, no slices) ordered position-major across the KPT keys like mode 5.
-template <int KPT>
-__device__ __forceinline__ void sort7(uint32_t (&p)[KPT][7], int r) {
-    constexpr int net[16][2] = {{0, 6}, {2, 3}, {4, 5}, {0, 2}, {1, 4}, {3, 6}, {0, 1}, {2, 5},
-                                {3, 4}, {1, 2}, {4, 6}, {2, 3}, {4, 5}, {1, 2}, {3, 4}, {5, 6}};
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const uint32_t a = p[r][net[c][0]], b = p[r][net[c][1]];
-        p[r][net[c][0]] = min(a, b);
-        p[r][net[c][1]] = max(a, b);
-    }
-}
-
-template <typename Src, int KPT, int MODE>
+// Sliced probe (k == 7, 2^29 <= m < 2^31, filters too large for packed residues): a filter
+// larger than one XCD's 4 MiB L2 is probed in phases.  Each thread keeps the 7 positions of its
+// KPT keys in registers and, in phase s, gathers only the words of slice s (2^slice_shift words),
+// skipping the rest of a key once a clear bit is seen.  Workgroups that progress at the same pace
+// on one XCD then share a single slice in that XCD's L2 instead of thrashing the whole filter.
+// Which slice a gather belongs to changes only when it is issued, never the answer.  (Variants
+// that put more gathers in flight per wave were measured slower)
+template <typename Src, int KPT>
 __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, const uint32_t *__restrict__ words,
                                                       ModArg md, uint8_t *__restrict__ out, uint32_t slice_shift,
                                                       uint32_t nslices) {
@@ -144,159 +119,19 @@ __global__ __launch_bounds__(256) void k_probe_sliced(Src src, uint64_t n, const
             for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
             acc[r] = i < n ? 1u : 0u;
         }
-        if constexpr (MODE == 4) {
-#pragma unroll
-            for (int r = 0; r < KPT; ++r) {
-                sort7<KPT>(pos, r);
-#pragma unroll
-                for (int q = 0; q < 7; ++q)
-                    if (acc[r] & 1u) acc[r] &= words[pos[r][q] >> 5] >> (pos[r][q] & 31);
-            }
-        } else if constexpr (MODE == 5) {
-            for (uint32_t sl = 0; sl < nslices; ++sl) {
-#pragma unroll
-                for (int q = 0; q < 7; ++q) {
-                    uint32_t v[KPT];
-#pragma unroll
-                    for (int r = 0; r < KPT; ++r) {
-                        const uint32_t w = pos[r][q] >> 5;
-                        v[r] = ~0u;
-                        if ((acc[r] & 1u) && (w >> slice_shift) == sl) v[r] = words[w];
-                    }
-#pragma unroll
-                    for (int r = 0; r < KPT; ++r) acc[r] &= v[r] >> (pos[r][q] & 31);
-                }
-            }
-        } else if constexpr (MODE == 6) {
-#pragma unroll
-            for (int r = 0; r < KPT; ++r) sort7<KPT>(pos, r);
-#pragma unroll
-            for (int q = 0; q < 7; ++q) {
-                uint32_t v[KPT];
-#pragma unroll
-                for (int r = 0; r < KPT; ++r) {
-                    v[r] = ~0u;
-                    if (acc[r] & 1u) v[r] = words[pos[r][q] >> 5];
-                }
-#pragma unroll
-                for (int r = 0; r < KPT; ++r) acc[r] &= v[r] >> (pos[r][q] & 31);
-            }
-        } else if constexpr (MODE == 2) {
-#pragma unroll
-            for (int r = 0; r < KPT; ++r) sort7<KPT>(pos, r);
-            uint32_t v[KPT][7];
-#pragma unroll
-            for (int q = 0; q < 7; ++q)
-#pragma unroll
-                for (int r = 0; r < KPT; ++r) v[r][q] = words[pos[r][q] >> 5];
+        for (uint32_t sl = 0; sl < nslices; ++sl) {
 #pragma unroll
             for (int r = 0; r < KPT; ++r)
 #pragma unroll
-                for (int q = 0; q < 7; ++q) acc[r] &= v[r][q] >> (pos[r][q] & 31);
-        } else if constexpr (MODE == 0) {
-            for (uint32_t sl = 0; sl < nslices; ++sl) {
-#pragma unroll
-                for (int r = 0; r < KPT; ++r)
-#pragma unroll
-                    for (int q = 0; q < 7; ++q) {
-                        const uint32_t w = pos[r][q] >> 5;
-                        if ((acc[r] & 1u) && (w >> slice_shift) == sl) acc[r] &= words[w] >> (pos[r][q] & 31);
-                    }
-            }
-        } else {
-            for (uint32_t sl = 0; sl < nslices; ++sl) {
-                uint32_t live[KPT];
-#pragma unroll
-                for (int r = 0; r < KPT; ++r) live[r] = MODE == 1 ? (acc[r] & 1u) : 1u;
-                uint32_t v[KPT][7];
-#pragma unroll
-                for (int r = 0; r < KPT; ++r)
-#pragma unroll
-                    for (int q = 0; q < 7; ++q) {
-                        const uint32_t w = pos[r][q] >> 5;
-                        v[r][q] = ~0u;
-                        if (live[r] && (w >> slice_shift) == sl) v[r][q] = words[w];
-                    }
-#pragma unroll
-                for (int r = 0; r < KPT; ++r)
-#pragma unroll
-                    for (int q = 0; q < 7; ++q) acc[r] &= v[r][q] >> (pos[r][q] & 31);
-            }
+                for (int q = 0; q < 7; ++q) {
+                    const uint32_t w = pos[r][q] >> 5;
+                    if ((acc[r] & 1u) && (w >> slice_shift) == sl) acc[r] &= words[w] >> (pos[r][q] & 31);
+                }
         }
 #pragma unroll
         for (int r = 0; r < KPT; ++r) {
             const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
             if (i < n) out[src.index(i)] = (uint8_t)(acc[r] & 1u);
-        }
-    }
-}
-
-// Compact sliced probe (MODE 7; k == 7, m < 2^31).  The sliced probe's L2 reuse grows with the
-// number of keys an XCD has in flight during one sweep over the slices, and holding 7 positions per
-// key in registers caps that (68 VGPRs at 2 keys per thread).  Here a key costs 4 registers: its
-// first residue r0, the two negated step addends (nb = m - b, nd = m - ((b - c) mod m)) and a word
-// of flags (bit i = the u64 sum h1 + i*h2 wrapped at step i; bit 0 = no clear bit seen yet).  Each
-// slice phase regenerates the 7 residues with 3 VALU ops per step (for_positions' recurrence) and
-// gathers, position-major across the thread's KPT keys, only the words that lie in the slice for
-// keys still alive: the same gathers and early exit as MODE 0, with KPT independent gathers per
-// step in flight.
-template <typename Src, int KPT>
-__global__ __launch_bounds__(256) void k_probe_compact(Src src, uint64_t n, const uint32_t *__restrict__ words,
-                                                       ModArg md, uint8_t *__restrict__ out, uint32_t slice_shift,
-                                                       uint32_t nslices) {
-    const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
-    const uint64_t span = (uint64_t)blockDim.x * KPT;
-    for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
-        uint32_t r0[KPT], nb[KPT], nd[KPT], fl[KPT];
-#pragma unroll
-        for (int r = 0; r < KPT; ++r) {
-            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
-            uint64_t h1 = 0, h2 = 0;
-            if (i < n) src.hash(i, h1, h2);
-            r0[r] = mod_m31(h1, m, md.mu);
-            const uint32_t b = mod_m31(h2, m, md.mu);
-            const uint32_t bc = b >= c ? b - c : b + (m - c);
-            nb[r] = m - b;
-            nd[r] = m - bc;
-            uint32_t f = i < n ? 1u : 0u;
-            uint64_t x = h1;
-#pragma unroll
-            for (uint32_t q = 1; q < 7; ++q) {
-                const uint64_t xn = x + h2;
-                f |= (xn < x ? 1u : 0u) << q;
-                x = xn;
-            }
-            fl[r] = f;
-        }
-        const uint32_t wshift = slice_shift + 5;  // residue -> slice
-        for (uint32_t sl = 0; sl < nslices; ++sl) {
-            uint32_t rc[KPT];
-#pragma unroll
-            for (int r = 0; r < KPT; ++r) rc[r] = r0[r];
-#pragma unroll
-            for (int q = 0; q < 7; ++q) {
-                if (q > 0) {
-#pragma unroll
-                    for (int r = 0; r < KPT; ++r) {
-                        const uint32_t na = (fl[r] >> q) & 1u ? nd[r] : nb[r];
-                        const uint32_t t = rc[r] - na;
-                        rc[r] = rc[r] >= na ? t : t + m;
-                    }
-                }
-                uint32_t v[KPT];
-#pragma unroll
-                for (int r = 0; r < KPT; ++r) {
-                    v[r] = ~0u;
-                    if ((fl[r] & 1u) && (rc[r] >> wshift) == sl) v[r] = words[rc[r] >> 5];
-                }
-#pragma unroll
-                for (int r = 0; r < KPT; ++r) fl[r] &= ~1u | (v[r] >> (rc[r] & 31));
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < KPT; ++r) {
-            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
-            if (i < n) out[src.index(i)] = (uint8_t)(fl[r] & 1u);
         }
     }
 }
@@ -317,7 +152,7 @@ __global__ __launch_bounds__(256) void k_pack_residues(Src src, uint64_t n, ModA
     }
 }
 
-// Sliced probe (MODE 0) from keys that also writes each key's packed residues: the root of a
+// Sliced probe from keys that also writes each key's packed residues: the root of a
 // multi-GPU probe answers a batch for its own filter and produces the broadcast form in one pass.
 template <typename Src, int KPT>
 __global__ __launch_bounds__(256) void k_probe_sliced_emit(Src src, uint64_t n, const uint32_t *__restrict__ words,
@@ -365,7 +200,7 @@ __global__ __launch_bounds__(256) void k_probe_sliced_emit(Src src, uint64_t n, 
     }
 }
 
-// ---- phased probe (MODE 8; k == 7, m < 2^29).  The sliced probe's cost is its L2 misses: its
+// ---- phased probe (k == 7, m < 2^29; the default).  The sliced probe's cost is its L2 misses: its
 // workgroups are only loosely aligned in their sweep over the slices, so each XCD refills its L2
 // with the 12 MB filter ~2.3 times per workgroup generation (profiles/r01z).  Here every phase (a
 // contiguous word range of the filter, about one L2's worth) is its own launch, so all waves of
@@ -373,14 +208,12 @@ __global__ __launch_bounds__(256) void k_probe_sliced_emit(Src src, uint64_t n, 
 // Phase 0 hashes the keys, writes their packed residues (k_pack_residues' layout) and tests the
 // positions in range 0; phase p > 0 reads the answer bytes and, for keys still alive,
 // regenerates the positions from the packed words and tests those in range p, each gather only
-// while the key's bits so far are all set (MODE 0's early exit; sampling liveness once per phase
+// while the key's bits so far are all set (the sliced probe's early exit; sampling liveness once per phase
 // so a key's gathers overlap was measured slower: more gathers).  The answer is the AND of the k
 // bits, as MayContain (lsm/bloom.go:82-92) returns.
-#ifndef SEB_PHASE_BLOCK  // diagnostic builds may change the phased probe's workgroup size
-#define SEB_PHASE_BLOCK 256
-#endif
+constexpr unsigned kPhaseBlock = 256;  // 512 measured the same
 template <typename Src, int KPT>
-__global__ __launch_bounds__(SEB_PHASE_BLOCK) void k_probe_phase0(Src src, uint64_t n, const uint32_t *__restrict__ words,
+__global__ __launch_bounds__(kPhaseBlock) void k_probe_phase0(Src src, uint64_t n, const uint32_t *__restrict__ words,
                                                       ModArg md, uint8_t *__restrict__ out,
                                                       uint64_t *__restrict__ packed, uint32_t hi) {
     const uint64_t span = (uint64_t)blockDim.x * KPT;
@@ -407,9 +240,6 @@ __global__ __launch_bounds__(SEB_PHASE_BLOCK) void k_probe_phase0(Src src, uint6
                                             packed + i);
             }
         }
-#ifdef SEB_DIAG_GATHER_PRIO  // diagnostic builds: the dependent gather chain issues ahead of hashing waves
-        __builtin_amdgcn_s_setprio(3);
-#endif
 #pragma unroll
         for (int r = 0; r < KPT; ++r)
 #pragma unroll
@@ -417,9 +247,6 @@ __global__ __launch_bounds__(SEB_PHASE_BLOCK) void k_probe_phase0(Src src, uint6
                 const uint32_t w = pos[r][q] >> 5;
                 if ((acc[r] & 1u) && w < hi) acc[r] &= words[w] >> (pos[r][q] & 31);
             }
-#ifdef SEB_DIAG_GATHER_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
 #pragma unroll
         for (int r = 0; r < KPT; ++r) {
             const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
@@ -429,10 +256,8 @@ __global__ __launch_bounds__(SEB_PHASE_BLOCK) void k_probe_phase0(Src src, uint6
 }
 
 // Phase p > 0 over words [lo, hi): thread t owns keys 4t..4t+3 (one u32 of answers, two 16-B
-// loads of packed words); `out` is 4-byte aligned (the host checks).  PMAJOR: walk the 7
-// positions of the 4 keys position-major (4 independent gathers per step) instead of key by key.
-template <bool PMAJOR>
-__global__ __launch_bounds__(SEB_PHASE_BLOCK) void k_probe_phase(const uint64_t *__restrict__ packed, uint64_t n,
+// loads of packed words); `out` is 4-byte aligned (the host checks).
+__global__ __launch_bounds__(kPhaseBlock) void k_probe_phase(const uint64_t *__restrict__ packed, uint64_t n,
                                                      const uint32_t *__restrict__ words, ModArg md,
                                                      uint8_t *__restrict__ out, uint32_t lo, uint32_t hi,
                                                      uint32_t first) {
@@ -465,59 +290,23 @@ __global__ __launch_bounds__(SEB_PHASE_BLOCK) void k_probe_phase(const uint64_t 
             for (uint32_t r = 0; r < 4; ++r) pv[r] = i0 + r < n ? packed[i0 + r] : 0ull;
         }
         uint32_t na = a;
-        if constexpr (PMAJOR) {
-            uint32_t live[4], x[4], nb[4], nd[4], f[4];
 #pragma unroll
-            for (uint32_t r = 0; r < 4; ++r) {
-                live[r] = (a >> (8 * r)) & 1u;
-                x[r] = (uint32_t)(pv[r] & kMask);
-                const uint32_t b = (uint32_t)((pv[r] >> kPackBits) & kMask);
-                f[r] = (uint32_t)(pv[r] >> (2 * kPackBits));
-                nb[r] = m - b;
-                nd[r] = m - (b >= c ? b - c : b + (m - c));
-            }
+        for (uint32_t r = 0; r < 4; ++r) {
+            uint32_t live = (a >> (8 * r)) & 1u;
+            uint32_t x = (uint32_t)(pv[r] & kMask);
+            const uint32_t b = (uint32_t)((pv[r] >> kPackBits) & kMask), f = (uint32_t)(pv[r] >> (2 * kPackBits));
+            const uint32_t nb = m - b, bc = b >= c ? b - c : b + (m - c), nd = m - bc;
 #pragma unroll
             for (int q = 0; q < 7; ++q) {
-                uint32_t v[4];
-#pragma unroll
-                for (uint32_t r = 0; r < 4; ++r) {
-                    if (q > 0) {
-                        const uint32_t d = (f[r] >> (q - 1)) & 1u ? nd[r] : nb[r];
-                        const uint32_t t = x[r] - d;
-                        x[r] = x[r] >= d ? t : t + m;
-                    }
-                    const uint32_t w = x[r] >> 5;
-                    v[r] = ~0u;
-                    if (live[r] && w >= lo && w < hi) v[r] = words[w];
+                if (q > 0) {
+                    const uint32_t d = (f >> (q - 1)) & 1u ? nd : nb;
+                    const uint32_t t = x - d;
+                    x = x >= d ? t : t + m;
                 }
-#pragma unroll
-                for (uint32_t r = 0; r < 4; ++r) live[r] &= v[r] >> (x[r] & 31);
+                const uint32_t w = x >> 5;
+                if (live && w >= lo && w < hi) live &= words[w] >> (x & 31);
             }
-#pragma unroll
-            for (uint32_t r = 0; r < 4; ++r) na &= ~((((a >> (8 * r)) & 1u) & (live[r] ^ 1u)) << (8 * r));
-        } else {
-#pragma unroll
-            for (uint32_t r = 0; r < 4; ++r) {
-                uint32_t live = (a >> (8 * r)) & 1u;
-                uint32_t x = (uint32_t)(pv[r] & kMask);
-                const uint32_t b = (uint32_t)((pv[r] >> kPackBits) & kMask), f = (uint32_t)(pv[r] >> (2 * kPackBits));
-                const uint32_t nb = m - b, bc = b >= c ? b - c : b + (m - c), nd = m - bc;
-#pragma unroll
-                for (int q = 0; q < 7; ++q) {
-                    if (q > 0) {
-                        const uint32_t d = (f >> (q - 1)) & 1u ? nd : nb;
-                        const uint32_t t = x - d;
-                        x = x >= d ? t : t + m;
-                    }
-                    const uint32_t w = x >> 5;
-#ifdef SEB_DIAG_PHASE_NO_GATHER  // diagnostic builds only (tools/diag_lib.sh): the phase without its gathers
-                    if (live && w >= lo && w < hi) live &= (uint32_t)(x != 0xFFFFFFFFu);
-#else
-                    if (live && w >= lo && w < hi) live &= words[w] >> (x & 31);
-#endif
-                }
-                na &= ~((((a >> (8 * r)) & 1u) & (live ^ 1u)) << (8 * r));
-            }
+            na &= ~((((a >> (8 * r)) & 1u) & (live ^ 1u)) << (8 * r));
         }
         if (na != a || first) {
             if (full)
@@ -528,7 +317,7 @@ __global__ __launch_bounds__(SEB_PHASE_BLOCK) void k_probe_phase(const uint64_t 
     }
 }
 
-// Sliced probe (MODE 0 gather order) over packed residues; k == 7.
+// Sliced probe over packed residues; k == 7.
 template <int KPT>
 __global__ __launch_bounds__(256) void k_probe_packed(const uint64_t *__restrict__ packed, uint64_t n,
                                                       const uint32_t *__restrict__ words, ModArg md,
@@ -570,44 +359,6 @@ __global__ __launch_bounds__(256) void k_probe_packed(const uint64_t *__restrict
         for (int r = 0; r < KPT; ++r) {
             const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
             if (i < n) out[i] = (uint8_t)(acc[r] & 1u);
-        }
-    }
-}
-
-// Persistent variant of the sliced probe: `gridDim.x` 1024-thread workgroups loop over batches of
-// 1024*KPT keys and finish each slice phase with a workgroup barrier, so all 16 waves of a CU's
-// workgroup gather from one slice at a time (workgroups on one XCD start together and do equal
-// work, which keeps them close to one slice).  Same answers as k_probe_sliced.
-template <typename Src, int KPT>
-__global__ __launch_bounds__(1024) void k_probe_sliced_pers(Src src, uint64_t n, const uint32_t *__restrict__ words,
-                                                            ModArg md, uint8_t *__restrict__ out, uint32_t slice_shift,
-                                                            uint32_t nslices) {
-    const uint64_t span = (uint64_t)blockDim.x * KPT;
-    for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
-        uint32_t pos[KPT][7];
-        uint32_t acc[KPT];
-#pragma unroll
-        for (int r = 0; r < KPT; ++r) {
-            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
-            uint64_t h1 = 0, h2 = 0;
-            if (i < n) src.hash(i, h1, h2);
-            for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
-            acc[r] = i < n ? 1u : 0u;
-        }
-        for (uint32_t sl = 0; sl < nslices; ++sl) {
-#pragma unroll
-            for (int r = 0; r < KPT; ++r)
-#pragma unroll
-                for (int q = 0; q < 7; ++q) {
-                    const uint32_t w = pos[r][q] >> 5;
-                    if ((acc[r] & 1u) && (w >> slice_shift) == sl) acc[r] &= words[w] >> (pos[r][q] & 31);
-                }
-            __syncthreads();
-        }
-#pragma unroll
-        for (int r = 0; r < KPT; ++r) {
-            const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
-            if (i < n) out[src.index(i)] = (uint8_t)(acc[r] & 1u);
         }
     }
 }
@@ -755,50 +506,6 @@ __global__ __launch_bounds__(256) void k_probe_interleaved_packed(const uint64_t
     }
 }
 
-// Phased form of the interleaved probe (the bloom probe's phased gather, §5.3 of DESIGN.md): one
-// launch per table range, so every XCD gathers from the same range while it sits in L2.  The
-// mask array carries liveness between phases (0 = every filter already said no).  Phase 0
-// hashes the keys, writes their packed residues and gathers range 0; phase p > 0 regenerates the
-// positions from the packed words of keys whose mask is still non-zero.  `first`: phase 0 run
-// from packed words (the broadcast batch of C5 at N > 1), every key starting with all bits set.
-template <typename Src, typename MaskT>
-__global__ __launch_bounds__(256) void k_probe_interleaved_phase0(Src src, uint64_t n, const MaskT *__restrict__ table,
-                                                                  ModArg md, MaskT *__restrict__ mask,
-                                                                  uint64_t *__restrict__ packed, uint32_t hi) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        uint64_t h1, h2;
-        src.hash(i, h1, h2);
-        uint32_t pos[7];
-        for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[q] = (uint32_t)p; });
-        __builtin_nontemporal_store(pack_residue(h1, h2, md), packed + i);
-        MaskT acc = (MaskT)~(MaskT)0;
-#pragma unroll
-        for (int q = 0; q < 7; ++q)
-            if (acc && pos[q] < hi) acc &= table[pos[q]];
-        mask[src.index(i)] = acc;
-    }
-}
-
-template <typename MaskT>
-__global__ __launch_bounds__(256) void k_probe_interleaved_phase(const uint64_t *__restrict__ packed, uint64_t n,
-                                                                 const MaskT *__restrict__ table, ModArg md,
-                                                                 MaskT *__restrict__ mask, uint32_t lo, uint32_t hi,
-                                                                 uint32_t first) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        MaskT acc = first ? (MaskT)~(MaskT)0 : mask[i];
-        if (!acc) continue;
-        uint32_t pos[7];
-        packed_positions(__builtin_nontemporal_load(packed + i), (uint32_t)md.m, (uint32_t)md.c, pos);
-        const MaskT in = acc;
-#pragma unroll
-        for (int q = 0; q < 7; ++q)
-            if (acc && pos[q] - lo < hi - lo) acc &= table[pos[q]];
-        if (acc != in || first) mask[i] = acc;
-    }
-}
-
 // Batched build of independent small filters (compaction outputs, lsm/compaction.go:226-333): each
 // filter's keys are split over `splits` workgroups, each holding the whole filter in LDS
 // (ds_or_b32, no global atomics while hashing), then OR-merging its image into HBM: a plain
@@ -845,40 +552,6 @@ static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
     return (unsigned)(g > cap ? cap : g);
 }
 
-// Table ranges of the phased interleaved probe: one per 4 MiB of table (0 = not phased).
-uint32_t multi_phase_count(uint64_t m, uint32_t mask_bytes) {
-    const int o = options().multi_phases;
-    if (o == 1) return 0;
-    if (o > 1) return (uint32_t)o;
-    const uint64_t bytes = m * mask_bytes;
-    const uint64_t np = (bytes + (4u << 20) - 1) >> 22;
-    return np > 1 ? (uint32_t)np : 0;
-}
-
-template <typename MaskT>
-static hipError_t interleaved_phased(const KeyBatch *kb, uint64_t n, const MaskT *table, const ModArg &md, MaskT *mask,
-                                     uint64_t *packed, uint32_t np, hipStream_t s) {
-    auto bound = [&](uint32_t p) { return (uint32_t)(md.m * p / np); };
-    uint32_t p0 = 0;
-    const unsigned g = grid_for(n, 256, options().grid_cap);
-    if (kb) {
-        hipError_t e = with_src(*kb, [&](auto src) {
-            using S = decltype(src);
-            hipLaunchKernelGGL((k_probe_interleaved_phase0<S, MaskT>), dim3(g), dim3(256), 0, s, src, n, table, md, mask,
-                               packed, bound(1));
-            return hipGetLastError();
-        });
-        if (e != hipSuccess) return e;
-        p0 = 1;
-    }
-    for (uint32_t p = p0; p < np; ++p) {
-        hipLaunchKernelGGL((k_probe_interleaved_phase<MaskT>), dim3(g), dim3(256), 0, s, packed, n, table, md, mask,
-                           bound(p), bound(p + 1), p == 0 ? 1u : 0u);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-}
 
 
 Options &options() {
@@ -915,96 +588,29 @@ static hipError_t launch_probe_t(const Src &src, uint64_t n, const uint32_t *wor
     return hipGetLastError();
 }
 
-template <typename Src, bool M32, int SPLIT>
-static hipError_t launch_probe7k(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
-                                 hipStream_t s) {
-    switch (options().probe_kpt) {
-        case 1: return launch_probe_t<Src, 7, M32, SPLIT, 1>(src, n, words, md, out, s);
-        case 4: return launch_probe_t<Src, 7, M32, SPLIT, 4>(src, n, words, md, out, s);
-        default: return launch_probe_t<Src, 7, M32, SPLIT, 2>(src, n, words, md, out, s);
-    }
+// 2 MiB of filter words per slice of the sliced probes (swept: 2^17-2^20 words).
+constexpr uint32_t kSliceShift = 19;
+
+static inline uint32_t slice_count(uint64_t m) {
+    const uint64_t nwords = (m + 31) / 32;
+    return (uint32_t)((nwords + (1ull << kSliceShift) - 1) >> kSliceShift);
 }
 
-template <typename Src, int KPT>
-static hipError_t launch_sliced_t(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
-                                  uint32_t shift, uint32_t nslices, hipStream_t s) {
-    const Options &o = options();
-    if (o.probe_persistent > 0) {
-        unsigned g = grid_for((n + KPT - 1) / KPT, 1024, (unsigned)o.probe_persistent);
-        hipLaunchKernelGGL((k_probe_sliced_pers<Src, KPT>), dim3(g), dim3(1024), 0, s, src, n, words, md, out, shift,
-                           nslices);
-        return hipGetLastError();
-    }
-    unsigned g = grid_for((n + KPT - 1) / KPT, 256, o.probe_slice_grid ? o.probe_slice_grid : o.grid_cap);
-    switch (o.probe_mode) {
-        case 1:
-            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 1>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
-                               nslices);
-            break;
-        case 2:
-            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 2>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
-                               nslices);
-            break;
-        case 4:
-            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 4>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
-                               nslices);
-            break;
-        case 3:
-            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 3>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
-                               nslices);
-            break;
-        case 5:
-            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 5>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
-                               nslices);
-            break;
-        case 6:
-            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 6>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
-                               nslices);
-            break;
-        default:
-            hipLaunchKernelGGL((k_probe_sliced<Src, KPT, 0>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift,
-                               nslices);
-    }
-    return hipGetLastError();
-}
-
-template <typename Src, int KPT>
-static hipError_t launch_compact_t(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
-                                   uint32_t shift, uint32_t nslices, hipStream_t s) {
-    const Options &o = options();
-    unsigned g = grid_for((n + KPT - 1) / KPT, 256, o.probe_slice_grid ? o.probe_slice_grid : o.grid_cap);
-    hipLaunchKernelGGL((k_probe_compact<Src, KPT>), dim3(g), dim3(256), 0, s, src, n, words, md, out, shift, nslices);
-    return hipGetLastError();
-}
-
+// k == 7 probes that are not phased: the sliced probe for m < 2^31 filters spanning more than one
+// slice, otherwise all positions of 2 keys per thread, 3 gathers first and the rest only for keys
+// still alive.
 template <typename Src, bool M32>
 static hipError_t launch_probe7(const Src &src, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
                                 hipStream_t s) {
-    const Options &o = options();
-    const uint64_t nwords = (md.m + 31) / 32;
     if constexpr (M32) {
-        if (o.probe_slice_shift > 0 && (nwords >> o.probe_slice_shift) > 0) {  // filter spans > 1 slice
-            const uint32_t nsl = (uint32_t)((nwords + (1ull << o.probe_slice_shift) - 1) >> o.probe_slice_shift);
-            if (o.probe_mode == 7) {
-                switch (o.probe_kpt) {
-                    case 2: return launch_compact_t<Src, 2>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
-                    case 6: return launch_compact_t<Src, 6>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
-                    case 8: return launch_compact_t<Src, 8>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
-                    default: return launch_compact_t<Src, 4>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
-                }
-            }
-            switch (o.probe_kpt) {
-                case 1: return launch_sliced_t<Src, 1>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
-                case 4: return launch_sliced_t<Src, 4>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
-                default: return launch_sliced_t<Src, 2>(src, n, words, md, out, o.probe_slice_shift, nsl, s);
-            }
+        if (const uint32_t nsl = slice_count(md.m); nsl > 1) {
+            const unsigned g = grid_for((n + 1) / 2, 256, options().grid_cap);
+            hipLaunchKernelGGL((k_probe_sliced<Src, 2>), dim3(g), dim3(256), 0, s, src, n, words, md, out, kSliceShift,
+                               nsl);
+            return hipGetLastError();
         }
     }
-    switch (o.probe_split) {
-        case 0: return launch_probe7k<Src, M32, 0>(src, n, words, md, out, s);
-        case 2: return launch_probe7k<Src, M32, 2>(src, n, words, md, out, s);
-        default: return launch_probe7k<Src, M32, 3>(src, n, words, md, out, s);
-    }
+    return launch_probe_t<Src, 7, M32, 3, 2>(src, n, words, md, out, s);
 }
 
 // Filter clear: one 16-B store per lane, 4 per thread (hipMemsetAsync's fill kernel took 7.0 us
@@ -1053,17 +659,19 @@ static hipError_t launch_multi_t(const Src &src, uint64_t n, const MultiArg &ma,
     return hipGetLastError();
 }
 
+// Slice of the interleaved table: 2 MiB of entries.
 template <typename MaskT>
-static hipError_t interleaved_mask(const KeyBatch &kb, const MultiArg &ma, void *mask, void *ws, uint64_t *packed,
-                                   hipStream_t s) {
+constexpr uint32_t table_slice_shift() {
+    return 21 - (sizeof(MaskT) == 1 ? 0 : sizeof(MaskT) == 2 ? 1 : sizeof(MaskT) == 4 ? 2 : 3);
+}
+
+template <typename MaskT>
+static hipError_t interleaved_mask(const KeyBatch &kb, const MultiArg &ma, void *mask, void *ws, hipStream_t s) {
     const ModArg &md = ma.f[0].md;
     MaskT *table = (MaskT *)ws;
     // valid-bit mask: filters beyond nf must read 0, which the zero-initialised entries give
     hipLaunchKernelGGL((k_interleave<MaskT>), dim3((unsigned)((md.m + 255) / 256)), dim3(256), 0, s, ma, md.m, table);
-    if (packed) return interleaved_phased<MaskT>(&kb, kb.n, table, md, (MaskT *)mask, packed,
-                                                 multi_phase_count(md.m, sizeof(MaskT)), s);
-    const uint64_t entries_per_slice_shift = 21 - (sizeof(MaskT) == 1 ? 0 : sizeof(MaskT) == 2 ? 1 : sizeof(MaskT) == 4 ? 2 : 3);
-    const uint32_t shift = (uint32_t)entries_per_slice_shift;  // 2 MiB of table per slice
+    const uint32_t shift = table_slice_shift<MaskT>();
     const uint32_t nsl = (uint32_t)((md.m + (1ull << shift) - 1) >> shift);
     return with_src(kb, [&](auto src) {
         using S = decltype(src);
@@ -1080,9 +688,7 @@ static hipError_t interleaved_mask_packed(const uint64_t *packed, uint64_t n, co
     const ModArg &md = ma.f[0].md;
     MaskT *table = (MaskT *)ws;
     hipLaunchKernelGGL((k_interleave<MaskT>), dim3((unsigned)((md.m + 255) / 256)), dim3(256), 0, s, ma, md.m, table);
-    if (const uint32_t np = multi_phase_count(md.m, sizeof(MaskT)))
-        return interleaved_phased<MaskT>(nullptr, n, table, md, (MaskT *)mask, const_cast<uint64_t *>(packed), np, s);
-    const uint32_t shift = 21 - (sizeof(MaskT) == 1 ? 0 : sizeof(MaskT) == 2 ? 1 : sizeof(MaskT) == 4 ? 2 : 3);
+    const uint32_t shift = table_slice_shift<MaskT>();
     const uint32_t nsl = (uint32_t)((md.m + (1ull << shift) - 1) >> shift);
     const unsigned g = grid_for((n + 1) / 2, 256, options().grid_cap);
     hipLaunchKernelGGL((k_probe_interleaved_packed<MaskT>), dim3(g), dim3(256), 0, s, packed, n, (const MaskT *)table, md,
@@ -1110,13 +716,13 @@ uint64_t interleaved_bytes(const MultiArg &ma, uint32_t mask_bytes) {
 }
 
 hipError_t launch_probe_interleaved(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes, void *ws,
-                                    uint64_t *packed, hipStream_t s) {
+                                    hipStream_t s) {
     if (kb.n == 0) return hipSuccess;
     switch (mask_bytes) {
-        case 1: return interleaved_mask<uint8_t>(kb, ma, mask, ws, packed, s);
-        case 2: return interleaved_mask<uint16_t>(kb, ma, mask, ws, packed, s);
-        case 4: return interleaved_mask<uint32_t>(kb, ma, mask, ws, packed, s);
-        default: return interleaved_mask<uint64_t>(kb, ma, mask, ws, packed, s);
+        case 1: return interleaved_mask<uint8_t>(kb, ma, mask, ws, s);
+        case 2: return interleaved_mask<uint16_t>(kb, ma, mask, ws, s);
+        case 4: return interleaved_mask<uint32_t>(kb, ma, mask, ws, s);
+        default: return interleaved_mask<uint64_t>(kb, ma, mask, ws, s);
     }
 }
 
@@ -1191,27 +797,20 @@ hipError_t launch_pack_residues(const KeyBatch &kb, const ModArg &md, uint64_t *
 hipError_t launch_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
                                uint8_t *out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const Options &o = options();
-    const uint64_t nwords = (md.m + 31) / 32;
-    const uint32_t shift = o.probe_slice_shift > 0 ? (uint32_t)o.probe_slice_shift : 31u;
-    const uint32_t nsl = shift >= 31 ? 1u : (uint32_t)((nwords + (1ull << shift) - 1) >> shift);
-    const unsigned g = grid_for((n + 1) / 2, 256, o.probe_slice_grid ? o.probe_slice_grid : o.grid_cap);
-    hipLaunchKernelGGL(k_probe_packed<2>, dim3(g), dim3(256), 0, s, packed, n, words, md, out, shift, nsl);
+    const unsigned g = grid_for((n + 1) / 2, 256, options().grid_cap);
+    hipLaunchKernelGGL(k_probe_packed<2>, dim3(g), dim3(256), 0, s, packed, n, words, md, out, kSliceShift,
+                       slice_count(md.m));
     return hipGetLastError();
 }
 
 hipError_t launch_probe_emit(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out,
                              uint64_t *packed, hipStream_t s) {
     if (kb.n == 0) return hipSuccess;
-    const Options &o = options();
-    const uint64_t nwords = (md.m + 31) / 32;
-    const uint32_t shift = o.probe_slice_shift > 0 ? (uint32_t)o.probe_slice_shift : 31u;
-    const uint32_t nsl = shift >= 31 ? 1u : (uint32_t)((nwords + (1ull << shift) - 1) >> shift);
-    const unsigned g = grid_for((kb.n + 1) / 2, 256, o.probe_slice_grid ? o.probe_slice_grid : o.grid_cap);
+    const unsigned g = grid_for((kb.n + 1) / 2, 256, options().grid_cap);
     return with_src(kb, [&](auto src) {
         using S = decltype(src);
         hipLaunchKernelGGL((k_probe_sliced_emit<S, 2>), dim3(g), dim3(256), 0, s, src, kb.n, words, md, out, packed,
-                           shift, nsl);
+                           kSliceShift, slice_count(md.m));
         return hipGetLastError();
     });
 }
@@ -1221,46 +820,27 @@ hipError_t launch_probe_emit(const KeyBatch &kb, const uint32_t *words, const Mo
 hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
                                uint64_t *packed, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const Options &o = options();
     const uint64_t nwords = (md.m + 31) / 32;
     const uint64_t np = probe_phase_count(md.m);
-    // probe_phase0_pct > 0: range 0 (where every key is still alive) takes that share of the
-    // filter and the other ranges split the rest evenly
-    const uint64_t pct = (uint64_t)o.probe_phase0_pct;
-    auto bound = [&](uint64_t p) {
-        if (p == 0) return 0u;
-        if (pct == 0 || np < 2 || p >= np) return (uint32_t)(nwords * p / np);
-        const uint64_t w0 = nwords * pct / 100;
-        return (uint32_t)(w0 + (nwords - w0) * (p - 1) / (np - 1));
-    };
-    hipError_t e = hipSuccess;
+    auto bound = [&](uint64_t p) { return (uint32_t)(nwords * p / np); };
+    const unsigned cap = options().grid_cap;
     uint64_t p0 = 0;
-    if (kb && o.probe_pack_first) {  // a streaming pack pass, then every range from the packed words
-        if ((e = launch_pack_residues(*kb, md, packed, s)) != hipSuccess) return e;
-        kb = nullptr;
-    }
-    if (kb) {
-        const uint32_t kpt0 = o.probe_phase0_kpt == 1 || o.probe_phase0_kpt == 4 ? (uint32_t)o.probe_phase0_kpt : 2u;
-        const unsigned g0 = grid_for((n + kpt0 - 1) / kpt0, SEB_PHASE_BLOCK, o.grid_cap);
-        e = with_src(*kb, [&](auto src) {
+    if (kb) {  // phase 0: one key per thread (2 per thread measured 3% slower)
+        const hipError_t e = with_src(*kb, [&](auto src) {
             using S = decltype(src);
-            auto k0 = kpt0 == 1 ? k_probe_phase0<S, 1> : kpt0 == 4 ? k_probe_phase0<S, 4> : k_probe_phase0<S, 2>;
-            hipLaunchKernelGGL(k0, dim3(g0), dim3(SEB_PHASE_BLOCK), 0, s, src, n, words, md, out, packed, bound(1));
+            hipLaunchKernelGGL((k_probe_phase0<S, 1>), dim3(grid_for(n, kPhaseBlock, cap)), dim3(kPhaseBlock), 0, s, src, n,
+                               words, md, out, packed, bound(1));
             return hipGetLastError();
         });
         if (e != hipSuccess) return e;
         p0 = 1;
     }
-    const unsigned g = grid_for((n + 3) / 4, SEB_PHASE_BLOCK, o.probe_phase_grid ? o.probe_phase_grid : o.grid_cap);
+    const unsigned g = grid_for((n + 3) / 4, kPhaseBlock, cap);
     for (uint64_t p = p0; p < np; ++p) {
-        const uint32_t first = p == 0 ? 1u : 0u;
-        if (o.probe_kpt == 4)
-            hipLaunchKernelGGL(k_probe_phase<true>, dim3(g), dim3(SEB_PHASE_BLOCK), 0, s, packed, n, words, md, out, bound(p),
-                               bound(p + 1), first);
-        else
-            hipLaunchKernelGGL(k_probe_phase<false>, dim3(g), dim3(SEB_PHASE_BLOCK), 0, s, packed, n, words, md, out, bound(p),
-                               bound(p + 1), first);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_probe_phase, dim3(g), dim3(kPhaseBlock), 0, s, packed, n, words, md, out, bound(p),
+                           bound(p + 1), p == 0 ? 1u : 0u);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }

@@ -69,66 +69,15 @@ __device__ __forceinline__ uint32_t test_filter(const RegSlot &sl, uint64_t h1, 
     return acc & 1u;
 }
 
-// MayContain of up to G filters side by side (k = 7, m < 2^31), bit j of `alive` = filter j
-// still to be tested; returns the filters whose 7 bits are all set.  Each filter keeps the
-// reference's early exit (a position is gathered only while its bits so far are set), so the
-// gathers are the same ones test_filter issues, but step q's gathers of the G filters are
-// independent and in flight together instead of one filter's chain after another's.  `fl` bit
-// q-1 = the u64 sum h1 + q*h2 wrapped at step q (shared by every filter: it does not depend on m).
-template <int G>
-__device__ __forceinline__ uint32_t test_group7(const RegSlot *const *sl, uint32_t alive, uint64_t h1, uint64_t h2,
-                                                uint32_t fl) {
-    uint32_t r[G], nb[G], nd[G], m[G];
-    const uint32_t *wp[G];
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-        const ModArg &md = sl[j]->md;
-        m[j] = (uint32_t)md.m;
-        const uint32_t c = (uint32_t)md.c;
-        r[j] = mod_m31(h1, m[j], md.mu);
-        const uint32_t b = mod_m31(h2, m[j], md.mu);
-        nb[j] = m[j] - b;
-        nd[j] = m[j] - (b >= c ? b - c : b + (m[j] - c));
-        wp[j] = sl[j]->words;
-    }
-#pragma unroll
-    for (int q = 0; q < 7; ++q) {
-        uint32_t w[G];
-#pragma unroll
-        for (int j = 0; j < G; ++j) w[j] = (alive >> j & 1u) ? wp[j][r[j] >> 5] : ~0u;
-#pragma unroll
-        for (int j = 0; j < G; ++j) alive &= ~((~(w[j] >> (r[j] & 31)) & 1u) << j);
-        if (q < 6) {
-            const bool cy = fl >> q & 1u;
-#pragma unroll
-            for (int j = 0; j < G; ++j) {  // r + (h2 mod m), less 2^64 mod m on a wrap, mod m
-                const uint32_t na = cy ? nd[j] : nb[j];
-                const uint32_t t = r[j] - na;
-                r[j] = r[j] >= na ? t : t + m[j];
-            }
-        }
-    }
-    return alive;
-}
-
-// One pass tests only the filters of slots [pass_lo, pass_hi) (lookup order).  With
-// multiget_pass_kib the host groups slots into passes of that many filter bytes, so the filters a
-// pass gathers from stay in each XCD's L2 (the phased probe's idea, seb_kernels.hip).  Every pass
-// re-reads, re-hashes and re-walks every key, which costs more than the L2 misses it saves on the
-// C-LSM layout (1.46 ms in one pass, 2.12 ms in 4 MiB passes): one pass is the default.  Pass 0
-// writes the mask and later passes OR into it.
-//
 // MODE 0: u64 mask, slot table in LDS.  MODE 1: candidate list, slot table in LDS.  MODE 2:
 // candidate list, slot table read from HBM/L2 (more than kMaxSlots files: an LSM past L1 holds
-// hundreds, lsm/levels.go:10-14 with ~4 MB files, lsm/compaction.go:253).  The list form always
-// runs as one pass.  GRP > 0 (k = 7, m < 2^31 registries): the L0 filters in groups of GRP and
-// the level hits as one group go through test_group7; GRP = 0 tests one filter after another.
-template <typename Src, int KFIX, bool M32, int MODE, int GRP>
+// hundreds, lsm/levels.go:10-14 with ~4 MB files, lsm/compaction.go:253).  (Testing filters 4 at a
+// time, and passes of one L2's worth of filters, were measured slower: DESIGN.md 5.7, 8.)
+template <typename Src, int KFIX, bool M32, int MODE>
 __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const RegSlot *__restrict__ gslots,
                                                   uint32_t nslots, RegLayout lay, const uint8_t *__restrict__ ranges,
                                                   uint64_t *__restrict__ maybe, uint16_t *__restrict__ cand,
-                                                  uint32_t cap, uint32_t pass_lo, uint32_t pass_hi,
-                                                  uint32_t accumulate, const uint32_t *__restrict__ order,
+                                                  uint32_t cap, const uint32_t *__restrict__ order,
                                                   uint32_t order_keys) {
     constexpr bool kLds = MODE < 2, kList = MODE > 0;
     __shared__ RegSlot lslots[kLds ? kMaxSlots : 1];
@@ -169,41 +118,10 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         auto take = [&](const RegSlot &sl) {
             if (test_filter<KFIX, M32>(sl, h1, h2)) record(sl);
         };
-        uint32_t fl = 0;  // wrap flags of h1 + q*h2, q = 1..6 (grouped tests)
-        if constexpr (GRP > 0) {
-            uint64_t x = h1;
-#pragma unroll
-            for (uint32_t q = 1; q < 7; ++q) {
-                const uint64_t xn = x + h2;
-                fl |= (uint32_t)(xn < x) << (q - 1);
-                x = xn;
-            }
-        }
-        const uint32_t s0 = lay.lo[0] > pass_lo ? lay.lo[0] : pass_lo;
-        const uint32_t s1 = lay.hi[0] < pass_hi ? lay.hi[0] : pass_hi;
-        if constexpr (GRP > 0) {
-            for (uint32_t s = s0; s < s1; s += GRP) {  // every L0 file (of this pass), GRP at a time
-                const RegSlot *grp[GRP];
-                uint32_t live = 0;
-#pragma unroll
-                for (int j = 0; j < GRP; ++j) {
-                    const bool in = s + j < s1;
-                    grp[j] = &slots[in ? s + j : s];
-                    live |= (uint32_t)in << j;
-                }
-                const uint32_t a = test_group7<GRP>(grp, live, h1, h2, fl);
-#pragma unroll
-                for (int j = 0; j < GRP; ++j)
-                    if (a >> j & 1u) record(*grp[j]);
-            }
-        } else {
-            for (uint32_t s = s0; s < s1; ++s) take(slots[s]);  // every L0 file (of this pass)
-        }
-        const RegSlot *lvl[4];
-        uint32_t lvl_live = 0;
+        for (uint32_t s = lay.lo[0]; s < lay.hi[0]; ++s) take(slots[s]);  // every L0 file
         for (uint32_t L = 1; L < 5; ++L) {
-            uint32_t lo = lay.lo[L], hi = lay.hi[L];
-            if (lo == hi || hi <= pass_lo || lo >= pass_hi) continue;  // no file of this level in the pass
+            const uint32_t lo = lay.lo[L], hi = lay.hi[L];
+            if (lo == hi) continue;
             int hit = -1;
             if (lay.nonoverlap >> L & 1u) {
                 // last file with MinKey <= key; it is the only one that can cover the key
@@ -228,31 +146,12 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                         hit = (int)s;
                 }
             }
-            if constexpr (GRP > 0) {
-                const bool in = hit >= (int)pass_lo && hit < (int)pass_hi;
-                lvl[L - 1] = &slots[in ? hit : 0];
-                lvl_live |= (uint32_t)in << (L - 1);
-            } else {
-                if (hit >= (int)pass_lo && hit < (int)pass_hi) take(slots[hit]);
-            }
-        }
-        if constexpr (GRP > 0) {
-            if (lvl_live) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (!(lvl_live >> j & 1u)) lvl[j] = lvl[__builtin_ctz(lvl_live)];
-                const uint32_t a = test_group7<4>(lvl, lvl_live, h1, h2, fl);
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (a >> j & 1u) record(*lvl[j]);
-            }
+            if (hit >= 0) take(slots[hit]);
         }
         if constexpr (kList) {
             for (uint32_t t = nc; t < cap; ++t) row[t] = 0xFFFFu;
-        } else if (!accumulate) {
+        } else {
             maybe[oi] = mask;
-        } else if (mask) {
-            maybe[oi] |= mask;
         }
     }
 }
@@ -408,44 +307,28 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
 }
 
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
-                           const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap,
-                           const uint32_t *pass_bounds, uint32_t npasses, hipStream_t s, const uint32_t *order,
-                           bool order_keys) {
+                           const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap, hipStream_t s,
+                           const uint32_t *order, bool order_keys) {
     if (kb.n == 0) return hipSuccess;
     if (!cand && nslots > kMaxSlots) return hipErrorInvalidValue;  // the mask form stages slots in LDS
     uint64_t g = (kb.n + 255) / 256;
     if (g > 65536) g = 65536;
-    const uint32_t one[2] = {0u, nslots};
-    if (npasses == 0 || cand) {
-        pass_bounds = one;
-        npasses = 1;
-    }
     const int mode = !cand ? 0 : nslots <= kMaxSlots ? 1 : 2;
     return with_src(kb, [&](auto src) {
         using S = decltype(src);
-        for (uint32_t p = 0; p < npasses; ++p) {
-            const uint32_t lo = pass_bounds[p], hi = pass_bounds[p + 1], acc = p > 0 ? 1u : 0u;
-            auto go = [&](auto kern) {
-                hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe,
-                                   cand, cap, lo, hi, acc, order, (uint32_t)(order && order_keys));
-            };
-            if (lay.all_k7_m32 && options().multiget_group) {
-                if (mode == 0) go(k_multiget<S, 7, true, 0, 4>);
-                else if (mode == 1) go(k_multiget<S, 7, true, 1, 4>);
-                else go(k_multiget<S, 7, true, 2, 4>);
-            } else if (lay.all_k7_m32) {
-                if (mode == 0) go(k_multiget<S, 7, true, 0, 0>);
-                else if (mode == 1) go(k_multiget<S, 7, true, 1, 0>);
-                else go(k_multiget<S, 7, true, 2, 0>);
-            } else {
-                if (mode == 0) go(k_multiget<S, 0, false, 0, 0>);
-                else if (mode == 1) go(k_multiget<S, 0, false, 1, 0>);
-                else go(k_multiget<S, 0, false, 2, 0>);
-            }
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe, cand,
+                               cap, order, (uint32_t)(order && order_keys));
+            return hipGetLastError();
+        };
+        if (lay.all_k7_m32) {
+            if (mode == 0) return go(k_multiget<S, 7, true, 0>);
+            if (mode == 1) return go(k_multiget<S, 7, true, 1>);
+            return go(k_multiget<S, 7, true, 2>);
         }
-        return hipSuccess;
+        if (mode == 0) return go(k_multiget<S, 0, false, 0>);
+        if (mode == 1) return go(k_multiget<S, 0, false, 1>);
+        return go(k_multiget<S, 0, false, 2>);
     });
 }
 

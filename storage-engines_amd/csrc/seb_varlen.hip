@@ -1,11 +1,11 @@
-// seb_varlen.hip — length-bucketed processing order for variable-length keys (BASELINE C4).
+// seb_varlen.hip — LDS-staged pre-hash of variable-length keys (BASELINE C4).
 //
 // The reference hashes each key with a byte-serial FNV chain (lsm/bloom.go:44-54), so a lane's
 // work is its key's length.  In a wave of 64 keys drawn from the C4 zipf lengths (8-256 B, mean
-// 40 B) almost every wave holds one long key, and the whole wave waits for it.  These kernels
-// build perm[] = the keys ordered by ceil(len/4) (a device counting sort over 65 length buckets),
-// so the build / probe kernels (KeysVarPerm) give each wave keys of one length.  Order never
-// changes a result: bits are OR-ed, and probe answers are written back to perm[i].
+// 40 B) almost every wave holds one long key, and the whole wave waits for it.  Batches of >= 64K
+// variable-length keys are therefore hashed first, here, with each workgroup sorting its own keys
+// by length in LDS; build and probe then read 16 (or 8, packed) bytes per key.  Order never changes
+// a result: every key's hashes land at its own index.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -15,74 +15,6 @@
 namespace seb {
 
 constexpr uint32_t kLenBuckets = 65;  // ceil(len/4) in [0, 64]; longer keys share bucket 64
-constexpr uint32_t kPermThreads = 1024;
-constexpr uint32_t kPermTile = 8192;  // keys per workgroup
-
-__device__ __forceinline__ uint32_t len_bucket(const uint64_t *off, uint64_t i) {
-    const uint64_t d = (off[i + 1] - off[i] + 3) >> 2;
-    return d > 64 ? 64u : (uint32_t)d;
-}
-
-// per-(bucket, tile) counts, bucket-major: counts[b * ntiles + t]
-__global__ __launch_bounds__(kPermThreads) void k_len_hist(const uint64_t *__restrict__ off, uint64_t n,
-                                                           uint32_t ntiles, uint32_t *__restrict__ counts) {
-    __shared__ uint32_t hist[kLenBuckets];
-    if (threadIdx.x < kLenBuckets) hist[threadIdx.x] = 0u;
-    __syncthreads();
-    const uint64_t k0 = (uint64_t)blockIdx.x * kPermTile;
-    const uint64_t k1 = k0 + kPermTile < n ? k0 + kPermTile : n;
-    for (uint64_t i = k0 + threadIdx.x; i < k1; i += blockDim.x) atomicAdd(&hist[len_bucket(off, i)], 1u);
-    __syncthreads();
-    if (threadIdx.x < kLenBuckets) counts[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = hist[threadIdx.x];
-}
-
-// exclusive scan of counts[0, len) in place, one workgroup: each thread owns a contiguous run
-__global__ __launch_bounds__(kPermThreads) void k_len_scan(uint32_t *__restrict__ counts, uint32_t len) {
-    __shared__ uint32_t wsum[kPermThreads / 64];
-    const uint32_t per = (len + blockDim.x - 1) / blockDim.x;
-    const uint32_t b0 = threadIdx.x * per;
-    uint32_t s = 0;
-    for (uint32_t j = 0; j < per; ++j)
-        if (b0 + j < len) s += counts[b0 + j];
-    // block exclusive scan of s
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t v = s;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(v, d, 64);
-        if (lane >= (uint32_t)d) v += y;
-    }
-    if (lane == 63) wsum[wid] = v;
-    __syncthreads();
-    if (wid == 0) {
-        uint32_t t = lane < nw ? wsum[lane] : 0u;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            uint32_t y = __shfl_up(t, d, 64);
-            if (lane >= (uint32_t)d) t += y;
-        }
-        if (lane < nw) wsum[lane] = t;
-    }
-    __syncthreads();
-    uint32_t run = (wid ? wsum[wid - 1] : 0u) + v - s;
-    for (uint32_t j = 0; j < per; ++j)
-        if (b0 + j < len) {
-            const uint32_t c = counts[b0 + j];
-            counts[b0 + j] = run;
-            run += c;
-        }
-}
-
-__global__ __launch_bounds__(kPermThreads) void k_len_scatter(const uint64_t *__restrict__ off, uint64_t n,
-                                                              uint32_t ntiles, const uint32_t *__restrict__ counts,
-                                                              uint32_t *__restrict__ perm) {
-    __shared__ uint32_t cur[kLenBuckets];
-    if (threadIdx.x < kLenBuckets) cur[threadIdx.x] = counts[(uint64_t)threadIdx.x * ntiles + blockIdx.x];
-    __syncthreads();
-    const uint64_t k0 = (uint64_t)blockIdx.x * kPermTile;
-    const uint64_t k1 = k0 + kPermTile < n ? k0 + kPermTile : n;
-    for (uint64_t i = k0 + threadIdx.x; i < k1; i += blockDim.x) perm[atomicAdd(&cur[len_bucket(off, i)], 1u)] = (uint32_t)i;
-}
 
 // ---- pre-hash: (h1, h2) of every variable-length key, written as one uint4 per key.
 // A workgroup owns kHashKeys consecutive keys.  It copies their byte span (16-B aligned chunks,
@@ -320,40 +252,17 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
     put_hash<PACK>(hashes, k0 + slot_idx[t], h1, h2, md);
 }
 
-template <uint32_t KEYS, bool PACK>
-static hipError_t launch_hash_varlen_keys(const KeyBatch &kb, void *out, const ModArg &md, uint32_t win,
-                                          hipStream_t s) {
-    // 1024-key workgroups: the window is at most 56 B per key (16-bit window offsets); two such
-    // workgroups (55 KB of LDS each) share a CU
-    void (*k)(const uint8_t *, const uint64_t *, uint64_t, void *, ModArg);
-    // 448 / 384 keys: 512 threads, the top 64 / 128 keys split over chain waves
-    constexpr uint32_t ns = KEYS == 448 ? 1u : KEYS == 384 ? 2u : 0u;
-    if constexpr (KEYS == 1024)
-        k = win <= 48 ? k_hash_varlen<1024, 48, PACK> : k_hash_varlen<1024, 56, PACK>;
-    else if constexpr (ns > 0)
-        k = win <= 64 ? k_hash_varlen<KEYS, 64, PACK, ns>
-            : win == 72 ? k_hash_varlen<KEYS, 72, PACK, ns>
-                        : k_hash_varlen<KEYS, 80, PACK, ns>;
-    else
-        k = win == 48   ? k_hash_varlen<KEYS, 48, PACK>
-            : win == 56 ? k_hash_varlen<KEYS, 56, PACK>
-            : win == 64 ? k_hash_varlen<KEYS, 64, PACK>
-            : win == 72 ? k_hash_varlen<KEYS, 72, PACK>
-                        : k_hash_varlen<KEYS, 80, PACK>;
-    const uint64_t ntiles = (kb.n + KEYS - 1) / KEYS;
-    hipLaunchKernelGGL(k, dim3((unsigned)ntiles), dim3(KEYS + 64 * ns), 0, s, kb.data, kb.offsets, kb.n, out, md);
-    return hipGetLastError();
-}
+// 448 keys per 512-thread workgroup, the top 64 split over two chain waves, a 64-B window per key
+// (256/384/512/1024-key workgroups and 48-80-B windows measured slower).
+constexpr uint32_t kVarKeys = 448, kVarWin = 64, kVarSplit = 1;
 
 template <bool PACK>
 static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const ModArg &md, hipStream_t s) {
     if (!kb.offsets || kb.n == 0) return hipSuccess;
-    const Options &o = options();
-    if (o.varlen_hash_keys == 256) return launch_hash_varlen_keys<256, PACK>(kb, out, md, o.varlen_hash_win, s);
-    if (o.varlen_hash_keys == 1024) return launch_hash_varlen_keys<1024, PACK>(kb, out, md, o.varlen_hash_win, s);
-    if (o.varlen_hash_keys == 448) return launch_hash_varlen_keys<448, PACK>(kb, out, md, o.varlen_hash_win, s);
-    if (o.varlen_hash_keys == 384) return launch_hash_varlen_keys<384, PACK>(kb, out, md, o.varlen_hash_win, s);
-    return launch_hash_varlen_keys<512, PACK>(kb, out, md, o.varlen_hash_win, s);
+    const uint64_t ntiles = (kb.n + kVarKeys - 1) / kVarKeys;
+    hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, kVarSplit>), dim3((unsigned)ntiles),
+                       dim3(kVarKeys + 64 * kVarSplit), 0, s, kb.data, kb.offsets, kb.n, out, md);
+    return hipGetLastError();
 }
 
 hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s) {
@@ -363,25 +272,6 @@ hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s) 
 hipError_t launch_hash_varlen_packed(const KeyBatch &kb, const ModArg &md, uint64_t *packed, hipStream_t s) {
     if (md.k != 7 || md.m >= (1ull << kPackBits)) return hipErrorInvalidValue;
     return launch_hash_varlen_any<true>(kb, packed, md, s);
-}
-
-uint64_t len_perm_workspace_bytes(uint64_t n) {
-    const uint64_t ntiles = (n + kPermTile - 1) / kPermTile;
-    return ((n * 4 + 255) & ~255ull) + ((kLenBuckets * ntiles * 4 + 255) & ~255ull);
-}
-
-hipError_t launch_len_perm(const KeyBatch &kb, void *ws, uint64_t ws_bytes, hipStream_t s, const uint32_t **perm_out) {
-    *perm_out = nullptr;
-    if (!kb.offsets || kb.n == 0) return hipSuccess;
-    if (kb.n > 0xffffffffull || ws_bytes < len_perm_workspace_bytes(kb.n)) return hipErrorInvalidValue;
-    const uint32_t ntiles = (uint32_t)((kb.n + kPermTile - 1) / kPermTile);
-    uint32_t *perm = (uint32_t *)ws;
-    uint32_t *counts = (uint32_t *)((uint8_t *)ws + ((kb.n * 4 + 255) & ~255ull));
-    hipLaunchKernelGGL(k_len_hist, dim3(ntiles), dim3(kPermThreads), 0, s, kb.offsets, kb.n, ntiles, counts);
-    hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(kPermThreads), 0, s, counts, kLenBuckets * ntiles);
-    hipLaunchKernelGGL(k_len_scatter, dim3(ntiles), dim3(kPermThreads), 0, s, kb.offsets, kb.n, ntiles, counts, perm);
-    *perm_out = perm;
-    return hipGetLastError();
 }
 
 }  // namespace seb

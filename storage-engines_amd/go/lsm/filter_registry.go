@@ -11,6 +11,7 @@ package lsm
 
 /*
 #include <stdint.h>
+#include <stdlib.h>
 #include "seb_bloom.h"
 */
 import "C"
@@ -78,7 +79,14 @@ func (r *FilterRegistry) Candidates(keys []string) [][]uint64 {
 		return out
 	}
 	data, offs := packKeys(keys)
-	ks := C.seb_keys{data: (*C.uint8_t)(unsafe.Pointer(&data[0])), offsets: (*C.uint64_t)(unsafe.Pointer(&offs[0])),
+	// the seb_keys struct holds Go pointers: it lives in C memory and what it points to is pinned
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	pin.Pin(&data[0])
+	pin.Pin(&offs[0])
+	ks := (*C.seb_keys)(C.malloc(C.size_t(unsafe.Sizeof(C.seb_keys{}))))
+	defer C.free(unsafe.Pointer(ks))
+	*ks = C.seb_keys{data: (*C.uint8_t)(unsafe.Pointer(&data[0])), offsets: (*C.uint64_t)(unsafe.Pointer(&offs[0])),
 		n: C.uint64_t(len(keys))}
 	// One C call sizes the rows, runs the lookup and maps slots to file numbers under the
 	// registry's lock, so a concurrent flush (Put) or compaction (Remove + Put reusing the slot)
@@ -92,7 +100,7 @@ func (r *FilterRegistry) Candidates(keys []string) [][]uint64 {
 	for {
 		files = make([]uint64, len(keys)*int(capRow))
 		var need C.uint32_t
-		rc := C.seb_registry_multiget_files(r.h, &ks, (*C.uint64_t)(unsafe.Pointer(&files[0])), capRow, &need)
+		rc := C.seb_registry_multiget_files(r.h, ks, (*C.uint64_t)(unsafe.Pointer(&files[0])), capRow, &need)
 		if rc == C.int(C.SEB_ERR_RANGE) && need > capRow {
 			capRow = need
 			continue

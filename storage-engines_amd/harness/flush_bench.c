@@ -13,7 +13,8 @@
  *                                       filter (lsm/lsm.go:166 releases the RLock before the loop)
  *
  * usage: flush_bench [--reps R] [--threads T] N...
- * Prints one JSON line: per N, median microseconds of New / Add loop / Encode / Free, sha256 of
+ * Prints one JSON line: per N, median microseconds of New / Add loop / Encode / Free, the same
+ * build in the cgo shim's pattern (keys buffered caller-side, one seb_filter_add_batch), sha256 of
  * Encode(), single-key MayContain ns per call on 1 and T threads, and the batched GPU MayContain.
  * Keys are key16(i) (common/benchmark/keygen.go:89-109); probes q < N: even q -> key16(q), odd
  * q -> key16(N + q).  Test/bench infrastructure; the cgo crossing itself (tens of ns per call in
@@ -63,8 +64,8 @@ static void *reader(void *p) {
     pthread_barrier_wait(a->bar);
     double t0 = now_us();
     uint64_t pos = 0;
-    for (uint64_t c = 0; c < a->calls; c++) {
-        uint64_t q = (a->start + c) % a->n;
+    uint64_t q = a->start % a->n;
+    for (uint64_t c = 0; c < a->calls; c++, q = q + 1 == a->n ? 0 : q + 1) {
         int r = seb_filter_may_contain(a->f, a->keys + 16 * q, 16);
         if (r < 0) die("MayContain");
         pos += (uint64_t)r;
@@ -145,6 +146,33 @@ int main(int argc, char **argv) {
         char henc[65];
         digest(enc, esz, henc);
 
+        /* The cgo shim's pattern (storage-engines_amd/go/lsm/bloom.go): Add appends the key to a
+         * Go-side arena with no cgo crossing, and the first Encode / MayContain hands the arena
+         * over in one seb_filter_add_batch call.  Here the arena is a C buffer. */
+        double s_add[1000], s_batch[1000], s_enc[1000], s_all[1000];
+        uint8_t *arena = malloc(16 * n);
+        for (int r = -1; r < reps; r++) {
+            double t0 = now_us();
+            seb_filter *f = seb_filter_new((int64_t)n, 0.01);
+            if (!f) die("NewBloomFilter");
+            for (uint64_t i = 0; i < n; i++) memcpy(arena + 16 * i, keys + 16 * i, 16);
+            double t1 = now_us();
+            seb_keys ab = {arena, NULL, n, 16, 0};
+            if (seb_filter_add_batch(f, &ab) != SEB_OK) die("AddBatch");
+            double t2 = now_us();
+            if (seb_filter_encode(f, enc, esz) != SEB_OK) die("Encode");
+            double t3 = now_us();
+            seb_filter_free(f);
+            if (r >= 0) s_add[r] = t1 - t0, s_batch[r] = t2 - t1, s_enc[r] = t3 - t2, s_all[r] = t3 - t0;
+        }
+        char henc2[65];
+        digest(enc, esz, henc2);
+        free(arena);
+        if (strcmp(henc, henc2) != 0) {
+            fprintf(stderr, "shim-pattern Encode differs at n=%" PRIu64 "\n", n);
+            return 1;
+        }
+
         seb_filter *g = seb_filter_decode(enc, esz);
         if (!g) die("DecodeBloomFilter");
         double ns1 = 0, nsT = 0, t_one[1000], t_b[1000];
@@ -179,13 +207,17 @@ int main(int argc, char **argv) {
         printf("%s{\"n\": %" PRIu64 ", \"encode_len\": %" PRIu64 ", \"encode_sha256\": \"%s\", "
                "\"build_us\": {\"new\": %.2f, \"add_loop\": %.2f, \"encode\": %.2f, \"free\": %.2f, \"total\": %.2f}, "
                "\"add_ns_per_key\": %.2f, \"build_keys_per_s\": %.0f, "
+               "\"shim_us\": {\"arena\": %.2f, \"add_batch\": %.2f, \"encode\": %.2f, \"total\": %.2f}, "
+               "\"shim_keys_per_s\": %.0f, "
                "\"may_contain\": {\"ns_per_call_1t\": %.2f, \"calls_per_s_1t\": %.0f, \"threads\": %d, "
                "\"ns_per_call_per_thread\": %.2f, \"calls_per_s\": %.0f}, "
                "\"batch_us\": %.2f, \"probe_positives\": %" PRIu64 ", \"probe_sha256\": \"%s\", "
                "\"batch_matches_single\": %s}",
                s ? ", " : "", n, esz, henc, median(t_new, reps), median(t_add, reps), median(t_enc, reps),
                median(t_free, reps), median(t_all, reps), median(t_add, reps) * 1e3 / (double)n,
-               (double)n / (median(t_all, reps) * 1e-6), ns1, rate1, threads, nsT, rateT, median(t_batch, reps),
+               (double)n / (median(t_all, reps) * 1e-6), median(s_add, reps), median(s_batch, reps),
+               median(s_enc, reps), median(s_all, reps), (double)n / (median(s_all, reps) * 1e-6), ns1, rate1,
+               threads, nsT, rateT, median(t_batch, reps),
                positives, hans, same ? "true" : "false");
         free(keys), free(pk), free(ans1), free(ansb), free(enc);
         if (!same) {

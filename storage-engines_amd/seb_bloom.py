@@ -174,7 +174,7 @@ def words_bytes(m: int) -> int:
 
 
 def set_option(name: str, value: int) -> None:
-    """Tuning knob (build_algo, probe_split, bucket_min_keys, grid_cap); results never change."""
+    """Tuning knob (build_algo, probe_phases, bucket_min_keys, grid_cap, ...); results never change."""
     check(lib().seb_set_option(name.encode(), int(value)))
 
 

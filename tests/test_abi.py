@@ -110,23 +110,23 @@ def test_no_silent_fallback_without_library(seb, monkeypatch, tmp_path):
         mod.params(10, 0.01)
 
 
-OPTION_NAMES = ["build_algo", "probe_split", "probe_kpt", "probe_slice_shift", "probe_slice_grid", "multi_interleave",
-                "scatter_threads", "stream_nt", "scatter_kpt", "probe_persistent", "probe_mode", "probe_phases",
-                "probe_pack_first", "multi_phases", "many_splits", "probe_phase0_pct", "probe_phase0_kpt", "multiget_pass_kib", "varlen_hash_keys",
-                "varlen_hash_win", "apply_threads", "varlen_prehash_packed", "wal_lds_kib", "varlen_sort_min_keys",
-                "varlen_prehash_min_keys", "grid_cap", "bucket_min_keys", "build_prepack", "multiget_group", "multiget_order", "lds_min_keys", "probe_phase_grid"]
+OPTION_NAMES = ["build_algo", "multi_interleave", "multiget_order", "varlen_prehash_min_keys", "bucket_min_keys",
+                "lds_min_keys", "many_splits", "probe_phases", "grid_cap", "workspace_limit_mib"]
 
 
 def test_options_round_trip_and_reject_bad_values(seb):
-    """Every knob reads back what was set, bad values are refused and leave the knob unchanged."""
+    """Every knob reads back what was set, bad values are refused and leave the knob unchanged; the
+    rejected variants of earlier rounds are gone from the library."""
     for name in OPTION_NAMES:
         old = seb.get_option(name)
         seb.set_option(name, old)
         assert seb.get_option(name) == old
-    with seb.option("apply_threads", 512):
-        assert seb.get_option("apply_threads") == 512
-    for name, bad in (("apply_threads", 300), ("varlen_hash_win", 50), ("probe_mode", 9), ("nonexistent", 1)):
-        before = seb.get_option(name) if name != "nonexistent" else None
+    with seb.option("probe_phases", 5):
+        assert seb.get_option("probe_phases") == 5
+    for name, bad in (("build_algo", 4), ("probe_phases", 65), ("many_splits", -1), ("grid_cap", 0),
+                      ("multiget_order", 2), ("nonexistent", 1), ("probe_mode", 8), ("scatter_xcd", 0),
+                      ("clear_kernel", 1)):
+        before = seb.get_option(name) if name in OPTION_NAMES else None
         with pytest.raises(seb.SebError):
             seb.set_option(name, bad)
         if before is not None:
@@ -136,11 +136,11 @@ def test_options_round_trip_and_reject_bad_values(seb):
 def test_options_from_environment(seb):
     """SEB_<NAME> sets a knob's initial value in a fresh process; an out-of-range value is ignored."""
     code = ("import sys; sys.path.insert(0, 'storage-engines_amd'); import seb_bloom as s; "
-            "print(s.get_option('apply_threads'), s.get_option('varlen_hash_win'), s.get_option('probe_phases'))")
+            "print(s.get_option('many_splits'), s.get_option('build_algo'), s.get_option('probe_phases'))")
     import os
-    env = dict(os.environ, SEB_APPLY_THREADS="512", SEB_VARLEN_HASH_WIN="13", SEB_PROBE_PHASES="5")
+    env = dict(os.environ, SEB_MANY_SPLITS="12", SEB_BUILD_ALGO="13", SEB_PROBE_PHASES="5")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run(["python", "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
-    apply, win, phases = map(int, out.stdout.split())
-    assert apply == 512 and phases == 5
-    assert win == 64  # 13 is not a valid window: the default stays
+    splits, algo, phases = map(int, out.stdout.split())
+    assert splits == 12 and phases == 5
+    assert algo == 0  # 13 is not a valid build_algo: the default stays

@@ -111,6 +111,45 @@ def test_go_api_variable_keys_and_empty_key(seb, torch_cuda):
     assert np.array_equal(f.may_contain_batch(probes), refp)
 
 
+def test_go_api_uniform_then_mixed_lengths_and_republish(seb, torch_cuda):
+    """The Add arena keeps no offsets while every key has one length (a fixed-stride build), and
+    materialises them at the first key of another length; MayContain after more Adds sees them
+    (the lock-free host copy is republished), from several threads at once."""
+    import threading
+
+    rng = np.random.default_rng(9)
+    fixed = [kg.key16_bytes(i) for i in range(3000)]
+    mixed = [bytes(rng.integers(0, 256, int(L), dtype=np.uint8)) for L in rng.integers(0, 40, 1000)]
+    f = seb.BloomFilter(4000, 0.01)
+    m, k = f.num_bits, f.num_hashes
+    for key in fixed[:2000]:
+        f.add(key)
+    assert f.may_contain(fixed[0]) and f.pending == 0  # flushed as one stride-16 batch
+    for key in fixed[2000:] + mixed:
+        f.add(key)
+    keys = fixed + mixed
+    lens = np.array([len(x) for x in keys], np.uint64)
+    off = np.zeros(len(keys) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    ref = oc.build(m, k, np.frombuffer(b"".join(keys), np.uint8), len(keys), offsets=off)
+    probes = keys[::3] + [bytes(rng.integers(0, 256, 16, dtype=np.uint8)) for _ in range(3000)]
+    pb = seb.as_keys(probes)
+    want = oc.probe(ref, m, k, pb.data, pb.n, offsets=pb.offsets)
+    results = [None] * 8
+
+    def reader(t):
+        results[t] = np.array([f.may_contain(p) for p in probes], np.uint8)
+
+    threads = [threading.Thread(target=reader, args=(t,)) for t in range(8)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    for r in results:
+        assert np.array_equal(r, want)
+    assert f.encode()[12:] == ref.tobytes()
+
+
 def test_go_api_errors_match_reference_panics(seb, torch_cuda):
     z = seb.BloomFilter.decode(bytes(12))  # numBits 0: Go panics with divide by zero
     with pytest.raises(seb.SebError):
@@ -165,29 +204,21 @@ def test_host_api_chunked_pipeline(seb, monkeypatch, torch_cuda):
 
 # --------------------------------------------------------- device-resident API --------------
 
-@pytest.fixture(params=[(1, 1024, 4, 1024, 0, 0), (2, 1024, 4, 256, 0, 0), (2, 512, 4, 512, 0, 0),
-                        (2, 1024, 5, 1024, 0, 0), (2, 1024, 5, 1024, 1, 0), (3, 1024, 5, 1024, 0, 0),
-                        (2, 1024, 5, 1024, 0, 8), (2, 512, 4, 256, 1, 16)],
-                ids=["atomic", "bucketed", "bucketed512", "bucketed-kpt5", "bucketed-prepack", "lds",
-                     "bucketed-xcd8", "bucketed512-prepack-grp16"])
+@pytest.fixture(params=[1, 2, 3], ids=["atomic", "bucketed", "lds"])
 def build_algo(request, seb):
-    """Build paths: device-scope atomics, radix-partitioned (several geometries, regions per tile
-    or per tile group), and the LDS-resident filter (algo 3; a filter over 160 KiB falls back to
-    atomics)."""
-    algo, thr, kpt, apply, prepack, grp = request.param
-    with seb.option("build_algo", algo), seb.option("scatter_threads", thr), seb.option("scatter_kpt", kpt), \
-            seb.option("apply_threads", apply), seb.option("build_prepack", prepack), seb.option("scatter_xcd", grp):
-        yield algo
+    """Build paths: device-scope atomics, radix-partitioned (bucketed), and the LDS-resident filter
+    (algo 3; a filter over 160 KiB falls back to atomics)."""
+    with seb.option("build_algo", request.param):
+        yield request.param
 
 
-@pytest.fixture(params=[(0, 1, 0, 0, 0), (2, 2, 0, 0, 0), (3, 1, 0, 0, 1), (3, 2, 0, 0, 0), (3, 4, 0, 0, 0),
-                        (0, 4, 0, 0, 0), (3, 1, 12, 0, 0), (3, 2, 10, 0, 1), (3, 4, 13, 0, 0), (3, 2, 12, 64, 0),
-                        (3, 1, 10, 7, 1)],
-                ids=lambda v: f"split{v[0]}-kpt{v[1]}-slice{v[2]}-pers{v[3]}-nt{v[4]}")
+@pytest.fixture(params=[(0, 1 << 20), (1, 1 << 20), (2, 1 << 20), (7, 1 << 20), (0, 97), (1, 61)],
+                ids=lambda v: f"phases{v[0]}-grid{v[1]}")
 def probe_split(request, seb):
-    sp, kpt, sl, pers, nt = request.param
-    with seb.option("probe_split", sp), seb.option("probe_kpt", kpt), seb.option("probe_slice_shift", sl), \
-            seb.option("probe_persistent", pers), seb.option("stream_nt", nt):
+    """Probe paths: phased (auto or forced range counts), the sliced probe (one phase), and
+    grid-stride loops (a capped grid)."""
+    phases, grid = request.param
+    with seb.option("probe_phases", phases), seb.option("grid_cap", grid):
         yield request.param
 
 
@@ -231,11 +262,10 @@ def test_c2_c3_10m_device_resident(seb, golden, torch_cuda, build_algo):
     assert np.array_equal(ans[:200000], oc.probe(bits, m, k, kg.key16(sl), 200000, stride=16))
 
 
-def test_sliced_probe_gather_orders(seb, golden, torch_cuda):
-    """Every gather order of the sliced probe (k_probe_sliced modes 0-6, k_probe_compact = mode 7,
-    the phased probe = mode 8)
-    and keys-per-thread choice gives the C3 answers bit for bit, also for a ragged batch whose
-    last workgroup is partly empty."""
+def test_probe_paths_and_phase_counts(seb, golden, torch_cuda):
+    """The phased probe at any number of filter ranges, the sliced probe (one range, or an answer
+    array that is not 4-byte aligned), give the C3 answers bit for bit, also for a ragged batch
+    whose last workgroup is partly empty."""
     torch = torch_cuda
     row = next(r for r in golden["fixed16"] if r["n"] == 10_000_000)
     n, m, k = row["n"], row["m"], row["k"]
@@ -244,22 +274,18 @@ def test_sliced_probe_gather_orders(seb, golden, torch_cuda):
     pk = to_dev(torch, kg.key16(kg.probe_indices(n)))
     ragged = 999_983
     ref_ragged = oc.probe(bits, m, k, kg.key16(kg.probe_indices(n)[:ragged]), ragged, stride=16)
-    # mode 8 (phased): the second number is the phase count (0 = one per 4 MiB of filter)
-    cases = [(mode, kpt) for mode in range(7) for kpt in (1, 2, 4)] + [(7, kpt) for kpt in (2, 4, 6, 8)] + \
-        [(8, ph) for ph in (0, 2, 4, 7)]
-    for mode, kpt in cases:
-        with seb.option("probe_mode", mode), seb.option("probe_kpt", kpt if mode < 8 else 2), \
-                seb.option("probe_phases", kpt if mode == 8 else 0), seb.option("probe_slice_shift", 19):
-            out = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
-            seb.dev_probe(seb.dev_keys(pk, n=n, stride=16), words, m, k, out)
+    for phases, shift in ((0, 0), (2, 0), (4, 0), (7, 0), (1, 0), (0, 1)):
+        with seb.option("probe_phases", phases):
+            buf = torch.full((n + 4,), 7, dtype=torch.uint8, device="cuda")
+            seb.dev_probe(seb.dev_keys(pk, n=n, stride=16), words, m, k, buf[shift:shift + n])
             torch.cuda.synchronize()
-            assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"], (mode, kpt)
-            outr = torch.full((ragged + 1,), 7, dtype=torch.uint8, device="cuda")
-            seb.dev_probe(seb.dev_keys(pk[:ragged], n=ragged, stride=16), words, m, k, outr)
+            assert sha(buf[shift:shift + n].cpu().numpy().tobytes()) == row["probe_sha256"], (phases, shift)
+            outr = torch.full((ragged + 2,), 7, dtype=torch.uint8, device="cuda")
+            seb.dev_probe(seb.dev_keys(pk[:ragged], n=ragged, stride=16), words, m, k, outr[shift:shift + ragged])
             torch.cuda.synchronize()
             got = outr.cpu().numpy()
-            assert np.array_equal(got[:ragged], ref_ragged), (mode, kpt)
-            assert got[ragged] == 7, (mode, kpt)  # nothing written past the batch
+            assert np.array_equal(got[shift:shift + ragged], ref_ragged), (phases, shift)
+            assert got[shift + ragged] == 7, (phases, shift)  # nothing written past the batch
 
 
 def test_multi_packed_matches_multi(seb, golden, torch_cuda):
@@ -291,14 +317,12 @@ def test_multi_packed_matches_multi(seb, golden, torch_cuda):
     seb.dev_pack_residues(pk8, m, k, p8)
     host = [(seb.words_to_bits(w, m), m, k) for w, m, k in sub]
     ref = oc.probe_multi(host, keys8, nn, stride=16)
-    for phases in (0, 1, 3):  # auto (one range: sliced), sliced, phased
-        with seb.option("multi_phases", phases):
-            m8 = torch.full((nn + 1,), 7, dtype=torch.uint8, device="cuda")
-            seb.dev_probe_multi_packed(p8, nn, sub, m8)
-            torch.cuda.synchronize()
-        got = m8.cpu().numpy()
-        assert np.array_equal(got[:nn].astype(np.uint64), ref), phases
-        assert got[nn] == 7
+    m8 = torch.full((nn + 1,), 7, dtype=torch.uint8, device="cuda")
+    seb.dev_probe_multi_packed(p8, nn, sub, m8)
+    torch.cuda.synchronize()
+    got = m8.cpu().numpy()
+    assert np.array_equal(got[:nn].astype(np.uint64), ref)
+    assert got[nn] == 7
     m2, k2 = seb.params(per + 1, 0.01)
     with pytest.raises(seb.SebError):
         seb.dev_probe_multi_packed(p8, nn, sub + [(seb.new_words(m2), m2, k2)],
@@ -385,21 +409,18 @@ def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
     assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
-@pytest.mark.parametrize("packed", [0, 1])
-@pytest.mark.parametrize("keys,win", [(512, 72), (448, 64), (448, 72), (448, 80), (384, 64), (384, 80), (256, 64),
-                                      (1024, 56)])
-def test_c4_prehash_geometries_golden(seb, golden, torch_cuda, keys, win, packed):
+@pytest.mark.parametrize("algo", [0, 2])
+def test_c4_prehash_golden(seb, golden, torch_cuda, algo):
     """C4's zipf lengths (the spans fit the LDS window, so the sorted and split-chain hashing
-    paths run rather than the overflow fallback): every pre-hash geometry, to 16-B hashes and to
-    packed residues, reproduces the C4 golden digests."""
+    paths run rather than the overflow fallback), pre-hashed to 16-B hashes (LDS-resident build,
+    unphased probe) and to packed residues (bucketed build), reproduce the C4 golden digests."""
     torch = torch_cuda
     n = 100000
     row = next(r for r in golden["varlen"] if r["n"] == n)
     m, k = row["m"], row["k"]
     data, off = kg.varlen_keys(np.arange(n))
     pdata, poff = kg.varlen_keys(kg.probe_indices(n))
-    with seb.option("varlen_hash_keys", keys), seb.option("varlen_hash_win", win), \
-            seb.option("varlen_prehash_min_keys", 0), seb.option("varlen_prehash_packed", packed):
+    with seb.option("varlen_prehash_min_keys", 0), seb.option("build_algo", algo):
         kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
         words, bits = dev_build_bits(seb, torch, kd, m, k)
         assert sha(bn.encode(bits, m, k)) == row["encode_sha256"]
@@ -409,13 +430,11 @@ def test_c4_prehash_geometries_golden(seb, golden, torch_cuda, keys, win, packed
         assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
-@pytest.mark.parametrize("mode", [(0, 1 << 40), (1 << 40, 0), (1 << 40, 1 << 40)],
-                         ids=["prehash", "length-bucketed", "direct"])
-def test_varlen_processing_order_invisible(seb, torch_cuda, mode, build_algo):
-    """The LDS-staged pre-hash, the length-bucketed processing order (perm) and the direct byte
-    walk give the same bit array and answers, including for empty keys and keys longer than
-    256 B (the last length bucket, and LDS spans that overflow the staging window)."""
-    prehash_min, sort_min = mode
+@pytest.mark.parametrize("prehash_min", [0, 1 << 40], ids=["prehash", "direct"])
+def test_varlen_processing_order_invisible(seb, torch_cuda, prehash_min, build_algo):
+    """The LDS-staged pre-hash and the direct byte walk give the same bit array and answers,
+    including for empty keys and keys longer than 256 B (the last length bucket, and LDS spans
+    that overflow the staging window)."""
     torch = torch_cuda
     rng = np.random.default_rng(5)
     n = 70000
@@ -425,7 +444,7 @@ def test_varlen_processing_order_invisible(seb, torch_cuda, mode, build_algo):
     data = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
     m, k = oc.params(n, 0.01)
     ref = oc.build(m, k, data, n, offsets=off)
-    with seb.option("varlen_sort_min_keys", sort_min), seb.option("varlen_prehash_min_keys", prehash_min):
+    with seb.option("varlen_prehash_min_keys", prehash_min):
         kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
         words, bits = dev_build_bits(seb, torch, kd, m, k)
         assert np.array_equal(bits, ref)
@@ -438,14 +457,13 @@ def test_varlen_processing_order_invisible(seb, torch_cuda, mode, build_algo):
         assert np.array_equal(out.cpu().numpy(), oc.probe(ref, m, k, pd, n, offsets=off))
 
 
-@pytest.mark.parametrize("keys,win", [(256, 64), (256, 80), (512, 48), (512, 64), (512, 72), (512, 80), (1024, 48),
-                                      (1024, 56), (448, 64), (448, 72), (448, 80), (384, 64), (384, 80)])
-def test_varlen_prehash_geometries(seb, torch_cuda, keys, win):
-    """Every pre-hash workgroup size and LDS window hashes like the oracle, over
-    lengths that mix empty, sub-word, bucket-edge and window-overflowing keys, and a ragged
-    last workgroup."""
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed):
+    """The pre-hash (448-key workgroups, 64-B window per key, split-chain tail waves) hashes like
+    the oracle over lengths that mix empty, sub-word, bucket-edge and window-overflowing keys,
+    and a ragged last workgroup."""
     torch = torch_cuda
-    rng = np.random.default_rng(keys + win)
+    rng = np.random.default_rng(seed)
     n = 40000 + 77
     w = np.array([4, 4, 4, 4, 4, 4, 4, 8, 4, 8, 4, 8, 8, 4, 4, 4, 4, 4, 4, 3, 1], float)
     lens = rng.choice([0, 1, 2, 3, 4, 5, 7, 8, 9, 16, 31, 39, 40, 41, 63, 64, 65, 255, 256, 300, 2000], size=n,
@@ -455,8 +473,7 @@ def test_varlen_prehash_geometries(seb, torch_cuda, keys, win):
     data = rng.integers(0, 256, int(off[-1]) + 1, dtype=np.uint8)[1:]  # odd base offset in the host copy
     m, k = oc.params(n, 0.01)
     ref = oc.build(m, k, data, n, offsets=off)
-    with seb.option("varlen_hash_keys", keys), seb.option("varlen_hash_win", win), \
-            seb.option("varlen_prehash_min_keys", 0):
+    with seb.option("varlen_prehash_min_keys", 0):
         dd = torch.zeros(int(off[-1]) + 64, dtype=torch.uint8, device="cuda")
         offd = to_dev(torch, off)
         for shift in (0, 3):  # key bytes at an unaligned device address too
@@ -471,13 +488,14 @@ def test_varlen_prehash_geometries(seb, torch_cuda, keys, win):
             assert bool(out.all()), shift
 
 
-@pytest.mark.parametrize("packed", [0, 1])
+@pytest.mark.parametrize("k", [7, 8])
 @pytest.mark.parametrize("algo", [1, 2])
-def test_varlen_prehash_packed_paths(seb, torch_cuda, packed, algo):
-    """Pre-hash to packed residues (bucketed build from KeysPacked, phased probe from packed
+def test_varlen_prehash_packed_paths(seb, torch_cuda, k, algo):
+    """Pre-hash to packed residues (k = 7: bucketed build from KeysPacked, phased probe from packed
     words, pack_residues / emit_packed over variable-length keys) against the oracle, and the
-    same with the 16-B hash path; a 2-range filter so the probe runs phased."""
+    16-B hash path (k = 8); a 2-range filter so the k = 7 probe runs phased."""
     torch = torch_cuda
+    packed = k == 7
     rng = np.random.default_rng(11 + packed)
     n = 600_001
     w = np.array([20, 10, 10, 10, 5, 3, 1, 1], float)
@@ -485,18 +503,22 @@ def test_varlen_prehash_packed_paths(seb, torch_cuda, packed, algo):
     off = np.zeros(n + 1, np.uint64)
     np.cumsum(lens, out=off[1:])
     data = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
-    m, k = 40_000_003, 7
+    m = 40_000_003
     ref = oc.build(m, k, data, n, offsets=off, threads=16)
     pd = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
     pd[: int(off[n // 2])] = data[: int(off[n // 2])]  # first half present
     want = oc.probe(ref, m, k, pd, n, offsets=off)
-    with seb.option("varlen_prehash_packed", packed), seb.option("build_algo", algo):
+    with seb.option("build_algo", algo):
         kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
         words, bits = dev_build_bits(seb, torch, kd, m, k)
         assert np.array_equal(bits, ref)
         pkd = seb.dev_keys(to_dev(torch, pd), to_dev(torch, off))
         out = torch.empty(n, dtype=torch.uint8, device="cuda")
         seb.dev_probe(pkd, words, m, k, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want)
+        if not packed:
+            return
         pk = torch.zeros(n, dtype=torch.int64, device="cuda")
         seb.dev_pack_residues(pkd, m, k, pk)
         out2 = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -511,8 +533,8 @@ def test_varlen_prehash_packed_paths(seb, torch_cuda, packed, algo):
         assert torch.equal(pk, pk3)
 
 
-@pytest.mark.parametrize("packed", [0, 1])
-def test_varlen_bucketed_build_chunks(seb, torch_cuda, packed):
+@pytest.mark.parametrize("k", [7, 8])
+def test_varlen_bucketed_build_chunks(seb, torch_cuda, k):
     """A pre-hashed variable-length build larger than one bucketed launch (16.7M keys at k = 7)
     runs in chunks; every chunk must take its own slice of the hashes / packed residues."""
     torch = torch_cuda
@@ -522,9 +544,9 @@ def test_varlen_bucketed_build_chunks(seb, torch_cuda, packed):
     off = np.zeros(n + 1, np.uint64)
     np.cumsum(lens, out=off[1:])
     data = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
-    m, k = 160_000_001, 7
+    m = 160_000_001
     ref = oc.build(m, k, data, n, offsets=off, threads=16)
-    with seb.option("varlen_prehash_packed", packed), seb.option("build_algo", 2):
+    with seb.option("build_algo", 2):
         kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
         words, bits = dev_build_bits(seb, torch, kd, m, k)
         assert np.array_equal(bits, ref)
@@ -757,10 +779,9 @@ def test_multi_filter_probe(seb, golden, torch_cuda, which):
     assert np.array_equal(mm.cpu().numpy(), ref.astype(np.uint8))
 
 
-@pytest.mark.parametrize("interleave,phases", [(0, 0), (1, 0), (1, 1), (1, 2), (1, 3), (1, 5)])
-def test_multi_filter_interleaved_vs_direct(seb, golden, torch_cuda, interleave, phases):
-    """The interleaved (bit-transposed) table path and the per-filter path give identical masks;
-    phases > 1 forces the phased interleaved probe (one launch per table range) on a small table."""
+@pytest.mark.parametrize("interleave", [0, 1])
+def test_multi_filter_interleaved_vs_direct(seb, golden, torch_cuda, interleave):
+    """The interleaved (bit-transposed) table path and the per-filter path give identical masks."""
     torch = torch_cuda
     row = golden["multi"][1]  # 64 filters x 2000 keys
     nf, per, npr, m, k = row["filters"], row["keys_per_filter"], row["probes"], row["m"], row["k"]
@@ -771,7 +792,7 @@ def test_multi_filter_interleaved_vs_direct(seb, golden, torch_cuda, interleave,
     half = q // 2
     kd = seb.dev_keys(to_dev(torch, kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q))),
                       n=npr, stride=16)
-    with seb.option("multi_interleave", interleave), seb.option("multi_phases", phases):
+    with seb.option("multi_interleave", interleave):
         for dt, nsub in ((torch.int64, 64), (torch.int32, 32), (torch.int16, 16), (torch.uint8, 8)):
             mask = torch.zeros(npr, dtype=dt, device="cuda")
             seb.dev_probe_multi(kd, filters[:nsub], mask)
@@ -961,17 +982,7 @@ def _lsm_get_walk(files, key: bytes):
     return out
 
 
-@pytest.fixture(params=[(0, 1), (4096, 1), (1, 1), (0, 0), (4096, 0)],
-                ids=["one-pass", "passes-4MiB", "pass-per-file", "one-pass-serial", "passes-4MiB-serial"])
-def multiget_passes(request, seb):
-    """MultiGet split into passes of filter bytes (multiget_pass_kib), filters tested 4 at a time
-    or one by one (multiget_group): the masks never change."""
-    kib, group = request.param
-    with seb.option("multiget_pass_kib", kib), seb.option("multiget_group", group):
-        yield kib
-
-
-def test_registry_multiget_matches_lsm_get_walk(seb, torch_cuda, multiget_passes):
+def test_registry_multiget_matches_lsm_get_walk(seb, torch_cuda):
     torch = torch_cuda
     rng = np.random.default_rng(17)
     reg = seb.Registry(0)
@@ -1028,7 +1039,7 @@ def test_registry_multiget_matches_lsm_get_walk(seb, torch_cuda, multiget_passes
     reg.close()
 
 
-def test_registry_multiget_overlap_long_keys_generic_k(seb, torch_cuda, multiget_passes):
+def test_registry_multiget_overlap_long_keys_generic_k(seb, torch_cuda):
     """The branches the LSM bench layout does not reach: an overlapping level (the reference's
     first-cover linear scan, lsm/lsm.go:184-196), range keys longer than the 16-byte LDS prefix
     that tie on it (HBM tail compare), prefix-of relations, and filters with k != 7."""
@@ -1077,13 +1088,7 @@ def _walk_rows(files, probes, cap):
     return want
 
 
-@pytest.fixture(params=[1, 0], ids=["grouped", "serial"])
-def multiget_group(request, seb):
-    with seb.option("multiget_group", request.param):
-        yield request.param
-
-
-def test_registry_multiget_list_beyond_64_files(seb, torch_cuda, multiget_group):
+def test_registry_multiget_list_beyond_64_files(seb, torch_cuda):
     """A registry past 64 files (an LSM with populated L1/L2: 400 MB / ~4 MB files,
     lsm/levels.go:10-14, lsm/compaction.go:253): the slot table is read from HBM instead of LDS
     and the answer is the list form, the slots Get would consult whose filter may contain the key
@@ -1217,6 +1222,26 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
             lists.append(lst.cpu().numpy().view(np.uint16))
     assert np.array_equal(outs[0], outs[1])
     assert np.array_equal(lists[0], lists[1])
+    # The order's scratch cannot be had (a 1 MiB workspace cap; its first request is ~2.6 MB):
+    # MultiGet falls back to batch order and answers the same.  A failed HIP call made just before
+    # (a device allocation of 2^60 B) must not leak into the MultiGet's launch check.
+    import ctypes
+
+    seb.workspace_release()
+    with seb.option("multiget_order", 1), seb.option("workspace_limit_mib", 1):
+        ptr = ctypes.c_void_p()
+        assert seb.lib().seb_dev_alloc(ctypes.byref(ptr), 1 << 60) != 0
+        out = torch.zeros(nf, dtype=torch.int64, device="cuda")
+        reg.multiget_dev(dk, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), outs[0])
+        assert np.array_equal(reg.multiget(probes), want_mask)
+        assert np.array_equal(reg.multiget_list(probes), want_list)
+        with pytest.raises(seb.SebError):  # a build whose scratch is over the cap fails loudly
+            big = seb.dev_keys(to_dev(torch, kg.key16(np.arange(1_000_000))), n=1_000_000, stride=16)
+            with seb.option("build_algo", 2):
+                seb.dev_build(big, seb.new_words(9_585_059), 9_585_059, 7)
+    seb.workspace_release()
     fixed_rows = np.array([i for i, p in enumerate(probes) if len(p) == 16])
     assert np.array_equal(lists[1], want_list[fixed_rows])
     # host fixed 16-B chunks: staged into aligned device buffers, so the keys move as well
@@ -1333,7 +1358,7 @@ def test_shared_stream_threads_and_workspace_release(seb, golden, torch_cuda):
     assert np.array_equal(out.cpu().numpy(), want[1])
 
 
-def test_registry_full_capacity(seb, torch_cuda, multiget_group):
+def test_registry_full_capacity(seb, torch_cuda):
     """4096 files (the u16 slot-id capacity): one L0 file and 4095 one-key L1 files.  The
     4097th put is refused; the list form still answers every key as Get's walk does, and a key
     between two files' ranges visits only L0."""
@@ -1363,9 +1388,8 @@ def test_registry_full_capacity(seb, torch_cuda, multiget_group):
     reg.close()
 
 
-@pytest.mark.parametrize("grp", [0, 8])
 @pytest.mark.parametrize("case", ["duplicates", "skewed", "large_m"])
-def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case, grp):
+def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
     """Radix-partitioned build paths a hash-distributed batch never takes: runs that overflow
     their fixed-capacity region (identical keys put a tile's positions into 7 buckets; skewed: a
     few distinct keys repeated) fall back to device-scope atomic OR, and a filter with more
@@ -1373,7 +1397,6 @@ def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case, grp):
     The bit array must equal the oracle's either way."""
     torch = torch_cuda
     seb.set_option("build_algo", 2)
-    seb.set_option("scatter_xcd", grp)  # regions per tile, or per group of 8 tiles (shared claims)
     try:
         rng = np.random.default_rng(5)
         if case == "duplicates":
@@ -1392,7 +1415,6 @@ def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case, grp):
         assert np.array_equal(bits, ref)
     finally:
         seb.set_option("build_algo", 0)
-        seb.set_option("scatter_xcd", 0)
 
 
 # ------------------------------------------------ sharded build of one filter (§8(e)) ----
@@ -1506,24 +1528,18 @@ def test_partitioned_probe_one_rank(seb, golden, torch_cuda):
     assert sha(ans.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("kernel", [1, 0])
-def test_dev_clear(seb, torch_cuda, kernel):
-    """seb_dev_clear zeroes exactly seb_words_bytes(m) (the 16-B store kernel and hipMemsetAsync),
-    and leaves the words past it alone; a pointer that is not 16-B aligned takes the memset."""
+def test_dev_clear(seb, torch_cuda):
+    """seb_dev_clear zeroes exactly seb_words_bytes(m) (the 16-B store kernel), and leaves the
+    words past it alone; a pointer that is not 16-B aligned takes hipMemsetAsync."""
     torch = torch_cuda
-    seb.set_option("clear_kernel", kernel)
-    try:
-        for m in (1, 127, 128, 129, 958_506, 95_850_584):
-            nw = seb.words_bytes(m) // 4
-            buf = torch.full((nw + 8,), -1, dtype=torch.int32, device="cuda")
-            seb.dev_clear(buf, m)
-            torch.cuda.synchronize()
-            assert int(buf[:nw].abs().sum()) == 0 and bool((buf[nw:] == -1).all()), m
-            view = buf[1:]  # 4-B aligned only
-            buf.fill_(-1)
-            seb.dev_clear(view, m)
-            torch.cuda.synchronize()
-            assert int(buf[0]) == -1 and int(buf[1:nw + 1].abs().sum()) == 0 and bool((buf[nw + 1:] == -1).all()), m
-    finally:
-        seb.set_option("clear_kernel", 1)
+    for m in (1, 127, 128, 129, 958_506, 95_850_584):
+        nw = seb.words_bytes(m) // 4
+        buf = torch.full((nw + 8,), -1, dtype=torch.int32, device="cuda")
+        seb.dev_clear(buf, m)
+        torch.cuda.synchronize()
+        assert int(buf[:nw].abs().sum()) == 0 and bool((buf[nw:] == -1).all()), m
+        view = buf[1:]  # 4-B aligned only
+        buf.fill_(-1)
+        seb.dev_clear(view, m)
+        torch.cuda.synchronize()
+        assert int(buf[0]) == -1 and int(buf[1:nw + 1].abs().sum()) == 0 and bool((buf[nw + 1:] == -1).all()), m
