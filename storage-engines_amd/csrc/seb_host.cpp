@@ -39,10 +39,15 @@ static int fail(int code, const char *fmt, ...) {
     return code;
 }
 
+// A failed HIP call is reported through the return code, and HIP's last-error state is cleared so
+// it does not surface again in the caller's own later checks (torch's hipGetLastError, say).
 #define HIP_OR_FAIL(expr)                                                                              \
     do {                                                                                               \
         hipError_t e_ = (expr);                                                                        \
-        if (e_ != hipSuccess) return fail(SEB_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_));    \
+        if (e_ != hipSuccess) {                                                                        \
+            (void)hipGetLastError();                                                                   \
+            return fail(SEB_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_));                       \
+        }                                                                                              \
     } while (0)
 
 // Makes `device` current for one call and restores the caller's device when it returns.
@@ -122,7 +127,7 @@ struct OptionDesc {
             [](Options &o, int64_t v) { o.field = (decltype(o.field))v; }                    \
     }
 static const OptionDesc kOptions[] = {
-    SEB_OPT(build_algo, 0, 3),
+    SEB_OPT(build_algo, 0, 4),
     SEB_OPT(multi_interleave, 0, 1),
     SEB_OPT(multiget_order, 0, 1),
     SEB_OPT(varlen_prehash_min_keys, 0, INT64_MAX),
@@ -354,12 +359,15 @@ static bool want_prehash_packed(const KeyBatch &kb, const ModArg &md) {
 // Build dispatcher: bucketed (LDS, no global atomics), LDS-resident or device-scope atomics;
 // large variable-length batches are pre-hashed first.  `ws` / `ws_bytes` may be null/0, in which
 // case `grow` supplies scratch.
+// fresh: `words` holds nothing yet (a new filter); the image build then writes it without a clear,
+// every other path clears it first.
 template <typename Grow>
 static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStream_t s, void *ws, uint64_t ws_bytes,
-                          Grow &&grow) {
+                          Grow &&grow, bool fresh = false) {
     if (kb.n == 0 || md.k == 0) return SEB_OK;
     const int algo = choose_build_algo(kb.n, md.m, md.k);
     const bool bucketed = algo == 2;
+    if (fresh && algo != 4) HIP_OR_FAIL(launch_clear_words(words, seb_words_bytes(md.m), s));
     if (bucketed && want_prehash_packed(kb, md)) {  // scratch: [packed residues | bucketed]
         const uint64_t pack_b = (kb.n * 8 + 255) & ~255ull;
         const uint64_t need = pack_b + bucketed_workspace_bytes(kb.n, md.m, md.k);
@@ -374,7 +382,8 @@ static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStr
         return SEB_OK;
     }
     const uint64_t head = prehash_bytes(kb);
-    const uint64_t need = head + (bucketed ? bucketed_workspace_bytes(kb.n, md.m, md.k) : 0);
+    const uint64_t need = head + (bucketed ? bucketed_workspace_bytes(kb.n, md.m, md.k)
+                                  : algo == 4 ? image_workspace_bytes(kb.n, md.m) : 0);
     if (need > ws_bytes) {
         int rc = grow(need, &ws);
         if (rc) return rc;
@@ -386,6 +395,10 @@ static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStr
     }
     if (bucketed) {
         HIP_OR_FAIL(launch_build_bucketed(kb, words, md, (uint8_t *)ws + head, ws_bytes - head, s));
+        return SEB_OK;
+    }
+    if (algo == 4) {
+        HIP_OR_FAIL(launch_build_images(kb, words, md, (uint8_t *)ws + head, ws_bytes - head, fresh, s));
         return SEB_OK;
     }
     if (algo == 3) {  // the whole filter in one CU's LDS, the keys split over workgroups (build_many's kernel)
@@ -454,7 +467,8 @@ extern "C" uint64_t seb_dev_build_workspace_size(uint64_t n, uint64_t m, uint32_
     if (m == 0 || n == 0) return 0;
     // conservative: assumes a variable-length batch (pre-hashed) as well
     const uint64_t pre_b = n >= options().varlen_prehash_min_keys ? ((n * 16 + 255) & ~255ull) : 0;
-    return pre_b + (choose_build_algo(n, m, k) == 2 ? bucketed_workspace_bytes(n, m, k) : 0);
+    const int algo = choose_build_algo(n, m, k);
+    return pre_b + (algo == 2 ? bucketed_workspace_bytes(n, m, k) : algo == 4 ? image_workspace_bytes(n, m) : 0);
 }
 
 extern "C" int seb_dev_build_ws(const seb_keys *keys, uint32_t *words, uint64_t m, uint32_t k, void *ws,
@@ -680,7 +694,7 @@ extern "C" int seb_dev_build_many(const seb_keys *keys, const uint64_t *key_begi
 extern "C" int seb_dev_alloc(void **ptr, uint64_t bytes) {
     if (!ptr) return fail(SEB_ERR_INVALID, "seb_dev_alloc: null");
     hipError_t e = hipMalloc(ptr, bytes ? bytes : 16);
-    if (e != hipSuccess) return fail(SEB_ERR_NOMEM, "hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
+    if (e != hipSuccess) return (void)hipGetLastError(), fail(SEB_ERR_NOMEM, "hipMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
     return SEB_OK;
 }
 extern "C" int seb_dev_free(void *ptr) {
@@ -690,7 +704,7 @@ extern "C" int seb_dev_free(void *ptr) {
 extern "C" int seb_host_alloc(void **ptr, uint64_t bytes) {
     if (!ptr) return fail(SEB_ERR_INVALID, "seb_host_alloc: null");
     hipError_t e = hipHostMalloc(ptr, bytes ? bytes : 16, hipHostMallocDefault);
-    if (e != hipSuccess) return fail(SEB_ERR_NOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
+    if (e != hipSuccess) return (void)hipGetLastError(), fail(SEB_ERR_NOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
     return SEB_OK;
 }
 extern "C" int seb_host_free(void *ptr) {
@@ -750,7 +764,7 @@ struct DevBuf {
         cap = 0;
         uint64_t want = std::max<uint64_t>(bytes, 4096);
         hipError_t e = hipMalloc(&p, want);
-        if (e != hipSuccess) return fail(SEB_ERR_NOMEM, "hipMalloc(%llu): %s", (unsigned long long)want, hipGetErrorString(e));
+        if (e != hipSuccess) return (void)hipGetLastError(), fail(SEB_ERR_NOMEM, "hipMalloc(%llu): %s", (unsigned long long)want, hipGetErrorString(e));
         cap = want;
         return SEB_OK;
     }
@@ -881,7 +895,8 @@ static int stage_chunk(seb_ctx *c, const seb_keys *kb, const Chunk &ch, int b, K
 }
 
 // OR host keys into device words (all on c->s_comp ordering), chunked + double buffered.
-static int build_device_from_host(seb_ctx *c, const seb_keys *kb, uint32_t *dwords, const ModArg &md) {
+static int build_device_from_host(seb_ctx *c, const seb_keys *kb, uint32_t *dwords, const ModArg &md,
+                                  bool fresh = false) {
     std::vector<Chunk> chunks;
     plan_chunks(kb, c->chunk_bytes, chunks);
     for (size_t j = 0; j < chunks.size(); ++j) {
@@ -894,7 +909,7 @@ static int build_device_from_host(seb_ctx *c, const seb_keys *kb, uint32_t *dwor
             int r = c->ws.reserve(need);
             *out = c->ws.p;
             return r;
-        });
+        }, fresh && j == 0);
         if (rc) return rc;
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
     }
@@ -1184,7 +1199,7 @@ static int host_may_contain(const seb_filter *f, const uint8_t *key, uint64_t le
 
 // The device word array, on `s`: a pooled or new buffer, zeroed, then the host bits unless the
 // filter is a fresh New (all zero).
-static int ensure_device_copy(seb_filter *f, hipStream_t s) {
+static int ensure_device_copy(seb_filter *f, hipStream_t s, bool clear = true) {
     if (f->dwords) return SEB_OK;
     HIP_OR_FAIL(hipSetDevice(f->device));
     uint64_t want = std::max<uint64_t>(seb_words_bytes(f->m), (f->nbytes + 15) / 16 * 16);
@@ -1202,7 +1217,7 @@ static int ensure_device_copy(seb_filter *f, hipStream_t s) {
     f->dwords = (uint32_t *)p;
     f->dbytes = got;
     if (f->host_zero) {
-        HIP_OR_FAIL(hipMemsetAsync(f->dwords, 0, f->dbytes, s));
+        if (clear) HIP_OR_FAIL(hipMemsetAsync(f->dwords, 0, f->dbytes, s));
     } else {
         const uint64_t tail = f->nbytes & ~15ull;  // zero the padding past the copied bytes
         HIP_OR_FAIL(hipMemsetAsync((uint8_t *)f->dwords + tail, 0, f->dbytes - tail, s));
@@ -1228,11 +1243,14 @@ static int build_into_filter(seb_filter *f, const seb_keys *kb) {
     std::lock_guard<std::mutex> g(L.c->mu);
     HIP_OR_FAIL(hipSetDevice(f->device));
     int rc;
-    if ((rc = ensure_device_copy(f, L.c->s_comp))) return rc;
+    // a new filter's first build writes its words whole (image build) or clears them first: no
+    // separate memset of the device copy
+    const bool fresh = f->host_zero && !f->dwords;
+    if ((rc = ensure_device_copy(f, L.c->s_comp, !fresh))) return rc;
     f->host_ok = false;  // the device copy is about to move ahead of the host copy
     f->host_zero = false;
     f->readable.store(false, std::memory_order_relaxed);
-    if ((rc = build_device_from_host(L.c, kb, f->dwords, mod_arg(f->m, f->k)))) return rc;
+    if ((rc = build_device_from_host(L.c, kb, f->dwords, mod_arg(f->m, f->k), fresh))) return rc;
     HIP_OR_FAIL(hipStreamSynchronize(L.c->s_comp));
     return SEB_OK;
 }
@@ -1502,7 +1520,7 @@ extern "C" int seb_registry_put(seb_registry *r, uint64_t file_num, int level, c
     e.max_key.assign((const char *)max_key, max_len);
     const uint64_t wb = seb_words_bytes(m);
     hipError_t a = hipMalloc((void **)&e.dwords, wb);
-    if (a != hipSuccess) return fail(SEB_ERR_NOMEM, "seb_registry_put: hipMalloc: %s", hipGetErrorString(a));
+    if (a != hipSuccess) return (void)hipGetLastError(), fail(SEB_ERR_NOMEM, "seb_registry_put: hipMalloc: %s", hipGetErrorString(a));
     HIP_OR_FAIL(hipMemset(e.dwords, 0, wb));
     HIP_OR_FAIL(hipMemcpy(e.dwords, bloom + 12, seb_num_bytes(m), hipMemcpyHostToDevice));
     r->entries.push_back(std::move(e));

@@ -94,7 +94,8 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
 // and the few shape choices tests force to cover both paths.  Variants measured slower were
 // removed from the kernels (DESIGN.md 8 keeps their numbers).
 struct Options {
-    int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed), 3 LDS-resident filter
+    int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed), 3 LDS-resident
+                                  // filter (atomic merge), 4 LDS images + OR kernel
     int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
     int multiget_order = 1;       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
     uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys
@@ -117,8 +118,14 @@ hipError_t launch_build_bucketed_packed(const uint64_t *packed, uint64_t n, uint
                                         void *ws, uint64_t ws_bytes, hipStream_t s);
 hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModArg &md, void *ws, uint64_t ws_bytes,
                                  hipStream_t s);
-// 1 = atomic, 2 = bucketed, for a batch of n keys into an m-bit filter.
+// 1 = atomic, 2 = bucketed, 3 = LDS-resident (atomic merge), 4 = LDS images + OR kernel, for a
+// batch of n keys into an m-bit filter.
 int choose_build_algo(uint64_t n, uint64_t m, uint32_t k);
+// The image build (algo 4): scratch bytes, and the launch.  fresh: the filter words hold nothing
+// yet, so they are written rather than OR-ed (and need no clear beforehand).
+uint64_t image_workspace_bytes(uint64_t n, uint64_t m);
+hipError_t launch_build_images(const KeyBatch &kb, uint32_t *words, const ModArg &md, void *ws, uint64_t ws_bytes,
+                               bool fresh, hipStream_t s);
 hipError_t launch_probe(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s);
 hipError_t launch_probe_multi(const KeyBatch &kb, const MultiArg &ma, void *mask, uint32_t mask_bytes,
                               hipStream_t s);

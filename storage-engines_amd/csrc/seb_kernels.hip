@@ -544,6 +544,51 @@ __global__ __launch_bounds__(1024) void k_build_many_lds(Src src, ManyArg ma, ui
     }
 }
 
+// Small-filter build in two launches, no global atomics (build_algo 4; flush- and
+// compaction-sized filters whose word array fits one CU's LDS).  k_build_images: workgroup g
+// sets the bits of its key range [n*g/G, n*(g+1)/G) in an LDS image of the whole filter with
+// ds_or, then stores the image to scratch with 16-B stores.  k_or_images: one thread per 16 B of
+// filter ORs the G images (and the old words, unless the filter is fresh) into the filter.  The
+// device-scope atomics of k_build go to memory one by one (TCC_EA0_ATOMIC = n*k,
+// profiles/r01a_pmc.csv); here the keys are hashed on G CUs and the only global traffic is
+// G images written and read once.
+template <typename Src, int KFIX, bool M32>
+__global__ __launch_bounds__(1024) void k_build_images(Src src, uint64_t n, ModArg md, uint32_t nw4,
+                                                       uint4 *__restrict__ images) {
+    extern __shared__ uint4 limg[];
+    uint32_t *lw = (uint32_t *)limg;
+    const uint32_t g = blockIdx.x, G = gridDim.x;
+    for (uint32_t j = threadIdx.x; j < nw4; j += blockDim.x) limg[j] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    const uint64_t k0 = n * g / G, k1 = n * (g + 1) / G;
+    for (uint64_t i = k0 + threadIdx.x; i < k1; i += blockDim.x) {
+        uint64_t h1, h2;
+        src.hash(i, h1, h2);
+        for_positions<KFIX, M32>(h1, h2, md, md.k, [&](uint32_t, uint64_t p) {
+            __hip_atomic_fetch_or(lw + (p >> 5), 1u << (uint32_t)(p & 31), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+        });
+    }
+    __syncthreads();
+    uint4 *out = images + (uint64_t)g * nw4;
+    for (uint32_t j = threadIdx.x; j < nw4; j += blockDim.x) out[j] = limg[j];
+}
+
+__global__ __launch_bounds__(256) void k_or_images(const uint4 *__restrict__ images, uint32_t G, uint32_t nw4,
+                                                   uint4 *__restrict__ words, uint32_t fresh) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nw4) return;
+    uint4 a = fresh ? make_uint4(0, 0, 0, 0) : words[j];
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint4 v = images[(uint64_t)g * nw4 + j];
+        a.x |= v.x;
+        a.y |= v.y;
+        a.z |= v.z;
+        a.w |= v.w;
+    }
+    words[j] = a;
+}
+
 // ------------------------------------------------------------------ launchers ----------------
 
 static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
@@ -560,17 +605,55 @@ Options &options() {
 }
 
 // 1 device-scope atomics, 2 radix-partitioned (bucketed), 3 the whole filter in one CU's LDS
-// with the keys split over workgroups (k_build_many_lds).  Auto (tools/small_builds.py,
-// profiles/r02_small_builds.jsonl): atomics below ~75K keys, the LDS build while the filter fits
-// 160 KiB (m <= 1.31M bits), bucketed from 100K keys for larger filters.
+// with the keys split over workgroups (k_build_many_lds), 4 LDS images OR-merged by a second
+// kernel (k_build_images).  Auto (tools/small_builds.py, profiles/r03_small_builds.jsonl): the
+// image build while the word array fits 160 KiB, bucketed from bucket_min_keys for larger
+// filters, device-scope atomics below that.
 int choose_build_algo(uint64_t n, uint64_t m, uint32_t k) {
     const Options &o = options();
     const bool lds = (m + 127) / 128 * 16 <= kLdsFilterBytes;
     if (o.build_algo == 1) return 1;
     if (o.build_algo == 2) return bucketed_supported(m, k) ? 2 : 1;
     if (o.build_algo == 3) return lds ? 3 : 1;
-    if (lds && n >= o.lds_min_keys) return 3;
+    if (o.build_algo == 4) return lds ? 4 : 1;
+    if (lds && n >= o.lds_min_keys) return 4;
     return bucketed_supported(m, k) && n >= o.bucket_min_keys ? 2 : 1;
+}
+
+// Workgroups of the image build: about 1024 keys each, at most 128 (more images cost more merge
+// traffic than the extra CUs save).
+uint32_t image_groups(uint64_t n) {
+    const uint64_t g = (n + 1023) / 1024;
+    return (uint32_t)(g < 1 ? 1 : g > 128 ? 128 : g);
+}
+
+uint64_t image_workspace_bytes(uint64_t n, uint64_t m) { return image_groups(n) * ((m + 127) / 128) * 16; }
+
+hipError_t launch_build_images(const KeyBatch &kb, uint32_t *words, const ModArg &md, void *ws, uint64_t ws_bytes,
+                               bool fresh, hipStream_t s) {
+    if (kb.n == 0 || md.k == 0) return hipSuccess;
+    const uint32_t nw4 = (uint32_t)((md.m + 127) / 128);
+    const uint32_t G = image_groups(kb.n);
+    if (nw4 * 16ull > kLdsFilterBytes || ws_bytes < image_workspace_bytes(kb.n, md.m)) return hipErrorInvalidValue;
+    // one workgroup: its image goes straight to the filter (fresh) or through the OR kernel
+    uint4 *images = G > 1 || !fresh ? (uint4 *)ws : (uint4 *)words;
+    const bool m32 = md.m < kM32Limit, k7 = md.k == 7;
+    const hipError_t e = with_src(kb, [&](auto src) {
+        using S = decltype(src);
+        auto go = [&](auto kern) {
+            hipError_t a = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)(nw4 * 16));
+            if (a != hipSuccess) return a;
+            hipLaunchKernelGGL(kern, dim3(G), dim3(1024), nw4 * 16, s, src, kb.n, md, nw4, images);
+            return hipGetLastError();
+        };
+        if (m32) return k7 ? go(k_build_images<S, 7, true>) : go(k_build_images<S, 0, true>);
+        return k7 ? go(k_build_images<S, 7, false>) : go(k_build_images<S, 0, false>);
+    });
+    if (e != hipSuccess || (G == 1 && fresh)) return e;
+    hipLaunchKernelGGL(k_or_images, dim3((nw4 + 255) / 256), dim3(256), 0, s, (const uint4 *)images, G, nw4,
+                       (uint4 *)words, fresh ? 1u : 0u);
+    return hipGetLastError();
 }
 
 template <typename Src, int KFIX, bool M32>

@@ -123,7 +123,7 @@ def test_options_round_trip_and_reject_bad_values(seb):
         assert seb.get_option(name) == old
     with seb.option("probe_phases", 5):
         assert seb.get_option("probe_phases") == 5
-    for name, bad in (("build_algo", 4), ("probe_phases", 65), ("many_splits", -1), ("grid_cap", 0),
+    for name, bad in (("build_algo", 5), ("probe_phases", 65), ("many_splits", -1), ("grid_cap", 0),
                       ("multiget_order", 2), ("nonexistent", 1), ("probe_mode", 8), ("scatter_xcd", 0),
                       ("clear_kernel", 1)):
         before = seb.get_option(name) if name in OPTION_NAMES else None

@@ -150,6 +150,30 @@ def test_go_api_uniform_then_mixed_lengths_and_republish(seb, torch_cuda):
     assert f.encode()[12:] == ref.tobytes()
 
 
+@pytest.mark.parametrize("n", [1, 500, 1024, 1025, 5000, 50_000, 100_003])
+def test_image_build_fresh_and_accumulating(seb, torch_cuda, n):
+    """The LDS-image build (build_algo 4): one workgroup writing the filter directly or G images
+    OR-merged by the second kernel; a new filter's first build writes its words whole (no clear),
+    later builds OR into them; the device API always ORs."""
+    torch = torch_cuda
+    keys = kg.key16(np.arange(2 * n))
+    m, k = oc.params(n, 0.01)
+    with seb.option("build_algo", 4):
+        f = seb.BloomFilter(n, 0.01)
+        f.add_batch(keys[:n])
+        assert f.encode()[12:] == oc.build(m, k, keys[:n], n, stride=16).tobytes()
+        f.add_batch(keys[n:])
+        assert f.encode()[12:] == oc.build(m, k, keys, 2 * n, stride=16).tobytes()
+        f.close()
+        words = seb.new_words(m)
+        seb.dev_build(seb.dev_keys(to_dev(torch, keys[n:]), n=n, stride=16), words, m, k)
+        seb.dev_build(seb.dev_keys(to_dev(torch, keys[:n]), n=n, stride=16), words, m, k)
+        torch.cuda.synchronize()
+        assert np.array_equal(seb.words_to_bits(words, m), oc.build(m, k, keys, 2 * n, stride=16))
+        tail = words.cpu().numpy().view(np.uint8)[(m + 7) // 8:]
+        assert not tail.any() or (m % 8 and tail[0] >> (m % 8) == 0 and not tail[1:].any())
+
+
 def test_go_api_errors_match_reference_panics(seb, torch_cuda):
     z = seb.BloomFilter.decode(bytes(12))  # numBits 0: Go panics with divide by zero
     with pytest.raises(seb.SebError):
@@ -204,10 +228,11 @@ def test_host_api_chunked_pipeline(seb, monkeypatch, torch_cuda):
 
 # --------------------------------------------------------- device-resident API --------------
 
-@pytest.fixture(params=[1, 2, 3], ids=["atomic", "bucketed", "lds"])
+@pytest.fixture(params=[1, 2, 3, 4], ids=["atomic", "bucketed", "lds", "images"])
 def build_algo(request, seb):
-    """Build paths: device-scope atomics, radix-partitioned (bucketed), and the LDS-resident filter
-    (algo 3; a filter over 160 KiB falls back to atomics)."""
+    """Build paths: device-scope atomics, radix-partitioned (bucketed), the LDS-resident filter
+    with an atomic merge (algo 3) and LDS images merged by a second kernel (algo 4); a filter
+    over 160 KiB takes atomics for 3 and 4."""
     with seb.option("build_algo", request.param):
         yield request.param
 
@@ -1224,14 +1249,17 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
     assert np.array_equal(lists[0], lists[1])
     # The order's scratch cannot be had (a 1 MiB workspace cap; its first request is ~2.6 MB):
     # MultiGet falls back to batch order and answers the same.  A failed HIP call made just before
-    # (a device allocation of 2^60 B) must not leak into the MultiGet's launch check.
+    # (the caller's hipMalloc of 2^60 B, its error left unread) must not leak into the MultiGet's
+    # launch check.
     import ctypes
 
     seb.workspace_release()
+    hip = ctypes.CDLL("libamdhip64.so")
     with seb.option("multiget_order", 1), seb.option("workspace_limit_mib", 1):
-        ptr = ctypes.c_void_p()
-        assert seb.lib().seb_dev_alloc(ctypes.byref(ptr), 1 << 60) != 0
         out = torch.zeros(nf, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        ptr = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(ptr), ctypes.c_size_t(1 << 60)) != 0  # left unread in HIP's state
         reg.multiget_dev(dk, out)
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy(), outs[0])
