@@ -870,25 +870,29 @@ static int validate_offsets(const seb_keys *kb, const char *who) {
     return SEB_OK;
 }
 
-// Stage one chunk of host keys into buffer b on s_h2d; returns the device KeyBatch for it.
-static int stage_chunk(seb_ctx *c, const seb_keys *kb, const Chunk &ch, int b, KeyBatch *dk) {
+// Stage one chunk of host keys into buffer b on s_h2d; returns the device KeyBatch for it.  A batch
+// of one chunk is copied on s_comp itself: nothing to overlap, and a cross-stream event wait
+// costs ~17 us before the kernel may start (profiles/r03_flush_trace.txt).
+static int stage_chunk(seb_ctx *c, const seb_keys *kb, const Chunk &ch, int b, KeyBatch *dk, bool single) {
     int rc;
     const uint64_t bytes = ch.byte1 - ch.byte0;
     if ((rc = c->keys[b].reserve(bytes + 16))) return rc;
-    HIP_OR_FAIL(hipStreamWaitEvent(c->s_h2d, c->ev_comp[b], 0));  // buffer b no longer read
-    if (bytes) HIP_OR_FAIL(hipMemcpyAsync(c->keys[b].p, kb->data + ch.byte0, bytes, hipMemcpyHostToDevice, c->s_h2d));
+    hipStream_t cs = single ? c->s_comp : c->s_h2d;
+    if (!single) HIP_OR_FAIL(hipStreamWaitEvent(c->s_h2d, c->ev_comp[b], 0));  // buffer b no longer read
+    if (bytes) HIP_OR_FAIL(hipMemcpyAsync(c->keys[b].p, kb->data + ch.byte0, bytes, hipMemcpyHostToDevice, cs));
     dk->n = ch.i1 - ch.i0;
     dk->stride = kb->stride;
     if (kb->offsets) {
         const uint64_t cnt = dk->n + 1;
         if ((rc = c->offs[b].reserve(cnt * 8))) return rc;
-        HIP_OR_FAIL(hipMemcpyAsync(c->offs[b].p, kb->offsets + ch.i0, cnt * 8, hipMemcpyHostToDevice, c->s_h2d));
+        HIP_OR_FAIL(hipMemcpyAsync(c->offs[b].p, kb->offsets + ch.i0, cnt * 8, hipMemcpyHostToDevice, cs));
         dk->offsets = (const uint64_t *)c->offs[b].p;
         dk->data = (const uint8_t *)c->keys[b].p - ch.byte0;  // offsets are absolute
     } else {
         dk->offsets = nullptr;
         dk->data = (const uint8_t *)c->keys[b].p;
     }
+    if (single) return SEB_OK;
     HIP_OR_FAIL(hipEventRecord(c->ev_h2d[b], c->s_h2d));
     HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_h2d[b], 0));
     return SEB_OK;
@@ -902,7 +906,7 @@ static int build_device_from_host(seb_ctx *c, const seb_keys *kb, uint32_t *dwor
     for (size_t j = 0; j < chunks.size(); ++j) {
         const int b = (int)(j & 1);
         KeyBatch dk{};
-        int rc = stage_chunk(c, kb, chunks[j], b, &dk);
+        int rc = stage_chunk(c, kb, chunks[j], b, &dk, chunks.size() == 1);
         if (rc) return rc;
         rc = build_dispatch(dk, dwords, md, c->s_comp, c->ws.p, c->ws.cap, [&](uint64_t need, void **out) -> int {
             HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));  // previous chunks may still use it
@@ -923,12 +927,18 @@ static int probe_device_to_host(seb_ctx *c, const seb_keys *kb, const uint32_t *
     for (size_t j = 0; j < chunks.size(); ++j) {
         const int b = (int)(j & 1);
         KeyBatch dk{};
-        int rc = stage_chunk(c, kb, chunks[j], b, &dk);
+        const bool single = chunks.size() == 1;  // copy in, probe, copy out on s_comp alone
+        int rc = stage_chunk(c, kb, chunks[j], b, &dk, single);
         if (rc) return rc;
         const uint64_t cnt = dk.n;
         if ((rc = c->out[b].reserve(cnt))) return rc;
-        HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));  // out[b] drained
+        if (!single) HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));  // out[b] drained
         if ((rc = probe_dispatch(dk, dwords, md, (uint8_t *)c->out[b].p, c->s_comp))) return rc;
+        if (single) {
+            HIP_OR_FAIL(hipMemcpyAsync(out + chunks[j].i0, c->out[b].p, cnt, hipMemcpyDeviceToHost, c->s_comp));
+            HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));
+            return SEB_OK;
+        }
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
         HIP_OR_FAIL(hipMemcpyAsync(out + chunks[j].i0, c->out[b].p, cnt, hipMemcpyDeviceToHost, c->s_d2h));
@@ -1008,7 +1018,7 @@ extern "C" int seb_probe_multi(seb_ctx *c, const seb_keys *kb, const seb_filter_
     for (size_t j = 0; j < chunks.size(); ++j) {
         const int b = (int)(j & 1);
         KeyBatch dk{};
-        if ((rc = stage_chunk(c, kb, chunks[j], b, &dk))) return rc;
+        if ((rc = stage_chunk(c, kb, chunks[j], b, &dk, false))) return rc;
         if ((rc = c->out[b].reserve(dk.n * 8))) return rc;
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));
         HIP_OR_FAIL(launch_probe_multi(dk, ma, c->out[b].p, 8, c->s_comp));
@@ -1134,7 +1144,8 @@ struct seb_filter {
     bool host_ok = true;
     bool host_zero = false;     // New, nothing built yet: the device copy starts as a memset
     std::atomic<bool> readable{false};  // host_ok, nothing pending, usable: lock-free MayContain
-    std::vector<uint8_t> pend;       // deferred Add arena
+    std::unique_ptr<uint8_t[]> pend; // deferred Add arena: pend_bytes of pend_capb used
+    uint64_t pend_bytes = 0, pend_capb = 0;
     std::vector<uint64_t> pend_off;  // n+1 offsets into pend, only once lengths differ
     uint64_t pend_n = 0;
     uint64_t pend_len = kNoLen;      // the common key length, or kMixedLen
@@ -1251,7 +1262,13 @@ static int build_into_filter(seb_filter *f, const seb_keys *kb) {
     f->host_zero = false;
     f->readable.store(false, std::memory_order_relaxed);
     if ((rc = build_device_from_host(L.c, kb, f->dwords, mod_arg(f->m, f->k), fresh))) return rc;
+    // the host copy follows in the same stream (Encode or a first MayContain comes next on the
+    // flush path): one synchronisation for build and copy
+    const bool mirror = f->nbytes <= (64ull << 20);
+    if (mirror && f->nbytes)
+        HIP_OR_FAIL(hipMemcpyAsync(f->host.data(), f->dwords, f->nbytes, hipMemcpyDeviceToHost, L.c->s_comp));
     HIP_OR_FAIL(hipStreamSynchronize(L.c->s_comp));
+    f->host_ok = mirror;
     return SEB_OK;
 }
 
@@ -1260,14 +1277,27 @@ static int flush_locked(seb_filter *f) {
     int rc = usable(f, "BloomFilter.Add");
     if (rc) return rc;
     const bool uniform = f->pend_len != kMixedLen;
-    seb_keys kb{f->pend.data(), uniform ? nullptr : f->pend_off.data(), f->pend_n,
+    seb_keys kb{f->pend.get(), uniform ? nullptr : f->pend_off.data(), f->pend_n,
                 uniform ? (uint32_t)f->pend_len : 0u, 0};
     if ((rc = build_into_filter(f, &kb))) return rc;
-    f->pend.clear();
+    f->pend_bytes = 0;
     f->pend_off.clear();
     f->pend_n = 0;
     f->pend_len = kNoLen;
+    publish_locked(f);
     return SEB_OK;
+}
+
+// Room for `more` bytes in the Add arena (doubling); false when memory runs out.
+static bool arena_reserve(seb_filter *f, uint64_t more) {
+    if (f->pend_bytes + more <= f->pend_capb) return true;
+    uint64_t cap = std::max<uint64_t>({f->pend_bytes + more, 2 * f->pend_capb, 4096});
+    uint8_t *p = new (std::nothrow) uint8_t[cap];
+    if (!p) return false;
+    if (f->pend_bytes) memcpy(p, f->pend.get(), f->pend_bytes);
+    f->pend.reset(p);
+    f->pend_capb = cap;
+    return true;
 }
 
 extern "C" seb_filter *seb_filter_new(int64_t n, double p) {
@@ -1286,7 +1316,7 @@ extern "C" seb_filter *seb_filter_new(int64_t n, double p) {
     long cap;
     if (env_flag("SEB_PENDING_CAP", &cap) && cap > 0) f->pend_cap = (uint64_t)cap;
     // the caller's expectedKeys: room for that many 16-B keys (the arena still grows past it)
-    if (n > 0) f->pend.reserve((size_t)std::min<uint64_t>((uint64_t)n * 16, f->pend_cap));
+    if (n > 0) (void)arena_reserve(f, std::min<uint64_t>((uint64_t)n * 16, f->pend_cap));
     publish_locked(f);  // an empty filter answers false everywhere
     return f;
 }
@@ -1314,12 +1344,16 @@ extern "C" int seb_filter_add(seb_filter *f, const uint8_t *key, uint64_t len) {
             f->pend_len = kMixedLen;
         }
     }
-    const size_t at = f->pend.size();
-    f->pend.resize(at + len);
-    if (len) memcpy(f->pend.data() + at, key, len);
+    if (!arena_reserve(f, len)) return fail(SEB_ERR_NOMEM, "BloomFilter.Add: arena of %llu B", (unsigned long long)len);
+    uint8_t *dst = f->pend.get() + f->pend_bytes;
+    if (len == 16)
+        memcpy(dst, key, 16);  // the reference's fixed-size keys: one 16-B move
+    else if (len)
+        memcpy(dst, key, len);
+    f->pend_bytes += len;
     ++f->pend_n;
-    if (f->pend_len == kMixedLen) f->pend_off.push_back(f->pend.size());
-    if (f->pend.size() >= f->pend_cap || f->pend_n >= (1ull << 32)) return flush_locked(f);
+    if (f->pend_len == kMixedLen) f->pend_off.push_back(f->pend_bytes);
+    if (f->pend_bytes >= f->pend_cap || f->pend_n >= (1ull << 32)) return flush_locked(f);
     return SEB_OK;
 }
 
@@ -1331,7 +1365,9 @@ extern "C" int seb_filter_add_batch(seb_filter *f, const seb_keys *kb) {
     if ((rc = usable(f, "BloomFilter.Add"))) return rc;
     if ((rc = flush_locked(f))) return rc;  // keep Add order: earlier single Adds first
     if (kb->n == 0) return SEB_OK;
-    return build_into_filter(f, kb);
+    if ((rc = build_into_filter(f, kb))) return rc;
+    publish_locked(f);
+    return SEB_OK;
 }
 
 extern "C" int seb_filter_may_contain_batch(seb_filter *f, const seb_keys *kb, uint8_t *out) {
@@ -1719,7 +1755,7 @@ static int registry_multiget_host_locked(seb_registry *r, const seb_keys *kb, ui
     for (size_t j = 0; j < chunks.size(); ++j) {
         const int b = (int)(j & 1);
         KeyBatch dk{};
-        if ((rc = stage_chunk(c, kb, chunks[j], b, &dk))) return rc;
+        if ((rc = stage_chunk(c, kb, chunks[j], b, &dk, false))) return rc;
         if ((rc = c->out[b].reserve(dk.n * per_key))) return rc;
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));
         uint32_t *order = nullptr;
