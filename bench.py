@@ -896,17 +896,20 @@ def main():
                 "S": 64, "bytes_per_key": spk,
                 "GB/s": {d: round(st.n * spk[d] / (kern_ms[d] * 1e-3) / 1e9, 1) for d in spk if d in kern_ms},
                 "note": "modelled bytes, most of them L2 hits; not comparable to the HBM peak"}
-            # The probe's real bound: filter-word gathers, counted offline per call
-            # with the oracle (tools/gather_count.py), against the measured L2-resident ceiling.
+        if args.config in ("c2c3", "lsm", "lsm_wide"):
+            # The probe's real bound: filter-word gathers, counted offline per
+            # call with the oracle (tools/gather_count.py, tools/gather_count_lsm.py), against the
+            # measured L2-resident ceiling.
             gpath = os.path.join(ROOT, "profiles", "gathers_c2c3.json")
             ceil, csrc = gather_ceiling()
-            if world == 1 and "probe" in kern_ms and ceil and os.path.exists(gpath):
+            if world == 1 and "probe" in kern_ms and ceil and os.path.exists(gpath) and args.lsm_order == "batch":
                 with open(gpath) as f:
-                    gc = json.load(f).get("c2c3", {}).get("probe")
+                    gc = json.load(f).get(args.config, {}).get("probe")
                 if gc and gc["n"] == st.n:
-                    rate = gc["gathers_phased"] / (kern_ms["probe"] * 1e-3) / 1e9
+                    cnt = gc.get("gathers_phased", gc.get("gathers"))
+                    rate = cnt / (kern_ms["probe"] * 1e-3) / 1e9
                     result["roofline"]["gather_model"] = {
-                        "gathers_per_call": gc["gathers_phased"], "Ggathers_s": round(rate, 1),
+                        "gathers_per_call": cnt, "Ggathers_s": round(rate, 1),
                         "ceiling_Ggathers_s": ceil, "frac": round(rate / ceil, 3),
                         "count_source": "profiles/gathers_c2c3.json", "ceiling_source": csrc}
         if world == 1 and args.config == "c2c3" and not args.no_host_inclusive:

@@ -30,7 +30,8 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STEP_KERNELS = {  # per config: timed step name -> kernels launched by that step
-    "c2c3": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned"), "probe": ("k_probe",)},
+    "c2c3": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned", "k_clear_words"),
+             "probe": ("k_probe",)},
     "c4": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned", "k_hash_varlen"),
            "probe": ("k_probe", "k_hash_varlen")},
     "c5": {"probe": ("k_probe_interleaved", "k_interleave", "k_probe_multi")},

@@ -4,6 +4,10 @@
 // likewise, and the two together on complementary CU sets.  If gathers keep their rate on half of
 // the CUs, a gather-bound phase can share the chip with a VALU-bound kernel.
 // Build: hipcc --offload-arch=gfx950 -O3 cumask.hip -o cumask
+// Run: cumask TABLE_BYTES CONFIG  — one mask configuration per process (at most two CU-masked
+// streams: each takes a hardware queue of its own, and the box has GPU_MAX_HW_QUEUES = 4; in one
+// process creating the 4th-6th masked stream stalled until the time limit, round 2).  Driven by
+// tools/ubench/run_cumask.py, a parent that never touches the GPU.  Every HIP call is checked.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -42,29 +46,47 @@ __global__ __launch_bounds__(256) void k_valu(uint64_t n, uint32_t seed, uint64_
     out[i] = h1 ^ h2;
 }
 
+#define CHECK(expr)                                                                          \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #expr, hipGetErrorString(e_)); \
+            exit(3);                                                                         \
+        }                                                                                    \
+    } while (0)
+
 static hipStream_t make_stream(const std::vector<uint32_t> &mask) {
     hipStream_t s;
-    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
-        fprintf(stderr, "cu mask stream failed\n");
-        exit(1);
-    }
+    CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
     return s;
 }
 
-int main() {
+int main(int argc, char **argv) {
+    if (argc != 3) {
+        fprintf(stderr, "usage: %s TABLE_BYTES CONFIG(0-4)\n", argv[0]);
+        return 2;
+    }
+    const uint32_t tb = (uint32_t)strtoul(argv[1], 0, 0);
+    const int cfg = atoi(argv[2]);
+    if (tb < 4096 || tb > (16u << 20) || (tb & (tb - 1)) || cfg < 0 || cfg > 4) {
+        fprintf(stderr, "table bytes must be a power of two in [4K, 16M], config 0-4\n");
+        return 2;
+    }
     int ncu = 0;
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+    CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
     const uint32_t words = (uint32_t)((ncu + 31) / 32);
     const uint64_t n = 10000000;
     uint32_t *out, *tab;
     uint64_t *vout;
-    hipMalloc(&out, n * 4);
-    hipMalloc(&vout, n * 8);
-    hipMalloc(&tab, 16ull << 20);
-    hipMemset(tab, 1, 16ull << 20);
-    hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
+    CHECK(hipMalloc(&out, n * 4));
+    CHECK(hipMalloc(&vout, n * 8));
+    CHECK(hipMalloc(&tab, 16ull << 20));
+    CHECK(hipMemset(tab, 1, 16ull << 20));
+    hipEvent_t e0, e1, da, db;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    CHECK(hipEventCreate(&da));
+    CHECK(hipEventCreate(&db));
 
     auto mk = [&](auto pred) {
         std::vector<uint32_t> m(words, 0u);
@@ -86,48 +108,42 @@ int main() {
     auto time_it = [&](hipStream_t sa, hipStream_t sb, bool g, bool v, uint32_t tmask) {
         float best = 1e30f;
         for (int rep = 0; rep < 5; ++rep) {
-            hipDeviceSynchronize();
-            hipEventRecord(e0, 0);
-            hipStreamWaitEvent(sa, e0, 0);
-            hipStreamWaitEvent(sb, e0, 0);
+            CHECK(hipDeviceSynchronize());
+            CHECK(hipEventRecord(e0, 0));
+            CHECK(hipStreamWaitEvent(sa, e0, 0));
+            CHECK(hipStreamWaitEvent(sb, e0, 0));
             for (int it = 0; it < 5; ++it) {
                 if (g) hipLaunchKernelGGL(k_gather7, dim3((gn + 255) / 256), dim3(256), 0, sa, tab, tmask, gn, 77u + it, out);
                 if (v) hipLaunchKernelGGL(k_valu, dim3((vn + 255) / 256), dim3(256), 0, sb, vn, 5u + it, vout);
+                CHECK(hipGetLastError());
             }
-            hipEvent_t da, db;
-            hipEventCreate(&da);
-            hipEventCreate(&db);
-            hipEventRecord(da, sa);
-            hipEventRecord(db, sb);
-            hipStreamWaitEvent(0, da, 0);
-            hipStreamWaitEvent(0, db, 0);
-            hipEventRecord(e1, 0);
-            hipEventSynchronize(e1);
+            CHECK(hipEventRecord(da, sa));
+            CHECK(hipEventRecord(db, sb));
+            CHECK(hipStreamWaitEvent(0, da, 0));
+            CHECK(hipStreamWaitEvent(0, db, 0));
+            CHECK(hipEventRecord(e1, 0));
+            CHECK(hipEventSynchronize(e1));
             float ms;
-            hipEventElapsedTime(&ms, e0, e1);
-            hipEventDestroy(da);
-            hipEventDestroy(db);
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
             if (ms / 5 < best) best = ms / 5;
         }
         return best;
     };
-    for (uint32_t tb : {1u << 20, 4u << 20}) {
-        const uint32_t tmask = tb / 4 - 1;
-        for (auto &mm : masks) {
-            hipStream_t sa = make_stream(mm.a);
-            hipStream_t sb = mm.b.empty() ? sa : make_stream(mm.b);
-            const float g_a = time_it(sa, sa, true, false, tmask);
-            const float v_b = time_it(sb, sb, false, true, tmask);
-            const float both = time_it(sa, sb, true, true, tmask);
-            const float g_b = mm.b.empty() ? g_a : time_it(sb, sb, true, false, tmask);
-            printf("{\"table_bytes\": %u, \"masks\": \"%s\", \"gather_on_a_ms\": %.4f, \"Ggathers_s_a\": %.1f, "
-                   "\"gather_on_b_ms\": %.4f, \"valu_on_b_ms\": %.4f, \"both_concurrent_ms\": %.4f, "
-                   "\"sum_ms\": %.4f}\n",
-                   tb, mm.name, g_a, 7.0 * gn / (g_a * 1e-3) / 1e9, g_b, v_b, both, g_a + v_b);
-            fflush(stdout);
-            hipStreamDestroy(sa);
-            if (sb != sa) hipStreamDestroy(sb);
-        }
-    }
+    const uint32_t tmask = tb / 4 - 1;
+    const M &mm = masks[cfg];
+    hipStream_t sa = make_stream(mm.a);
+    hipStream_t sb = mm.b.empty() ? sa : make_stream(mm.b);
+    const float g_a = time_it(sa, sa, true, false, tmask);
+    const float v_b = time_it(sb, sb, false, true, tmask);
+    const float both = time_it(sa, sb, true, true, tmask);
+    const float g_b = mm.b.empty() ? g_a : time_it(sb, sb, true, false, tmask);
+    printf("{\"table_bytes\": %u, \"masks\": \"%s\", \"gather_on_a_ms\": %.4f, \"Ggathers_s_a\": %.1f, "
+           "\"gather_on_b_ms\": %.4f, \"valu_on_b_ms\": %.4f, \"both_concurrent_ms\": %.4f, "
+           "\"sum_ms\": %.4f}\n",
+           tb, mm.name, g_a, 7.0 * gn / (g_a * 1e-3) / 1e9, g_b, v_b, both, g_a + v_b);
+    fflush(stdout);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipStreamDestroy(sa));
+    if (sb != sa) CHECK(hipStreamDestroy(sb));
     return 0;
 }
