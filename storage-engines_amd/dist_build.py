@@ -124,6 +124,8 @@ class PartitionedProbe:
             probe_fn(keys, words, m, k, self.out[: self.hi - self.lo])
         if self.world == 1:
             return self.out[: self.n]
+        if self.n == 0:  # an empty batch: nothing to gather (chunk() of an empty tensor is one chunk)
+            return self.out[:0] if self.rank == dst else None
         chunks = list(self.all.chunk(self.world)) if self.rank == dst else None
         dist.gather(self.out[: self.width], gather_list=chunks, dst=dst, group=self.group)
         if self.rank != dst:

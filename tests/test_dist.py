@@ -265,7 +265,7 @@ def _pprobe_worker(rank, world, port, n, nq, dst, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,nq,dst", [(2, 20_001, 0), (3, 30_000, 2), (3, 2, 0)])
+@pytest.mark.parametrize("world,nq,dst", [(2, 20_001, 0), (3, 30_000, 2), (3, 2, 0), (2, 0, 0), (3, 0, 1)])
 def test_partitioned_probe_of_one_filter(world, nq, dst):
     """dist_build.PartitionedProbe: the filter replicated from its owner, the batch split by key
     over the ranks, answers gathered in batch order = the oracle's MayContain of every key."""
