@@ -775,12 +775,42 @@ struct DevBuf {
     }
 };
 
+// Grow-only host-pinned buffer (device-accessible), for the small builds' zero-copy path.
+struct PinBuf {
+    void *p = nullptr;
+    void *dev = nullptr;  // the device's address of p
+    uint64_t cap = 0;
+    int reserve(uint64_t bytes) {
+        if (bytes <= cap) return SEB_OK;
+        release();
+        uint64_t want = std::max<uint64_t>(bytes, 1 << 20);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return (void)hipGetLastError(), fail(SEB_ERR_NOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)want,
+                                                 hipGetErrorString(e));
+        }
+        if ((e = hipHostGetDevicePointer(&dev, p, 0)) != hipSuccess) {
+            release();
+            return (void)hipGetLastError(), fail(SEB_ERR_DEVICE, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+        }
+        cap = want;
+        return SEB_OK;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = dev = nullptr;
+        cap = 0;
+    }
+};
+
 struct seb_ctx {
     int device = 0;
     std::mutex mu;
     hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr;
     hipEvent_t ev_h2d[2] = {}, ev_comp[2] = {}, ev_d2h[2] = {};
     DevBuf keys[2], offs[2], out[2], words, filt, ws;
+    PinBuf hkeys, hbits;  // small filter builds: keys in, bits out, read and written by the kernels
     uint64_t chunk_bytes = 64ull << 20;
     std::vector<uint64_t> off_tmp[2];
 };
@@ -826,6 +856,8 @@ extern "C" void seb_ctx_destroy(seb_ctx *c) {
     c->words.release();
     c->filt.release();
     c->ws.release();
+    c->hkeys.release();
+    c->hbits.release();
     if (c->s_h2d) (void)hipStreamDestroy(c->s_h2d);
     if (c->s_comp) (void)hipStreamDestroy(c->s_comp);
     if (c->s_d2h) (void)hipStreamDestroy(c->s_d2h);
@@ -1261,10 +1293,44 @@ static int build_into_filter(seb_filter *f, const seb_keys *kb) {
     f->host_ok = false;  // the device copy is about to move ahead of the host copy
     f->host_zero = false;
     f->readable.store(false, std::memory_order_relaxed);
+    // Flush- and compaction-sized builds (keys and bits up to 16 MiB each) are zero-copy: the keys
+    // are staged in host-pinned memory that the build kernels read over PCIe, and a kernel writes
+    // the bits back into pinned memory.  The DMA copies they replace started ~8 us (keys) and ~16 us
+    // (bits) after the work before them ended (profiles/r03_flush_trace.txt).
+    const uint64_t kbytes = kb->offsets ? kb->offsets[kb->n] - kb->offsets[0] : kb->n * (uint64_t)kb->stride;
+    const uint64_t obytes = kb->offsets ? (kb->n + 1) * 8 : 0;
+    const bool zc = kbytes <= (16ull << 20) && obytes <= (8ull << 20) && f->nbytes <= (16ull << 20);
+    const bool mirror = f->nbytes <= (64ull << 20);
+    if (zc) {
+        const uint64_t kpad = (kbytes + 15) & ~15ull;
+        if ((rc = L.c->hkeys.reserve(kpad + obytes + 16)) || (rc = L.c->hbits.reserve(f->nbytes + 16))) return rc;
+        uint8_t *hk = (uint8_t *)L.c->hkeys.p;
+        if (kbytes) memcpy(hk, kb->data + (kb->offsets ? kb->offsets[0] : 0), kbytes);
+        KeyBatch dk{(const uint8_t *)L.c->hkeys.dev, nullptr, kb->n, kb->stride};
+        if (kb->offsets) {
+            uint64_t *ho = (uint64_t *)(hk + kpad);
+            const uint64_t o0 = kb->offsets[0];
+            for (uint64_t i = 0; i <= kb->n; ++i) ho[i] = kb->offsets[i] - o0;
+            dk.offsets = (const uint64_t *)((uint8_t *)L.c->hkeys.dev + kpad);
+        }
+        seb_ctx *c = L.c;
+        rc = build_dispatch(dk, f->dwords, mod_arg(f->m, f->k), c->s_comp, c->ws.p, c->ws.cap,
+                            [&](uint64_t need, void **out) -> int {
+                                HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));
+                                int r = c->ws.reserve(need);
+                                *out = c->ws.p;
+                                return r;
+                            }, fresh);
+        if (rc) return rc;
+        HIP_OR_FAIL(launch_copy_out(f->dwords, (uint8_t *)c->hbits.dev, f->nbytes, c->s_comp));
+        HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));
+        if (f->nbytes) memcpy(f->host.data(), c->hbits.p, f->nbytes);
+        f->host_ok = true;
+        return SEB_OK;
+    }
     if ((rc = build_device_from_host(L.c, kb, f->dwords, mod_arg(f->m, f->k), fresh))) return rc;
     // the host copy follows in the same stream (Encode or a first MayContain comes next on the
     // flush path): one synchronisation for build and copy
-    const bool mirror = f->nbytes <= (64ull << 20);
     if (mirror && f->nbytes)
         HIP_OR_FAIL(hipMemcpyAsync(f->host.data(), f->dwords, f->nbytes, hipMemcpyDeviceToHost, L.c->s_comp));
     HIP_OR_FAIL(hipStreamSynchronize(L.c->s_comp));

@@ -109,6 +109,8 @@ struct Options {
 Options &options();
 
 hipError_t launch_build(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s);
+// Copy `bytes` of filter words to host-pinned memory (both 16-B aligned) with a kernel.
+hipError_t launch_copy_out(const uint32_t *words, uint8_t *host, uint64_t bytes, hipStream_t s);
 // Zero `bytes` (a multiple of 16) of filter words.
 hipError_t launch_clear_words(uint32_t *words, uint64_t bytes, hipStream_t s);
 bool bucketed_supported(uint64_t m, uint32_t k);

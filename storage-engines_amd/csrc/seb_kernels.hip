@@ -716,6 +716,26 @@ hipError_t launch_clear_words(uint32_t *words, uint64_t bytes, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Copy `bytes` of device words to host-pinned memory with 16-B stores over PCIe (the small
+// builds' bits back to the host): a kernel in the build's stream, where a DMA copy would start
+// ~16 us after the build ends (profiles/r03_flush_trace.txt).  dst and src 16-B aligned.
+__global__ __launch_bounds__(256) void k_copy_out(const uint4 *__restrict__ src, uint4 *__restrict__ dst, uint64_t n16,
+                                                  const uint8_t *__restrict__ tail_src, uint8_t *__restrict__ tail_dst,
+                                                  uint32_t tail) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n16) dst[i] = src[i];
+    if (i < tail) tail_dst[i] = tail_src[i];
+}
+
+hipError_t launch_copy_out(const uint32_t *words, uint8_t *host, uint64_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    const uint64_t n16 = bytes / 16, tail = bytes % 16;
+    const uint64_t items = n16 > tail ? n16 : tail;
+    hipLaunchKernelGGL(k_copy_out, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, (const uint4 *)words,
+                       (uint4 *)host, n16, (const uint8_t *)words + n16 * 16, host + n16 * 16, (uint32_t)tail);
+    return hipGetLastError();
+}
+
 hipError_t launch_build(const KeyBatch &kb, uint32_t *words, const ModArg &md, hipStream_t s) {
     if (kb.n == 0 || md.k == 0) return hipSuccess;
     const bool m32 = md.m < kM32Limit;
