@@ -1293,28 +1293,32 @@ static int build_into_filter(seb_filter *f, const seb_keys *kb) {
     f->host_ok = false;  // the device copy is about to move ahead of the host copy
     f->host_zero = false;
     f->readable.store(false, std::memory_order_relaxed);
-    // Flush- and compaction-sized builds (keys and bits up to 16 MiB each) are zero-copy: the keys
-    // are staged in host-pinned memory that the build kernels read over PCIe, and a kernel writes
-    // the bits back into pinned memory.  The DMA copies they replace started ~8 us (keys) and ~16 us
-    // (bits) after the work before them ended (profiles/r03_flush_trace.txt).
+    // Small builds skip the DMA engine, whose copies started ~8 us (keys in) and ~16 us (bits out)
+    // after the work before them ended (profiles/r03_flush_trace.txt).  Keys: a device-scope-atomic
+    // build (flush sizes, one thread per key, hundreds of workgroups) reads them straight from
+    // host-pinned staging over PCIe; the LDS builds (a dozen workgroups) read too few at a time for
+    // that and get a DMA copy.  Bits: a kernel writes filters up to 16 MiB into pinned memory.
+    const ModArg md = mod_arg(f->m, f->k);
     const uint64_t kbytes = kb->offsets ? kb->offsets[kb->n] - kb->offsets[0] : kb->n * (uint64_t)kb->stride;
     const uint64_t obytes = kb->offsets ? (kb->n + 1) * 8 : 0;
-    const bool zc = kbytes <= (16ull << 20) && obytes <= (8ull << 20) && f->nbytes <= (16ull << 20);
+    const bool zc_keys = choose_build_algo(kb->n, f->m, f->k) == 1 && kbytes <= (16ull << 20) &&
+                         obytes <= (8ull << 20) && !(kb->offsets && kb->n >= options().varlen_prehash_min_keys);
+    const bool zc_bits = f->nbytes <= (16ull << 20);
     const bool mirror = f->nbytes <= (64ull << 20);
-    if (zc) {
+    seb_ctx *c = L.c;
+    if (zc_keys) {
         const uint64_t kpad = (kbytes + 15) & ~15ull;
-        if ((rc = L.c->hkeys.reserve(kpad + obytes + 16)) || (rc = L.c->hbits.reserve(f->nbytes + 16))) return rc;
-        uint8_t *hk = (uint8_t *)L.c->hkeys.p;
+        if ((rc = c->hkeys.reserve(kpad + obytes + 16))) return rc;
+        uint8_t *hk = (uint8_t *)c->hkeys.p;
         if (kbytes) memcpy(hk, kb->data + (kb->offsets ? kb->offsets[0] : 0), kbytes);
-        KeyBatch dk{(const uint8_t *)L.c->hkeys.dev, nullptr, kb->n, kb->stride};
+        KeyBatch dk{(const uint8_t *)c->hkeys.dev, nullptr, kb->n, kb->stride};
         if (kb->offsets) {
             uint64_t *ho = (uint64_t *)(hk + kpad);
             const uint64_t o0 = kb->offsets[0];
             for (uint64_t i = 0; i <= kb->n; ++i) ho[i] = kb->offsets[i] - o0;
-            dk.offsets = (const uint64_t *)((uint8_t *)L.c->hkeys.dev + kpad);
+            dk.offsets = (const uint64_t *)((uint8_t *)c->hkeys.dev + kpad);
         }
-        seb_ctx *c = L.c;
-        rc = build_dispatch(dk, f->dwords, mod_arg(f->m, f->k), c->s_comp, c->ws.p, c->ws.cap,
+        rc = build_dispatch(dk, f->dwords, md, c->s_comp, c->ws.p, c->ws.cap,
                             [&](uint64_t need, void **out) -> int {
                                 HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));
                                 int r = c->ws.reserve(need);
@@ -1322,18 +1326,19 @@ static int build_into_filter(seb_filter *f, const seb_keys *kb) {
                                 return r;
                             }, fresh);
         if (rc) return rc;
-        HIP_OR_FAIL(launch_copy_out(f->dwords, (uint8_t *)c->hbits.dev, f->nbytes, c->s_comp));
-        HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));
-        if (f->nbytes) memcpy(f->host.data(), c->hbits.p, f->nbytes);
-        f->host_ok = true;
-        return SEB_OK;
+    } else if ((rc = build_device_from_host(c, kb, f->dwords, md, fresh))) {
+        return rc;
     }
-    if ((rc = build_device_from_host(L.c, kb, f->dwords, mod_arg(f->m, f->k), fresh))) return rc;
     // the host copy follows in the same stream (Encode or a first MayContain comes next on the
     // flush path): one synchronisation for build and copy
-    if (mirror && f->nbytes)
-        HIP_OR_FAIL(hipMemcpyAsync(f->host.data(), f->dwords, f->nbytes, hipMemcpyDeviceToHost, L.c->s_comp));
-    HIP_OR_FAIL(hipStreamSynchronize(L.c->s_comp));
+    if (zc_bits) {
+        if ((rc = c->hbits.reserve(f->nbytes + 16))) return rc;
+        HIP_OR_FAIL(launch_copy_out(f->dwords, (uint8_t *)c->hbits.dev, f->nbytes, c->s_comp));
+    } else if (mirror && f->nbytes) {
+        HIP_OR_FAIL(hipMemcpyAsync(f->host.data(), f->dwords, f->nbytes, hipMemcpyDeviceToHost, c->s_comp));
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));
+    if (zc_bits && f->nbytes) memcpy(f->host.data(), c->hbits.p, f->nbytes);
     f->host_ok = mirror;
     return SEB_OK;
 }
