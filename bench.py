@@ -33,6 +33,7 @@ import glob
 import hashlib
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -91,6 +92,8 @@ def parse():
     ap.add_argument("--keys", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="c2c3 at N=1: skip the secondary lines (lsm, lsm_wide, flush) run as child processes")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--lsm-order", default="batch", choices=["batch", "sorted"],
@@ -628,7 +631,6 @@ def launch_ranks(args, argv) -> int:
     has N GPUs for the RCCL backend, then starts N child processes of this same script, one per
     GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N), and exits with the first failing child's status.
     Rank 0 prints the JSON line.  gloo (a rehearsal) may put several ranks on one GPU."""
-    import subprocess
 
     n = args.gpus
     if not args.launch_check:
@@ -689,7 +691,6 @@ def run_flush(args):
     includes the arena, the H2D copy, the build launch and the D2H copy.  value = flush-size
     filter builds, in keys per second end to end.  The oracle's C restatement is timed beside each
     (cpu_baseline), and every digest is checked against it."""
-    import subprocess
 
     exe = os.path.join(ROOT, "storage-engines_amd", "lib", "flush_bench")
     sizes = [50_000, 100_000]
@@ -978,11 +979,49 @@ def main():
             result["host_inclusive"] = host_inclusive(seb, st.build_host, st.probe_host, st.m, st.k)
         if world == 1 and not args.no_cpu_baseline and args.config in ("c2c3", "c4"):
             result["cpu_baseline"] = cpu_baseline(args, st.n, st.m, st.k)
+        if world == 1 and args.config == "c2c3" and not args.no_secondary:
+            result["secondary"] = secondary_lines()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     if result is not None:
         print(json.dumps(result), flush=True)
+
+
+SECONDARY = (("lsm", ["--steps", "10", "--warmup", "3"]), ("lsm_wide", ["--steps", "10", "--warmup", "3"]),
+             ("flush", []))
+
+
+def secondary_lines():
+    """The other SURVEY 8 rows on the default (driver-run) line, each from its own child process
+    (`bench.py --config X`, the same code path as run alone) after the headline's timed region:
+    the registry MultiGet (f1/f2, 28 and 244 files) and the drop-in ABI at flush/compaction size
+    (b).  A compact summary of each child's JSON line; a failure is recorded, never fatal."""
+    out = []
+    for cfg, extra in SECONDARY:
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", cfg, "--no-secondary", *extra]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+            line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+        except Exception as e:  # noqa: BLE001 - reported in the line, the headline stands
+            out.append({"config": cfg, "error": f"{type(e).__name__}: {str(e)[:200]}"})
+            continue
+        item = {"config": cfg, "workload": line.get("config", {}).get("workload"),
+                "metric": line.get("metric") if cfg == "flush" else "registry MultiGet Mkeys/s (10M keys)",
+                "value": line.get("value"), "unit": line.get("unit"),
+                "ms_per_step": line.get("ms_per_step"), "parity": line.get("parity")}
+        gm = line.get("roofline", {}).get("gather_model")
+        if gm:
+            item["gather_model"] = {k: gm[k] for k in ("gathers_per_call", "Ggathers_s", "ceiling_Ggathers_s", "frac")}
+        if cfg == "flush":
+            item["sizes"] = [{"n": z["n"], "shim_us": z["shim_us"]["total"], "per_key_add_us": z["build_us"]["total"],
+                              "may_contain_ns_1t": z["may_contain"]["ns_per_call_1t"],
+                              "may_contain_calls_s_8t": z["may_contain"]["calls_per_s"]} for z in line["sizes"]]
+            cb = line.get("cpu_baseline")
+            if cb:
+                item["cpu_baseline_build_us"] = {k: v["build_us"] for k, v in cb["per_size"].items()}
+        out.append(item)
+    return out
 
 
 def host_inclusive(seb, build_host, probe_host, m, k):

@@ -158,17 +158,25 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
 
 // ---- key-range order (multiget_order).  A batch probed in key order gathers from a few files of
 // each level at a time, so those filters stay in L2: a key-sorted 10M batch took 0.70 ms against
-// 1.47 ms in batch order (bench.py --lsm-order sorted).  Three small launches put the batch in
-// that order without sorting it: k_mg_bucket finds each key's bucket, the number of files of the
-// partition level (the disjoint level with the most files) whose MinKey <= key, which is
-// monotone in the key; k_mg_scan turns the bucket counts into cursors; k_mg_scatter writes the
-// key indices bucket by bucket (each tile reserves its runs with one atomic per bucket).
+// 1.47 ms in batch order (bench.py --lsm-order sorted).  The batch is put in that order without
+// sorting it, by one counting pass over the buckets of the partition level (the disjoint level
+// with the most files; a key's bucket = the number of its files whose MinKey <= key, monotone in
+// the key), like one digit of a radix sort:
+//   k_mg_bucket   tile t of the batch: each key's bucket, and the tile's bucket counts at
+//                 hist[b * T + t] (bucket-major, so one exclusive scan of hist yields every
+//                 (bucket, tile) output offset)
+//   k_mg_rows     scans each bucket's row of T tile counts in place, and writes the row total
+//   k_mg_scatter  tile t: scans the row totals into bucket bases, then per chunk of kMgChunk keys
+//                 sorts the key indices by bucket in LDS and writes each bucket's run of indices,
+//                 and of 16-B keys read through them (lines of the chunk just fetched into L2),
+//                 contiguously
 // k_multiget then walks `order` and writes every answer at the key's own index, so the results
-// are those of the batch order.  Measured (gpurun_out/s3k, 28-file layout): bucket 239 us, scatter
-// 48 us, and k_multiget through `order` 1683 us against 1470 in batch order: its key loads and
-// answer stores become 64-B sector accesses per key, which costs more than the filter locality
-// saves.  Off by default; the next form materialises the keys in bucket order.
-constexpr uint32_t kMgTile = 4096;  // keys per k_mg_scatter tile (one cursor atomic per bucket per tile)
+// are those of the batch order.  Round 3 replaced global cursor atomics per tile and per-lane
+// scattered stores with this (1.022 -> 1.010 ms on 28 files, 1.322 -> 1.183 ms on 244; DESIGN.md
+// 5.7 has the variants measured on the way).
+constexpr uint32_t kMgChunk = 2048;  // keys sorted in LDS at a time by k_mg_scatter
+constexpr uint32_t kMgTiles = 768;   // most tiles (blocks) of the ordering passes: one round on 256 CUs
+constexpr uint32_t kMgBucketThreads = 1024;
 
 __device__ __forceinline__ void key_at(const KeyBatch &kb, uint64_t i, const uint8_t *&key, uint32_t &klen) {
     if (kb.offsets) {
@@ -180,20 +188,55 @@ __device__ __forceinline__ void key_at(const KeyBatch &kb, uint64_t i, const uin
     }
 }
 
-__global__ __launch_bounds__(256) void k_mg_bucket(KeyBatch kb, const RegSlot *__restrict__ slots, uint32_t lo,
-                                                   uint32_t hi, const uint8_t *__restrict__ ranges,
-                                                   uint16_t *__restrict__ bucket, uint32_t *__restrict__ counts) {
-    __shared__ uint32_t h[kMgMaxBuckets];
-    __shared__ uint64_t pmin[2 * (kMgMaxBuckets - 1)];  // the level's MinKey prefixes (16 B per file)
-    const uint32_t nb = hi - lo + 1;
-    for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x) h[t] = 0;
-    for (uint32_t t = threadIdx.x; t < nb - 1; t += blockDim.x) {
-        pmin[2 * t] = slots[lo + t].min_be[0];
-        pmin[2 * t + 1] = slots[lo + t].min_be[1];
+// Exclusive scan of a[0..n) in LDS by a 256-thread block; returns the total.  Every thread must
+// call it; it synchronises before returning.
+__device__ uint32_t block_scan_lds(uint32_t *a, uint32_t n, uint32_t *wsum) {
+    const uint32_t per = (n + 255) / 256;
+    const uint32_t b0 = min(threadIdx.x * per, n), b1 = min(b0 + per, n);
+    uint32_t own = 0;
+    for (uint32_t t = b0; t < b1; ++t) own += a[t];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = own;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t run = x - own;
+    for (uint32_t v = 0; v < w; ++v) run += wsum[v];
+    const uint32_t total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    for (uint32_t t = b0; t < b1; ++t) {
+        const uint32_t c = a[t];
+        a[t] = run;
+        run += c;
     }
     __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kb.n; i += stride) {
+    return total;
+}
+
+// Tiles are whole chunks (the last one ragged): tile t = keys [t * tl, min(n, (t + 1) * tl)).
+__device__ __forceinline__ uint64_t tile_begin(uint64_t n, uint32_t tl, uint32_t t) {
+    const uint64_t b = (uint64_t)tl * t;
+    return b < n ? b : n;
+}
+
+__global__ __launch_bounds__(kMgBucketThreads) void k_mg_bucket(KeyBatch kb, const RegSlot *__restrict__ slots, uint32_t lo,
+                                                   uint32_t hi, const uint8_t *__restrict__ ranges,
+                                                   uint16_t *__restrict__ bucket, uint32_t *__restrict__ hist,
+                                                   uint32_t tl) {
+    __shared__ uint32_t h[kMgMaxBuckets];
+    __shared__ uint64_t pmin[2 * (kMgMaxBuckets - 1)];  // the level's MinKey prefixes (16 B per file)
+    const uint32_t nb = hi - lo + 1, T = gridDim.x, t = blockIdx.x;
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) h[u] = 0;
+    for (uint32_t u = threadIdx.x; u < nb - 1; u += blockDim.x) {
+        pmin[2 * u] = slots[lo + u].min_be[0];
+        pmin[2 * u + 1] = slots[lo + u].min_be[1];
+    }
+    __syncthreads();
+    const uint64_t end = tile_begin(kb.n, tl, t + 1);
+    for (uint64_t i = tile_begin(kb.n, tl, t) + threadIdx.x; i < end; i += blockDim.x) {
         const uint8_t *key;
         uint32_t klen;
         key_at(kb, i, key, klen);
@@ -221,48 +264,80 @@ __global__ __launch_bounds__(256) void k_mg_bucket(KeyBatch kb, const RegSlot *_
         atomicAdd(&h[a - lo], 1u);
     }
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x)
-        if (h[t]) atomicAdd(&counts[t], h[t]);
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) hist[(uint64_t)u * T + t] = h[u];
 }
 
-__global__ void k_mg_scan(uint32_t *counts, uint32_t nb) {  // exclusive scan in place, one thread (nb <= 1025)
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    uint32_t run = 0;
-    for (uint32_t t = 0; t < nb; ++t) {
-        const uint32_t c = counts[t];
-        counts[t] = run;
-        run += c;
-    }
+// block b: exclusive scan of hist row b (T tile counts) in place; totals[b] = the row's sum
+__global__ __launch_bounds__(256) void k_mg_rows(uint32_t *__restrict__ hist, uint32_t T,
+                                                 uint32_t *__restrict__ totals) {
+    __shared__ uint32_t row[kMgTiles];
+    __shared__ uint32_t wsum[4];
+    uint32_t *g = hist + (uint64_t)blockIdx.x * T;
+    for (uint32_t u = threadIdx.x; u < T; u += blockDim.x) row[u] = g[u];
+    __syncthreads();
+    const uint32_t total = block_scan_lds(row, T, wsum);
+    for (uint32_t u = threadIdx.x; u < T; u += blockDim.x) g[u] = row[u];
+    if (threadIdx.x == 0) totals[blockIdx.x] = total;
 }
 
 __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *__restrict__ bucket,
-                                                    uint32_t *__restrict__ cursor, uint32_t nb,
+                                                    const uint32_t *__restrict__ hist,
+                                                    const uint32_t *__restrict__ totals, uint32_t nb,
                                                     uint32_t *__restrict__ order, const uint4 *__restrict__ keys,
-                                                    uint4 *__restrict__ keys_out) {
-    __shared__ uint32_t h[kMgMaxBuckets];
-    constexpr uint32_t kPer = kMgTile / 256;
-    for (uint64_t t0 = (uint64_t)blockIdx.x * kMgTile; t0 < n; t0 += (uint64_t)gridDim.x * kMgTile) {
-        for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x) h[t] = 0;
-        __syncthreads();
-        uint32_t bk[kPer], rk[kPer];
+                                                    uint4 *__restrict__ keys_out, uint32_t tl) {
+    __shared__ uint32_t base[kMgMaxBuckets];     // next output position of each bucket for this tile
+    __shared__ uint32_t loc[kMgMaxBuckets + 1];  // chunk counts, then their exclusive scan
+    __shared__ uint32_t sidx[kMgChunk];
+    __shared__ uint16_t sb[kMgChunk];
+    __shared__ uint32_t wsum[4];
+    constexpr uint32_t kPer = kMgChunk / 256;
+    const uint32_t T = gridDim.x, t = blockIdx.x;
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] = totals[u];
+    __syncthreads();
+    block_scan_lds(base, nb, wsum);
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] += hist[(uint64_t)u * T + t];
+    const uint64_t end = tile_begin(n, tl, t + 1);
+    uint32_t bk[kPer], rk[kPer];
+    auto load = [&](uint64_t c0) {  // chunk c0's buckets into registers
+        const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, end - c0);
 #pragma unroll
         for (uint32_t r = 0; r < kPer; ++r) {
-            const uint64_t i = t0 + (uint64_t)r * 256 + threadIdx.x;
-            bk[r] = i < n ? bucket[i] : 0u;
-            rk[r] = i < n ? atomicAdd(&h[bk[r]], 1u) : 0u;
+            const uint32_t q = r * 256 + threadIdx.x;
+            bk[r] = q < cnt ? bucket[c0 + q] : 0u;
         }
-        __syncthreads();
-        for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x)
-            if (h[t]) h[t] = atomicAdd(&cursor[t], h[t]);  // this tile's run of bucket t starts here
+    };
+    uint64_t c0 = tile_begin(n, tl, t);
+    if (c0 < end) load(c0);
+    for (; c0 < end; c0 += kMgChunk) {
+        const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, end - c0);
+        for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) loc[u] = 0;
         __syncthreads();
 #pragma unroll
+        for (uint32_t r = 0; r < kPer; ++r)
+            if (r * 256 + threadIdx.x < cnt) rk[r] = atomicAdd(&loc[bk[r]], 1u);
+        __syncthreads();
+        block_scan_lds(loc, nb, wsum);
+        if (threadIdx.x == 0) loc[nb] = cnt;
+#pragma unroll
         for (uint32_t r = 0; r < kPer; ++r) {
-            const uint64_t i = t0 + (uint64_t)r * 256 + threadIdx.x;
-            if (i < n) {
-                order[h[bk[r]] + rk[r]] = (uint32_t)i;
-                if (keys_out) keys_out[h[bk[r]] + rk[r]] = keys[i];  // 16-B keys move with their index
+            const uint32_t q = r * 256 + threadIdx.x;
+            if (q < cnt) {
+                const uint32_t p = loc[bk[r]] + rk[r];
+                sidx[p] = (uint32_t)(c0 + q);
+                sb[p] = (uint16_t)bk[r];
             }
         }
+        __syncthreads();
+        if (c0 + kMgChunk < end) load(c0 + kMgChunk);  // the next chunk's buckets load during the stores
+        // each bucket's run of this chunk goes out contiguously
+        for (uint32_t q = threadIdx.x; q < cnt; q += blockDim.x) {
+            const uint32_t b = sb[q];
+            const uint32_t dst = base[b] + (q - loc[b]);
+            order[dst] = sidx[q];
+            if (keys_out) keys_out[dst] = keys[sidx[q]];
+        }
+        __syncthreads();
+        for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] += loc[u + 1] - loc[u];
         __syncthreads();
     }
 }
@@ -271,9 +346,21 @@ bool multiget_order_moves(const KeyBatch &kb) {
     return !kb.offsets && !kb.hashes && kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0;
 }
 
+static uint32_t tile_keys(uint64_t n) {  // keys per tile: whole chunks, at most kMgTiles tiles
+    const uint64_t chunks = (n + kMgChunk - 1) / kMgChunk;
+    return (uint32_t)((chunks + kMgTiles - 1) / kMgTiles) * kMgChunk;
+}
+
+static uint32_t order_tiles(uint64_t n) {
+    const uint64_t tl = tile_keys(n);
+    return n ? (uint32_t)((n + tl - 1) / tl) : 1u;
+}
+
+static uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
+
 uint64_t multiget_order_bytes(const KeyBatch &kb) {
     const uint64_t n = kb.n;
-    return ((n * 2 + 255) & ~255ull) + ((n * 4 + 255) & ~255ull) + ((4 * kMgMaxBuckets + 255) & ~255ull) +
+    return al256(n * 2) + al256(n * 4) + al256(4ull * kMgMaxBuckets * order_tiles(n)) + al256(4 * kMgMaxBuckets) +
            (multiget_order_moves(kb) ? n * 16 : 0);
 }
 
@@ -284,23 +371,20 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
     *keys_out = nullptr;
     const uint32_t nb = hi - lo + 1;
     if (kb.n == 0 || nb > kMgMaxBuckets || nb < 2 || kb.n > 0xffffffffull) return hipSuccess;
-    uint16_t *bucket = (uint16_t *)ws;
-    uint32_t *order = (uint32_t *)((uint8_t *)ws + ((kb.n * 2 + 255) & ~255ull));
-    uint32_t *counts = (uint32_t *)((uint8_t *)order + ((kb.n * 4 + 255) & ~255ull));
+    const uint32_t T = order_tiles(kb.n), tl = tile_keys(kb.n);
+    uint8_t *p = (uint8_t *)ws;
+    uint16_t *bucket = (uint16_t *)p;
+    uint32_t *order = (uint32_t *)(p += al256(kb.n * 2));
+    uint32_t *hist = (uint32_t *)(p += al256(kb.n * 4));
+    uint32_t *totals = (uint32_t *)(p += al256(4ull * kMgMaxBuckets * T));
     // aligned fixed 16-B keys are moved into bucket order as well (the MultiGet then streams them)
-    const bool move = multiget_order_moves(kb);
-    uint4 *sorted = move ? (uint4 *)((uint8_t *)counts + ((4 * kMgMaxBuckets + 255) & ~255ull)) : nullptr;
-    hipError_t e = hipMemsetAsync(counts, 0, 4 * nb, s);
+    uint4 *sorted = multiget_order_moves(kb) ? (uint4 *)(p + al256(4 * kMgMaxBuckets)) : nullptr;
+    hipLaunchKernelGGL(k_mg_bucket, dim3(T), dim3(kMgBucketThreads), 0, s, kb, slots, lo, hi, ranges, bucket, hist, tl);
+    hipLaunchKernelGGL(k_mg_rows, dim3(nb), dim3(256), 0, s, hist, T, totals);
+    hipLaunchKernelGGL(k_mg_scatter, dim3(T), dim3(256), 0, s, kb.n, bucket, hist, totals, nb, order,
+                       (const uint4 *)kb.data, sorted, tl);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    uint64_t g = (kb.n + 255) / 256;
-    if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_mg_bucket, dim3((unsigned)g), dim3(256), 0, s, kb, slots, lo, hi, ranges, bucket, counts);
-    hipLaunchKernelGGL(k_mg_scan, dim3(1), dim3(64), 0, s, counts, nb);
-    uint64_t gt = (kb.n + kMgTile - 1) / kMgTile;
-    if (gt > 2048) gt = 2048;
-    hipLaunchKernelGGL(k_mg_scatter, dim3((unsigned)gt), dim3(256), 0, s, kb.n, bucket, counts, nb, order,
-                       (const uint4 *)kb.data, sorted);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     *order_out = order;
     *keys_out = (const uint8_t *)sorted;
     return hipSuccess;

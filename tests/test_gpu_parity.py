@@ -1286,6 +1286,18 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
             want_files[i, j] = by_slot[int(s)]
     assert files_got.shape[1] == reg.max_candidates()
     assert np.array_equal(files_got, want_files)
+    # a batch past 8192 tiles x 2048 keys: tiles of two LDS-sorted chunks, the last one ragged
+    nbig = 17_000_003
+    big = to_dev(torch, kg.key16(rng.integers(0, 64000, nbig)))
+    dbig = seb.dev_keys(big, n=nbig, stride=16)
+    res = []
+    for order in (0, 1):
+        with seb.option("multiget_order", order):
+            out = torch.zeros(nbig, dtype=torch.int64, device="cuda")
+            reg.multiget_dev(dbig, out)
+            torch.cuda.synchronize()
+            res.append(out.cpu().numpy())
+    assert np.array_equal(res[0], res[1])
     reg.close()
 
 
