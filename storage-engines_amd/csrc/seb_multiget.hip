@@ -86,6 +86,11 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         __syncthreads();
     }
     const RegSlot *slots = kLds ? lslots : gslots;
+    // list rows of <= 16 slots are built in registers and stored as the widest aligned words (one
+    // u32 store per 2 slots instead of a u16 store per slot: 1.189 -> 1.120 ms on 244 files)
+    const uint32_t rowpack = !kList || cap > 16 ? 0u
+                             : (cap % 4 == 0 && ((uintptr_t)cand & 7) == 0) ? 8u
+                             : (cap % 2 == 0 && ((uintptr_t)cand & 3) == 0) ? 4u : 2u;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < kb.n; j += stride) {
         // key-range order (multiget_order): answer index oi = order[j]; the keys are read through the
@@ -108,9 +113,22 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         uint64_t mask = 0;
         uint16_t *row = kList ? cand + oi * (uint64_t)cap : nullptr;
         uint32_t nc = 0;
+        uint64_t rw[4] = {~0ull, ~0ull, ~0ull, ~0ull};  // a row of <= 16 slots in registers (0xFFFF = none)
         auto record = [&](const RegSlot &sl) {  // in Get's visiting order
             if constexpr (kList) {
-                if (nc < cap) row[nc++] = (uint16_t)sl.slot;  // the host checks cap >= the walk's length
+                if (nc < cap) {  // the host checks cap >= the walk's length
+                    if (rowpack) {
+#pragma unroll
+                        for (uint32_t q = 0; q < 4; ++q)
+                            if (q == (nc >> 2)) {
+                                const uint32_t sh = (nc & 3) * 16;
+                                rw[q] = (rw[q] & ~(0xFFFFull << sh)) | ((uint64_t)sl.slot << sh);
+                            }
+                    } else {
+                        row[nc] = (uint16_t)sl.slot;
+                    }
+                    ++nc;
+                }
             } else {
                 mask |= 1ull << sl.slot;
             }
@@ -149,7 +167,21 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
             if (hit >= 0) take(slots[hit]);
         }
         if constexpr (kList) {
-            for (uint32_t t = nc; t < cap; ++t) row[t] = 0xFFFFu;
+            if (rowpack == 8) {  // the row as whole words: cap % 4 == 0 / cap % 2 == 0, aligned
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q)
+                    if (4 * q < cap) ((uint64_t *)row)[q] = rw[q];
+            } else if (rowpack == 4) {
+#pragma unroll
+                for (uint32_t q = 0; q < 8; ++q)
+                    if (2 * q < cap) ((uint32_t *)row)[q] = (uint32_t)(rw[q >> 1] >> ((q & 1) * 32));
+            } else if (rowpack == 2) {
+#pragma unroll
+                for (uint32_t q = 0; q < 16; ++q)
+                    if (q < cap) row[q] = (uint16_t)(rw[q >> 2] >> ((q & 3) * 16));
+            } else {
+                for (uint32_t t = nc; t < cap; ++t) row[t] = 0xFFFFu;
+            }
         } else {
             maybe[oi] = mask;
         }

@@ -1163,6 +1163,17 @@ def test_registry_multiget_list_beyond_64_files(seb, torch_cuda):
     reg.multiget_list_dev(dk, out, 6)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint16), _walk_rows(files, fixed, 6))
+    # rows of <= 16 slots are stored as u64 / u32 / u16 words by cap and alignment, wider rows
+    # slot by slot: every cap and a 2-B-aligned output give the same rows
+    want_rows = {cap: _walk_rows(files, fixed, cap) for cap in (6, 7, 8, 12, 16, 17, 20)}
+    for cap, want_c in want_rows.items():
+        for shift in (0, 1):
+            flat = torch.full((len(fixed) * cap + 1,), 7, dtype=torch.int16, device="cuda")
+            view = flat[shift:shift + len(fixed) * cap].view(len(fixed), cap)
+            reg.multiget_list_dev(dk, view, cap)
+            torch.cuda.synchronize()
+            assert np.array_equal(view.cpu().numpy().view(np.uint16), want_c), (cap, shift)
+            assert int(flat[len(fixed) * cap if shift == 0 else 0].item()) == 7  # nothing written past the rows
     # L2 compacted away: 30 files (LDS slot table), but L3 keeps slots 113..119, beyond a u64 mask
     for f in [f for f in files if f["level"] == 2]:
         reg.remove(f["file"])
