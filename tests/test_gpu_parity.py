@@ -1312,6 +1312,50 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
     reg.close()
 
 
+def test_registry_key_range_order_wide_partition_level(seb, torch_cuda):
+    """Key-range order over a partition level of 1020 files (1021 buckets, near kMgMaxBuckets =
+    1025: the block scans run 4 buckets per thread), with an L1 of 60 files over it and two L0
+    files, on a 300K-key batch with keys below, between and above the files: the list rows equal
+    the batch-order walk's and, on a sample, the Python model of LSM.Get's walk."""
+    torch = torch_cuda
+    rng = np.random.default_rng(61)
+    reg = seb.Registry(0)
+    files = []
+
+    def add(file_num, level, keys):
+        m, k = oc.params(max(len(keys), 1), 0.01)
+        arr = np.frombuffer(b"".join(keys), np.uint8)
+        bits = oc.build(m, k, arr, len(keys), stride=16)
+        slot = reg.put(file_num, level, bn.encode(bits, m, k), min(keys), max(keys))
+        files.append(dict(file=file_num, level=level, min=min(keys), max=max(keys), bits=bits, m=m, k=k,
+                          seq=len(files), slot=slot))
+
+    universe = [kg.key16_bytes(int(i)) for i in range(10_000, 10_000 + 2 * 40_800, 2)]  # sorted
+    for f in range(2):
+        add(10 + f, 0, sorted(rng.choice(universe, 500, replace=False).tolist()))
+    for lvl, parts in ((1, 60), (2, 1020)):
+        chunks = np.array_split(np.array(universe, dtype=object), parts)
+        for j in rng.permutation(parts):
+            add(1000 * lvl + int(j), lvl, list(chunks[j])[::2])
+    assert reg.max_candidates() == 4
+    n = 300_000
+    pk = kg.key16(rng.integers(0, 100_000, n))
+    probes = pk.reshape(n, 16)
+    with seb.option("multiget_order", 0):
+        want = reg.multiget_list(probes)
+    with seb.option("multiget_order", 1):
+        got = reg.multiget_list(probes)
+        dk = seb.dev_keys(to_dev(torch, pk), n=n, stride=16)
+        out = torch.zeros((n, 4), dtype=torch.int16, device="cuda")
+        reg.multiget_list_dev(dk, out, 4)
+        torch.cuda.synchronize()
+    assert np.array_equal(got, want)
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    sample = list(range(0, n, 499))
+    assert np.array_equal(want[sample], _walk_rows(files, [probes[i].tobytes() for i in sample], 4))
+    reg.close()
+
+
 def test_registry_key_range_order_long_min_keys(seb, torch_cuda):
     """Key-range order over a partition level whose MinKeys are longer than 16 bytes and share
     their first 16 bytes: the bucket pass must break the tie with the HBM tail compare.  Probes
