@@ -988,15 +988,18 @@ def main():
         print(json.dumps(result), flush=True)
 
 
-SECONDARY = (("lsm", ["--steps", "10", "--warmup", "3"]), ("lsm_wide", ["--steps", "10", "--warmup", "3"]),
+SECONDARY = (("c4", ["--steps", "10", "--warmup", "3", "--no-cpu-baseline"]),
+             ("c5", ["--steps", "10", "--warmup", "3"]),
+             ("lsm", ["--steps", "10", "--warmup", "3"]), ("lsm_wide", ["--steps", "10", "--warmup", "3"]),
              ("flush", []))
 
 
 def secondary_lines():
-    """The other SURVEY 8 rows on the default (driver-run) line, each from its own child process
-    (`bench.py --config X`, the same code path as run alone) after the headline's timed region:
-    the registry MultiGet (f1/f2, 28 and 244 files) and the drop-in ABI at flush/compaction size
-    (b).  A compact summary of each child's JSON line; a failure is recorded, never fatal."""
+    """The other BASELINE configs and SURVEY 8 rows on the default (driver-run) line, each from
+    its own child process (`bench.py --config X`, the same code path as run alone) after the
+    headline's timed region: C4 (variable-length keys), C5 (64 filters, one GPU), the registry
+    MultiGet (f1/f2, 28 and 244 files) and the drop-in ABI at flush/compaction size (b).  A
+    compact summary of each child's JSON line; a failure is recorded, never fatal."""
     out = []
     for cfg, extra in SECONDARY:
         cmd = [sys.executable, os.path.abspath(__file__), "--config", cfg, "--no-secondary", *extra]
@@ -1007,7 +1010,9 @@ def secondary_lines():
             out.append({"config": cfg, "error": f"{type(e).__name__}: {str(e)[:200]}"})
             continue
         item = {"config": cfg, "workload": line.get("config", {}).get("workload"),
-                "metric": line.get("metric") if cfg == "flush" else "registry MultiGet Mkeys/s (10M keys)",
+                "metric": {"flush": line.get("metric"), "c4": "C4 build+probe Mkeys/s (10M variable-length keys)",
+                           "c5": "C5 probe Mkeys/s (10M keys x 64 filters)"}.get(
+                               cfg, "registry MultiGet Mkeys/s (10M keys)"),
                 "value": line.get("value"), "unit": line.get("unit"),
                 "ms_per_step": line.get("ms_per_step"), "parity": line.get("parity")}
         gm = line.get("roofline", {}).get("gather_model")
