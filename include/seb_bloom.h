@@ -81,6 +81,8 @@ int seb_abi_version(void);
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
  *   "multiget_order"  registry MultiGet walks batches of >= 64K keys in key-range order (1, default)
  *                     or batch order (0)
+ *   "multiget_l0_group" registry MultiGet tests the L0 files that share (m, k) through one
+ *                     bit-interleaved table, one gather per position for all of them (1, default)
  *   "varlen_prehash_min_keys"  variable-length batches of this many keys are pre-hashed in LDS
  *   "grid_cap"        maximum workgroups of the grid-stride kernels
  *   "workspace_limit_mib"  cap on library scratch (0 = none); a request above it fails with

@@ -130,6 +130,7 @@ static const OptionDesc kOptions[] = {
     SEB_OPT(build_algo, 0, 4),
     SEB_OPT(multi_interleave, 0, 1),
     SEB_OPT(multiget_order, 0, 1),
+    SEB_OPT(multiget_l0_group, 0, 1),
     SEB_OPT(varlen_prehash_min_keys, 0, INT64_MAX),
     SEB_OPT(bucket_min_keys, 0, INT64_MAX),
     SEB_OPT(lds_min_keys, 0, INT64_MAX),
@@ -1556,6 +1557,7 @@ struct seb_registry {
     uint64_t seq = 0;
     bool dirty = true;
     DevBuf dslots, dranges;
+    DevBuf dl0;                    // the L0 group's interleaved table (RegLayout::l0tab)
     uint32_t nslots = 0;
     uint32_t max_cand = 0;         // longest Get walk: every L0 file + one file per non-empty level 1..4
     uint32_t max_slot = 0;         // 1 + the largest slot id in use (the mask form needs <= 64)
@@ -1588,6 +1590,7 @@ extern "C" void seb_registry_free(seb_registry *r) {
     for (auto &e : r->entries) (void)hipFree(e.dwords);
     r->dslots.release();
     r->dranges.release();
+    r->dl0.release();
     if (r->ctx) seb_ctx_destroy(r->ctx);
     delete r;
 }
@@ -1698,15 +1701,43 @@ static int sync_registry_locked(seb_registry *r) {
         ranges += e->max_key;
         s.level = e->level;
         s.slot = e->slot;
+        s.gbit = -1;
         be_prefix(e->min_key, s.min_be);
         be_prefix(e->max_key, s.max_be);
         slots.push_back(s);
     }
+    // L0 group: the largest set of L0 files sharing (m, k) (flushes of equal-sized memtables do;
+    // MaxL0Files = 4, lsm/levels.go:9), at most kL0GroupMax, tested through one interleaved table
+    std::vector<uint32_t> grp;
+    for (uint32_t i = lay.lo[0]; i < lay.hi[0]; ++i) {
+        std::vector<uint32_t> same;
+        for (uint32_t j = lay.lo[0]; j < lay.hi[0] && same.size() < kL0GroupMax; ++j)
+            if (order[j]->m == order[i]->m && order[j]->k == order[i]->k) same.push_back(j);
+        if (same.size() > grp.size()) grp = same;
+    }
+    if (grp.size() < 2) grp.clear();
+    uint32_t gbits = 2;
+    while (gbits < grp.size()) gbits *= 2;
     int rc;
     if ((rc = r->dslots.reserve(sizeof(RegSlot) * (slots.size() + 1))) ||
-        (rc = r->dranges.reserve(ranges.size() + 16)))
+        (rc = r->dranges.reserve(ranges.size() + 16)) ||
+        (!grp.empty() && (rc = r->dl0.reserve(4 * l0_table_words(order[grp[0]]->m, gbits) + 16))))
         return rc;
     HIP_OR_FAIL(hipDeviceSynchronize());  // previous multigets may still read the tables
+    lay.l0g = 0;
+    if (!grp.empty()) {
+        L0Members mem{};
+        for (uint32_t f = 0; f < grp.size(); ++f) {
+            mem.w[f] = order[grp[f]]->dwords;
+            slots[grp[f]].gbit = (int32_t)f;
+        }
+        const RegEntry *g0 = order[grp[0]];
+        HIP_OR_FAIL(launch_l0_table(mem, (uint32_t)grp.size(), gbits, g0->m, (uint32_t *)r->dl0.p, nullptr));
+        lay.l0tab = (const uint32_t *)r->dl0.p;
+        lay.l0md = mod_arg(g0->m, g0->k);
+        lay.l0g = (uint32_t)grp.size();
+        lay.l0b = gbits;
+    }
     if (!slots.empty()) HIP_OR_FAIL(hipMemcpy(r->dslots.p, slots.data(), sizeof(RegSlot) * slots.size(), hipMemcpyHostToDevice));
     if (!ranges.empty()) HIP_OR_FAIL(hipMemcpy(r->dranges.p, ranges.data(), ranges.size(), hipMemcpyHostToDevice));
     r->nslots = (uint32_t)slots.size();
@@ -1739,6 +1770,13 @@ extern "C" int seb_registry_slots(seb_registry *r, uint64_t *file_nums, int32_t 
             if (levels) levels[e.slot] = e.level;
         }
     return (int)r->entries.size();
+}
+
+// The layout a MultiGet launches with: the L0 group table only while multiget_l0_group is on.
+static RegLayout mg_layout(const seb_registry *r) {
+    RegLayout l = r->layout;
+    if (!options().multiget_l0_group) l.l0g = 0;
+    return l;
 }
 
 // multiget_order: the batch's key-range order over the registry's partition level, in the
@@ -1792,7 +1830,7 @@ static int registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t
     uint32_t *order = nullptr;
     bool order_keys = true;
     if ((rc = multiget_order(r, kb, (hipStream_t)stream, &order, &order_keys))) return rc;
-    HIP_OR_FAIL(launch_multiget(kb, (const RegSlot *)r->dslots.p, r->nslots, r->layout, (const uint8_t *)r->dranges.p,
+    HIP_OR_FAIL(launch_multiget(kb, (const RegSlot *)r->dslots.p, r->nslots, mg_layout(r), (const uint8_t *)r->dranges.p,
                                 maybe, cand, cap, (hipStream_t)stream,
                                 order, order_keys));
     return SEB_OK;
@@ -1832,7 +1870,7 @@ static int registry_multiget_host_locked(seb_registry *r, const seb_keys *kb, ui
         uint32_t *order = nullptr;
         bool order_keys = true;
         if ((rc = multiget_order(r, dk, c->s_comp, &order, &order_keys))) return rc;
-        HIP_OR_FAIL(launch_multiget(dk, (const RegSlot *)r->dslots.p, r->nslots, r->layout,
+        HIP_OR_FAIL(launch_multiget(dk, (const RegSlot *)r->dslots.p, r->nslots, mg_layout(r),
                                     (const uint8_t *)r->dranges.p, maybe ? (uint64_t *)c->out[b].p : nullptr,
                                     maybe ? nullptr : (uint16_t *)c->out[b].p, cap, c->s_comp, order, order_keys));
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));

@@ -57,6 +57,8 @@ struct RegSlot {
     uint32_t min_off, min_len, max_off, max_len;  // key range bytes in the registry's range buffer
     int32_t level;
     uint32_t slot;          // bit of the output mask
+    int32_t gbit;           // L0 group member: its bit in the group table's entries, else -1
+    uint32_t pad;
     uint64_t min_be[2];     // first 16 bytes of MinKey / MaxKey as big-endian words (zero padded)
     uint64_t max_be[2];
 };
@@ -64,7 +66,20 @@ struct RegLayout {          // slot index ranges per level (lookup order) + shap
     uint32_t lo[5], hi[5];
     uint32_t nonoverlap;    // bit L: level L's files are disjoint and in MinKey order (bisection exact)
     uint32_t all_k7_m32;    // every filter has k == 7 and m < kM32Limit (2^31)
+    // L0 group: the L0 files sharing one (m, k), every key tests all of them, as one bit-interleaved
+    // table (entry p = bit p of each member, l0b bits per entry): one gather per position for the
+    // whole group.  l0g == 0: none.
+    const uint32_t *l0tab;
+    ModArg l0md;
+    uint32_t l0g, l0b;
 };
+constexpr uint32_t kL0GroupMax = 32;
+struct L0Members {          // builder argument: the group's word arrays, in bit order
+    const uint32_t *w[kL0GroupMax];
+};
+uint64_t l0_table_words(uint64_t m, uint32_t bits);
+hipError_t launch_l0_table(const L0Members &mem, uint32_t g, uint32_t bits, uint64_t m, uint32_t *table,
+                           hipStream_t s);
 // seb_codec.hip: shard routing (FNV-1a32) and WAL CRC32
 hipError_t launch_route(const KeyBatch &kb, uint32_t bits, uint16_t *shard, uint32_t *hash, hipStream_t s);
 uint64_t route_workspace_bytes(uint64_t n, uint32_t bits);
@@ -97,7 +112,8 @@ struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed), 3 LDS-resident
                                   // filter (atomic merge), 4 LDS images + OR kernel
     int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
-    int multiget_order = 1;       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
+    int multiget_order = 1;
+    int multiget_l0_group = 1;    // MultiGet: L0 files of one (m, k) tested through one interleaved table       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
     uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys
     uint64_t bucket_min_keys = 100000;  // auto: bucketed build from this many keys on
     uint64_t lds_min_keys = 75000;      // auto: LDS-resident build (filter <= 160 KiB) from this many keys on

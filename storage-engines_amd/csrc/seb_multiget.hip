@@ -69,6 +69,21 @@ __device__ __forceinline__ uint32_t test_filter(const RegSlot &sl, uint64_t h1, 
     return acc & 1u;
 }
 
+// The L0 group (RegLayout::l0tab): every member's MayContain at once.  A position's entry holds
+// its bit of every member, so the walk gathers one word per position and stops once no member
+// is left whose bits so far are all set; each member's answer is the AND of its k bits, as alone.
+template <int KFIX, bool M32>
+__device__ __forceinline__ uint32_t test_l0_group(const RegLayout &lay, uint64_t h1, uint64_t h2) {
+    uint32_t alive = lay.l0g >= 32 ? ~0u : (1u << lay.l0g) - 1u;
+    for_positions<KFIX, M32>(h1, h2, lay.l0md, lay.l0md.k, [&](uint32_t, uint64_t p) {
+        if (alive) {
+            const uint64_t bit = p * lay.l0b;
+            alive &= lay.l0tab[bit >> 5] >> (uint32_t)(bit & 31);
+        }
+    });
+    return alive;
+}
+
 // MODE 0: u64 mask, slot table in LDS.  MODE 1: candidate list, slot table in LDS.  MODE 2:
 // candidate list, slot table read from HBM/L2 (more than kMaxSlots files: an LSM past L1 holds
 // hundreds, lsm/levels.go:10-14 with ~4 MB files, lsm/compaction.go:253).  (Testing filters 4 at a
@@ -136,7 +151,15 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         auto take = [&](const RegSlot &sl) {
             if (test_filter<KFIX, M32>(sl, h1, h2)) record(sl);
         };
-        for (uint32_t s = lay.lo[0]; s < lay.hi[0]; ++s) take(slots[s]);  // every L0 file
+        const uint32_t gm = lay.l0g ? test_l0_group<KFIX, M32>(lay, h1, h2) : 0u;
+        for (uint32_t s = lay.lo[0]; s < lay.hi[0]; ++s) {  // every L0 file, in order
+            const RegSlot &sl = slots[s];
+            if (lay.l0g && sl.gbit >= 0) {
+                if (gm >> sl.gbit & 1u) record(sl);
+            } else {
+                take(sl);
+            }
+        }
         for (uint32_t L = 1; L < 5; ++L) {
             const uint32_t lo = lay.lo[L], hi = lay.hi[L];
             if (lo == hi) continue;
@@ -372,6 +395,35 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *
         for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] += loc[u + 1] - loc[u];
         __syncthreads();
     }
+}
+
+// L0 group table: one thread per output word (32 / bits entries; every member's bits of those
+// positions lie in one of its words).
+__global__ __launch_bounds__(256) void k_l0_table(L0Members mem, uint32_t g, uint32_t bits, uint64_t m,
+                                                  uint64_t nwords, uint32_t *__restrict__ table) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwords) return;
+    const uint32_t per = 32 / bits;
+    const uint64_t p0 = w * per;
+    uint32_t out = 0;
+    if (p0 < m) {
+        const uint32_t sh = (uint32_t)(p0 & 31), lim = m - p0 < per ? (uint32_t)(m - p0) : per;
+        for (uint32_t f = 0; f < g; ++f) {
+            const uint32_t v = mem.w[f][p0 >> 5] >> sh;
+            for (uint32_t e = 0; e < lim; ++e) out |= ((v >> e) & 1u) << (e * bits + f);
+        }
+    }
+    table[w] = out;
+}
+
+uint64_t l0_table_words(uint64_t m, uint32_t bits) { return (m * bits + 31) / 32; }
+
+hipError_t launch_l0_table(const L0Members &mem, uint32_t g, uint32_t bits, uint64_t m, uint32_t *table,
+                           hipStream_t s) {
+    if (g < 2 || g > kL0GroupMax || bits < g || 32 % bits != 0 || m == 0) return hipErrorInvalidValue;
+    const uint64_t nw = l0_table_words(m, bits);
+    hipLaunchKernelGGL(k_l0_table, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, mem, g, bits, m, nw, table);
+    return hipGetLastError();
 }
 
 bool multiget_order_moves(const KeyBatch &kb) {

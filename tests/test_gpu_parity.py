@@ -1312,6 +1312,65 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
     reg.close()
 
 
+def test_registry_l0_group_table(seb, torch_cuda):
+    """The L0 files sharing (m, k) are tested through one bit-interleaved table (multiget_l0_group):
+    every answer, mask and list form, equals the per-file walk (option off) and the Python model of
+    LSM.Get's walk, with a differently sized L0 file between the members (visiting order kept), as
+    members are removed (group of 3 -> 2 -> none), for 5 members (8-bit entries) and for k != 7."""
+    rng = np.random.default_rng(67)
+
+    def run(layout_l0, p=0.01, probes_n=20_000):
+        reg = seb.Registry(0)
+        files = []
+        universe = [kg.key16_bytes(int(i)) for i in range(0, 60_000, 2)]
+
+        def add(file_num, level, keys, fpr):
+            m, k = oc.params(max(len(keys), 1), fpr)
+            arr = np.frombuffer(b"".join(keys), np.uint8)
+            bits = oc.build(m, k, arr, len(keys), stride=16)
+            slot = reg.put(file_num, level, bn.encode(bits, m, k), min(keys), max(keys))
+            files.append(dict(file=file_num, level=level, min=min(keys), max=max(keys), bits=bits, m=m, k=k,
+                              seq=len(files), slot=slot))
+
+        for f, nkeys in enumerate(layout_l0):
+            add(10 + f, 0, sorted(rng.choice(universe, nkeys, replace=False).tolist()), p)
+        chunks = np.array_split(np.array(universe, dtype=object), 10)
+        for j in rng.permutation(10):
+            add(1000 + int(j), 1, list(chunks[j])[::3], 0.01)
+        idx = rng.integers(0, 64_000, probes_n)
+        probes = kg.key16(idx)
+        return reg, files, probes
+
+    def check(reg, files, probes):
+        cap = reg.max_candidates()
+        res = {}
+        for grp in (1, 0):
+            with seb.option("multiget_l0_group", grp):
+                res[grp] = (reg.multiget_list(probes, cap=cap),
+                            reg.multiget(probes) if max(f["slot"] for f in files) < 64 else None)
+        assert np.array_equal(res[1][0], res[0][0])
+        if res[1][1] is not None:
+            assert np.array_equal(res[1][1], res[0][1])
+        sample = list(range(0, len(probes), 97))
+        assert np.array_equal(res[1][0][sample], _walk_rows(files, [probes[i].tobytes() for i in sample], cap))
+        return res[1][0]
+
+    # A, B, D (other size), C: group {A, B, C} with 4-bit entries, D tested alone between B and C
+    reg, files, probes = run([2000, 2000, 1500, 2000])
+    rows = check(reg, files, probes)
+    assert all((rows == f["slot"]).any() for f in files if f["level"] == 0)  # each L0 file answers "maybe"
+    for fn in (11, 10):  # group of 2 (2-bit entries), then none (C alone shares no shape)
+        reg.remove(fn)
+        files[:] = [f for f in files if f["file"] != fn]
+        check(reg, files, probes)
+    reg.close()
+    # five members: 8-bit entries; and a k = 4 group (p = 0.1: the generic-k position walk)
+    for layout, p in (([1000] * 5, 0.01), ([3000, 3000, 3000], 0.1)):
+        reg, files, probes = run(layout, p)
+        check(reg, files, probes)
+        reg.close()
+
+
 def test_registry_key_range_order_wide_partition_level(seb, torch_cuda):
     """Key-range order over a partition level of 1020 files (1021 buckets, near kMgMaxBuckets =
     1025: the block scans run 4 buckets per thread), with an L1 of 60 files over it and two L0
