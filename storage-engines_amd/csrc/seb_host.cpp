@@ -1733,6 +1733,7 @@ static int sync_registry_locked(seb_registry *r) {
         }
         const RegEntry *g0 = order[grp[0]];
         HIP_OR_FAIL(launch_l0_table(mem, (uint32_t)grp.size(), gbits, g0->m, (uint32_t *)r->dl0.p, nullptr));
+        HIP_OR_FAIL(hipStreamSynchronize(nullptr));  // MultiGets run on other (non-blocking) streams
         lay.l0tab = (const uint32_t *)r->dl0.p;
         lay.l0md = mod_arg(g0->m, g0->k);
         lay.l0g = (uint32_t)grp.size();
