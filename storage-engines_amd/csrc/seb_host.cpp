@@ -228,6 +228,7 @@ struct WsEntry {
 struct WsSlot {
     int device;
     hipStream_t stream;
+    bool dead = false;  // its stream was destroyed (ws_drop_stream); reusable for a new one
     std::recursive_mutex mu;  // held by the call enqueueing against this slot's buffers
     std::vector<WsEntry> bufs;
 };
@@ -254,7 +255,14 @@ struct WsCall {
 static WsSlot *ws_slot(int dev, hipStream_t s) {
     std::lock_guard<std::mutex> g(g_ws_mu);
     for (auto &sl : g_ws)
-        if (sl->device == dev && sl->stream == s) return sl.get();
+        if (!sl->dead && sl->device == dev && sl->stream == s) return sl.get();
+    for (auto &sl : g_ws)
+        if (sl->dead) {  // buffers already freed; nobody holds a dead slot's lock
+            sl->dead = false;
+            sl->device = dev;
+            sl->stream = s;
+            return sl.get();
+        }
     g_ws.emplace_back(new WsSlot());
     g_ws.back()->device = dev;
     g_ws.back()->stream = s;
@@ -305,6 +313,27 @@ static int cached_workspace(hipStream_t s, uint64_t bytes, void **out, int tag =
     sl->bufs.push_back({tag, p, bytes});
     *out = p;
     return SEB_OK;
+}
+
+// A stream about to be destroyed (a context's) gives its scratch back first: otherwise its slot
+// would keep a dead handle that a later seb_workspace_release would synchronise on.
+static void ws_drop_stream(int dev, hipStream_t s) {
+    WsSlot *sl = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_ws_mu);
+        for (auto &x : g_ws)
+            if (!x->dead && x->device == dev && x->stream == s) sl = x.get();
+    }
+    if (!sl) return;
+    std::lock_guard<std::recursive_mutex> g2(sl->mu);  // a call still enqueueing on it finishes first
+    if (!sl->bufs.empty()) {
+        (void)hipStreamSynchronize(s);
+        for (auto &b : sl->bufs) (void)hipFree(b.p);
+        sl->bufs.clear();
+    }
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    sl->dead = true;
 }
 
 // Slots are never deleted, so the pointers stay valid after g_ws_mu is dropped (a call holding a
@@ -859,6 +888,8 @@ extern "C" void seb_ctx_destroy(seb_ctx *c) {
     c->ws.release();
     c->hkeys.release();
     c->hbits.release();
+    for (hipStream_t st : {c->s_h2d, c->s_comp, c->s_d2h})
+        if (st) ws_drop_stream(c->device, st);
     if (c->s_h2d) (void)hipStreamDestroy(c->s_h2d);
     if (c->s_comp) (void)hipStreamDestroy(c->s_comp);
     if (c->s_d2h) (void)hipStreamDestroy(c->s_d2h);

@@ -1512,6 +1512,36 @@ def test_shared_stream_threads_and_workspace_release(seb, golden, torch_cuda):
     assert np.array_equal(out.cpu().numpy(), want[1])
 
 
+def test_workspace_release_after_context_streams_destroyed(seb, torch_cuda):
+    """A context's (and a registry's) streams hold library scratch while they live: destroying the
+    context gives it back, so a later seb_workspace_release never synchronises a dead stream."""
+    m, k = seb.params(10_000_000, 0.01)  # phased probe: packed scratch on the context's stream
+    keys = kg.key16(np.arange(200_000)).reshape(-1)
+    q = kg.key16(kg.probe_indices(200_000, count=300_000)).reshape(-1)
+    bits = oc.build(m, k, keys, 200_000, stride=16)
+    want = oc.probe(bits, m, k, q, 300_000, stride=16)
+    seb.workspace_release()
+    for _ in range(3):
+        ctx = seb.Ctx(0)
+        assert np.array_equal(ctx.probe(seb.HostKeys(q.reshape(-1, 16)), bits, m, k), want)
+        assert seb.workspace_bytes() > 0
+        ctx.close()
+        assert seb.workspace_bytes() == 0
+        seb.workspace_release()
+    reg = seb.Registry(0)
+    for f in range(3):
+        fk = [kg.key16_bytes(int(i)) for i in range(f * 1000, f * 1000 + 1000)]
+        fm, fkk = oc.params(len(fk), 0.01)
+        fb = oc.build(fm, fkk, np.frombuffer(b"".join(fk), np.uint8), len(fk), stride=16)
+        reg.put(10 + f, 0, bn.encode(fb, fm, fkk), min(fk), max(fk))
+    probes = [kg.key16_bytes(int(i)) for i in range(0, 6000, 3)]
+    got = reg.multiget(probes)
+    reg.close()
+    seb.workspace_release()
+    assert seb.workspace_bytes() == 0
+    assert got.shape == (len(probes),)
+
+
 def test_registry_full_capacity(seb, torch_cuda):
     """4096 files (the u16 slot-id capacity): one L0 file and 4095 one-key L1 files.  The
     4097th put is refused; the list form still answers every key as Get's walk does, and a key
