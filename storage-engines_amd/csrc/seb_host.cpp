@@ -136,6 +136,7 @@ static const OptionDesc kOptions[] = {
     SEB_OPT(lds_min_keys, 0, INT64_MAX),
     SEB_OPT(many_splits, 0, 64),
     SEB_OPT(probe_phases, 0, 64),
+    SEB_OPT(probe_compact, 0, 1),
     SEB_OPT(grid_cap, 1, 1 << 30),
     SEB_OPT(workspace_limit_mib, 0, 1 << 30),
 };
@@ -482,6 +483,12 @@ static int probe_dispatch(KeyBatch kb, const uint32_t *words, const ModArg &md, 
         return SEB_OK;
     }
     if ((rc = prepare_probe_keys(kb, s, 0, &ws))) return rc;
+    if (want_phased(kb.n, md, out) && options().probe_compact) {  // compacted rows in their own scratch (tag 1)
+        void *rows;
+        if ((rc = cached_workspace(s, probe_compact_bytes(kb.n), &rows, 1))) return rc;
+        HIP_OR_FAIL(launch_probe_compact(kb, words, md, out, rows, s));
+        return SEB_OK;
+    }
     if (want_phased(kb.n, md, out)) {  // packed residues in their own scratch (tag 1)
         void *packed;
         if ((rc = cached_workspace(s, kb.n * 8, &packed, 1))) return rc;

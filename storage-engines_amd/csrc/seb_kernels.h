@@ -112,8 +112,9 @@ struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed), 3 LDS-resident
                                   // filter (atomic merge), 4 LDS images + OR kernel
     int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
-    int multiget_order = 1;
-    int multiget_l0_group = 1;    // MultiGet: L0 files of one (m, k) tested through one interleaved table       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
+    int multiget_order = 1;       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
+    int multiget_l0_group = 1;    // MultiGet: L0 files of one (m, k) tested through one interleaved table
+    int probe_compact = 1;        // phased probe from keys: later phases read only the live keys' words
     uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys
     uint64_t bucket_min_keys = 100000;  // auto: bucketed build from this many keys on
     uint64_t lds_min_keys = 75000;      // auto: LDS-resident build (filter <= 160 KiB) from this many keys on
@@ -176,6 +177,11 @@ uint64_t probe_phase_count(uint64_t m);
 // kb == nullptr: probe the packed words themselves (no phase 0 hashing).
 hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out,
                                uint64_t *packed, hipStream_t s);
+// The phased probe from keys with compacted later phases (probe_compact_bytes of 16-B aligned
+// scratch in `ws`; needs probe_phase_count(m) >= 2).
+uint64_t probe_compact_bytes(uint64_t n);
+hipError_t launch_probe_compact(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, void *ws,
+                                hipStream_t s);
 // Probe from keys that also writes the batch's packed residues.
 hipError_t launch_probe_emit(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out,
                              uint64_t *packed, hipStream_t s);

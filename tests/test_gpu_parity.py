@@ -288,9 +288,10 @@ def test_c2_c3_10m_device_resident(seb, golden, torch_cuda, build_algo):
 
 
 def test_probe_paths_and_phase_counts(seb, golden, torch_cuda):
-    """The phased probe at any number of filter ranges, the sliced probe (one range, or an answer
-    array that is not 4-byte aligned), give the C3 answers bit for bit, also for a ragged batch
-    whose last workgroup is partly empty."""
+    """The phased probe at any number of filter ranges (compacted later phases, or every key's
+    word and answer through every phase), the sliced probe (one range, or an answer array that is
+    not 4-byte aligned), give the C3 answers bit for bit, also for a ragged batch whose last
+    workgroup (and group of 64 keys) is partly empty."""
     torch = torch_cuda
     row = next(r for r in golden["fixed16"] if r["n"] == 10_000_000)
     n, m, k = row["n"], row["m"], row["k"]
@@ -299,17 +300,18 @@ def test_probe_paths_and_phase_counts(seb, golden, torch_cuda):
     pk = to_dev(torch, kg.key16(kg.probe_indices(n)))
     ragged = 999_983
     ref_ragged = oc.probe(bits, m, k, kg.key16(kg.probe_indices(n)[:ragged]), ragged, stride=16)
-    for phases, shift in ((0, 0), (2, 0), (4, 0), (7, 0), (1, 0), (0, 1)):
-        with seb.option("probe_phases", phases):
+    for phases, shift, compact in ((0, 0, 1), (0, 0, 0), (2, 0, 1), (2, 0, 0), (4, 0, 1), (7, 0, 1), (7, 0, 0),
+                                   (1, 0, 1), (0, 1, 1)):
+        with seb.option("probe_phases", phases), seb.option("probe_compact", compact):
             buf = torch.full((n + 4,), 7, dtype=torch.uint8, device="cuda")
             seb.dev_probe(seb.dev_keys(pk, n=n, stride=16), words, m, k, buf[shift:shift + n])
             torch.cuda.synchronize()
-            assert sha(buf[shift:shift + n].cpu().numpy().tobytes()) == row["probe_sha256"], (phases, shift)
+            assert sha(buf[shift:shift + n].cpu().numpy().tobytes()) == row["probe_sha256"], (phases, shift, compact)
             outr = torch.full((ragged + 2,), 7, dtype=torch.uint8, device="cuda")
             seb.dev_probe(seb.dev_keys(pk[:ragged], n=ragged, stride=16), words, m, k, outr[shift:shift + ragged])
             torch.cuda.synchronize()
             got = outr.cpu().numpy()
-            assert np.array_equal(got[shift:shift + ragged], ref_ragged), (phases, shift)
+            assert np.array_equal(got[shift:shift + ragged], ref_ragged), (phases, shift, compact)
             assert got[shift + ragged] == 7, (phases, shift)  # nothing written past the batch
 
 

@@ -15,7 +15,8 @@ FETCH_SIZE counts exactly half the bytes of a wide (16 B/lane) coalesced streami
 where `wide` is every 16-B-per-lane stream of the step (WIDE_STREAMS): the key batch (dwordx4 per
 lane; for variable-length keys the pre-hash's 16-B span copy), the bucketed build's u16 position
 runs read back by k_bkt_apply (uint4 loads, 2 B per position), and the packed residues (8 B per
-key) the later probe phases read as u32x4.  The random 4-byte gathers of the probe are one 64-B
+key) the later phases of the uncompacted phased probe read as u32x4 (the compacted phases,
+k_probe_cp, read 8 B per lane: not corrected).  The random 4-byte gathers of the probe are one 64-B
 EA request each (TCC_EA0_RDREQ), which FETCH_SIZE counts at 64 B; they need no correction.
 """
 from __future__ import annotations
@@ -102,6 +103,8 @@ def main():
             elif c == "WRITE_SIZE":
                 write += v
         wide = WIDE_STREAMS.get(a.config, {}).get(step, a.key_bytes)
+        if any("k_probe_c0" in k for k in kernels) and a.config in WIDE_STREAMS:
+            wide -= 2 * 8 * N  # compacted phases read their rows 8 B per lane: no wide packed stream
         read = fetch * 1024 + wide / 2
         steps[step] = {"hbm_bytes_per_launch": int(read + write * 1024), "read_bytes": int(read),
                        "write_bytes": int(write * 1024), "fetch_size_kib": fetch, "write_size_kib": write,
