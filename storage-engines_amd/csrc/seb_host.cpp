@@ -222,7 +222,7 @@ extern "C" int seb_dev_clear(uint32_t *words, uint64_t m, void *stream) {
 // on the same stream therefore enqueues after the first call's launches, and a grow (stream sync
 // + free) can never free a buffer that another thread has been handed but not yet launched on.
 struct WsEntry {
-    int tag;  // 0: build / key preparation; 1: packed residues; 3: MultiGet key-range order
+    int tag;  // 0: build / key preparation; 1: packed residues; 2: compacted probe rows; 3: MultiGet key-range order
     void *p;
     uint64_t bytes;
 };
@@ -479,7 +479,13 @@ static int probe_dispatch(KeyBatch kb, const uint32_t *words, const ModArg &md, 
         void *packed;
         if ((rc = cached_workspace(s, kb.n * 8, &packed, 1))) return rc;
         HIP_OR_FAIL(launch_hash_varlen_packed(kb, md, (uint64_t *)packed, s));
-        HIP_OR_FAIL(launch_probe_phased(nullptr, kb.n, words, md, out, (uint64_t *)packed, s));
+        if (options().probe_compact) {  // compacted rows (tag 2) from the packed words
+            void *rows;
+            if ((rc = cached_workspace(s, probe_compact_bytes(kb.n), &rows, 2))) return rc;
+            HIP_OR_FAIL(launch_probe_compact_packed((const uint64_t *)packed, kb.n, words, md, out, rows, s));
+        } else {
+            HIP_OR_FAIL(launch_probe_phased(nullptr, kb.n, words, md, out, (uint64_t *)packed, s));
+        }
         return SEB_OK;
     }
     if ((rc = prepare_probe_keys(kb, s, 0, &ws))) return rc;
@@ -572,12 +578,17 @@ extern "C" int seb_dev_pack_residues(const seb_keys *keys, uint64_t m, uint32_t 
 
 extern "C" int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, uint64_t m, uint32_t k,
                                     uint8_t *out, void *stream) {
+    WsCall ws_call;
     enter();
     int rc = check_packed_args(m, k, "seb_dev_probe_packed");
     if (rc) return rc;
     if (n && (!packed || !words || !out)) return fail(SEB_ERR_INVALID, "seb_dev_probe_packed: null pointer");
     const ModArg md = mod_arg(m, k);
-    if (want_phased(n, md, out))
+    if (want_phased(n, md, out) && options().probe_compact) {
+        void *rows;
+        if ((rc = cached_workspace((hipStream_t)stream, probe_compact_bytes(n), &rows, 2))) return rc;
+        HIP_OR_FAIL(launch_probe_compact_packed(packed, n, words, md, out, rows, (hipStream_t)stream));
+    } else if (want_phased(n, md, out))
         HIP_OR_FAIL(launch_probe_phased(nullptr, n, words, md, out, const_cast<uint64_t *>(packed), (hipStream_t)stream));
     else
         HIP_OR_FAIL(launch_probe_packed(packed, n, words, md, out, (hipStream_t)stream));

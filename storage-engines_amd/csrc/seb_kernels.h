@@ -182,6 +182,9 @@ hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *w
 uint64_t probe_compact_bytes(uint64_t n);
 hipError_t launch_probe_compact(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, void *ws,
                                 hipStream_t s);
+// The same from a batch of packed residues (the pre-hashed variable-length batch, a broadcast batch).
+hipError_t launch_probe_compact_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
+                                       uint8_t *out, void *ws, hipStream_t s);
 // Probe from keys that also writes the batch's packed residues.
 hipError_t launch_probe_emit(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out,
                              uint64_t *packed, hipStream_t s);

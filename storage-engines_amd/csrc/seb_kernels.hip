@@ -333,19 +333,25 @@ __global__ __launch_bounds__(kPhaseBlock) void k_probe_c0(Src src, uint64_t n, c
     const uint32_t lane = threadIdx.x & 63u;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t i = base + threadIdx.x;  // base is a multiple of 64: a wave is one group
-        uint64_t h1 = 0, h2 = 0;
-        if (i < n) src.hash(i, h1, h2);
         uint32_t pos[7];
-        for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[q] = (uint32_t)p; });
-        uint64_t f = 0, x = h1;
+        uint64_t pw;
+        if constexpr (IsPacked<Src>::value) {  // a batch of packed residues (pre-hashed, or broadcast)
+            const uint4 v = i < n ? src.load(i) : make_uint4(0u, 0u, 0u, 0u);
+            pw = (uint64_t)v.x | (uint64_t)v.y << 32;
+            packed_positions(pw, (uint32_t)md.m, (uint32_t)md.c, pos);
+        } else {
+            uint64_t h1 = 0, h2 = 0;
+            if (i < n) src.hash(i, h1, h2);
+            for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[q] = (uint32_t)p; });
+            uint64_t f = 0, x = h1;
 #pragma unroll
-        for (uint32_t q = 1; q < 7; ++q) {
-            const uint64_t xn = x + h2;
-            f |= (uint64_t)(xn < x) << (q - 1);
-            x = xn;
+            for (uint32_t q = 1; q < 7; ++q) {
+                const uint64_t xn = x + h2;
+                f |= (uint64_t)(xn < x) << (q - 1);
+                x = xn;
+            }
+            pw = (uint64_t)pos[0] | ((uint64_t)mod_m31(h2, (uint32_t)md.m, md.mu) << kPackBits) | (f << (2 * kPackBits));
         }
-        const uint64_t pw = (uint64_t)pos[0] | ((uint64_t)mod_m31(h2, (uint32_t)md.m, md.mu) << kPackBits) |
-                            (f << (2 * kPackBits));
         uint32_t acc = i < n ? 1u : 0u;
 #pragma unroll
         for (int q = 0; q < 7; ++q) {
@@ -1068,9 +1074,9 @@ uint64_t probe_compact_bytes(uint64_t n) {
     return ng * 64 * 8 + ng * 16;
 }
 
-hipError_t launch_probe_compact(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, void *ws,
-                                hipStream_t s) {
-    const uint64_t n = kb.n;
+template <typename Phase0>
+static hipError_t run_probe_compact(uint64_t n, const uint32_t *words, const ModArg &md, uint8_t *out, void *ws,
+                                    hipStream_t s, Phase0 &&phase0) {
     if (n == 0) return hipSuccess;
     const uint64_t nwords = (md.m + 31) / 32;
     const uint64_t np = probe_phase_count(md.m);
@@ -1080,12 +1086,13 @@ hipError_t launch_probe_compact(const KeyBatch &kb, const uint32_t *words, const
     const uint64_t ng = (n + 63) / 64;
     uint64_t *rows = (uint64_t *)ws;
     ulonglong2 *recs = (ulonglong2 *)(rows + ng * 64);
-    hipError_t e = with_src(kb, [&](auto src) {
+    auto launch0 = [&](auto src) {
         using S = decltype(src);
         hipLaunchKernelGGL(k_probe_c0<S>, dim3(grid_for(n, kPhaseBlock, cap)), dim3(kPhaseBlock), 0, s, src, n, words,
                            md, rows, recs, bound(1));
         return hipGetLastError();
-    });
+    };
+    hipError_t e = phase0(launch0);
     if (e != hipSuccess) return e;
     // 4 groups per wave iteration (1, 2 and 8 measured slower)
     constexpr int G = 4;
@@ -1100,6 +1107,16 @@ hipError_t launch_probe_compact(const KeyBatch &kb, const uint32_t *words, const
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t launch_probe_compact(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, void *ws,
+                                hipStream_t s) {
+    return run_probe_compact(kb.n, words, md, out, ws, s, [&](auto &&launch0) { return with_src(kb, launch0); });
+}
+
+hipError_t launch_probe_compact_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
+                                       uint8_t *out, void *ws, hipStream_t s) {
+    return run_probe_compact(n, words, md, out, ws, s, [&](auto &&launch0) { return launch0(KeysPacked{packed}); });
 }
 
 // Phases of the phased probe: probe_phases, or one per 4 MiB of filter (one XCD's L2).

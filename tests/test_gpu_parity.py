@@ -247,6 +247,14 @@ def probe_split(request, seb):
         yield request.param
 
 
+@pytest.fixture(params=[1, 0], ids=["compact", "dense"])
+def probe_compact(request, seb):
+    """Later phases of the phased probe: compacted rows of live keys, or every key's word and
+    answer byte through every phase."""
+    with seb.option("probe_compact", request.param):
+        yield request.param
+
+
 def test_c2_c3_10m_device_resident(seb, golden, torch_cuda, build_algo):
     """BASELINE C2 (build 10M x 16B @1%) and C3 (probe 10M, 50% present), digests + properties,
     for both build algorithms (device-scope atomics and the radix-partitioned LDS build)."""
@@ -371,7 +379,7 @@ def unpack_positions(packed: np.ndarray, m: int) -> np.ndarray:
     return out
 
 
-def test_packed_residues(seb, golden, torch_cuda):
+def test_packed_residues(seb, golden, torch_cuda, probe_compact):
     """Packed residues (the multi-GPU broadcast form): positions equal the oracle's
     (h1 + i*h2 mod 2^64) mod m, and probing them gives the C3 answers bit for bit, for fixed 16-B
     and variable-length batches; unsupported (k, m) are rejected."""
@@ -517,7 +525,7 @@ def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed):
 
 @pytest.mark.parametrize("k", [7, 8])
 @pytest.mark.parametrize("algo", [1, 2])
-def test_varlen_prehash_packed_paths(seb, torch_cuda, k, algo):
+def test_varlen_prehash_packed_paths(seb, torch_cuda, k, algo, probe_compact):
     """Pre-hash to packed residues (k = 7: bucketed build from KeysPacked, phased probe from packed
     words, pack_residues / emit_packed over variable-length keys) against the oracle, and the
     16-B hash path (k = 8); a 2-range filter so the k = 7 probe runs phased."""
