@@ -388,14 +388,14 @@ __global__ __launch_bounds__(kPhaseBlock) void k_probe_cp(const uint64_t *__rest
     for (uint64_t g0 = wave * G; g0 < ng; g0 += step) {
         uint64_t m0[G], lv[G], pv[G];
         uint32_t live[G];
+        // the G records in one wave-uniform load (the record array is padded to a multiple of G)
+        struct Recs { ulonglong2 r[G]; };
+        const Recs rv = *(const Recs *)(recs + g0);
 #pragma unroll
         for (int j = 0; j < G; ++j) {
-            m0[j] = lv[j] = 0;
-            if (g0 + j < ng) {
-                const ulonglong2 r = recs[g0 + j];  // one address for the whole wave
-                m0[j] = uniform64(r.x);
-                lv[j] = uniform64(r.y);
-            }
+            const bool in = g0 + j < ng;
+            m0[j] = in ? uniform64(rv.r[j].x) : 0ull;
+            lv[j] = in ? uniform64(rv.r[j].y) : 0ull;
             live[j] = (uint32_t)(lv[j] >> lane) & 1u;
         }
 #pragma unroll
@@ -1071,7 +1071,7 @@ hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *w
 // 16-B records.
 uint64_t probe_compact_bytes(uint64_t n) {
     const uint64_t ng = (n + 63) / 64;
-    return ng * 64 * 8 + ng * 16;
+    return ng * 64 * 8 + (ng + 8) * 16;  // records padded for k_probe_cp's G-record loads
 }
 
 template <typename Phase0>
