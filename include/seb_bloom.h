@@ -78,6 +78,8 @@ int seb_abi_version(void);
  *   "many_splits"     batched small-filter build: workgroups per filter (0 = auto)
  *   "probe_phases"    k == 7, m < 2^29 probes: filter ranges of the phased probe, one launch each
  *                     (0 = one per 4 MiB of filter; 1 = the single-launch sliced probe)
+ *   "probe_compact"   phased probe: later phases read only the live keys' packed words, kept
+ *                     compacted per 64-key group (1, default), or every key's (0)
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
  *   "multiget_order"  registry MultiGet walks batches of >= 64K keys in key-range order (1, default)
  *                     or batch order (0)
