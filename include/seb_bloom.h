@@ -166,7 +166,9 @@ int seb_timer_destroy(void *event);
  * grow-only buffers kept per (device, stream); a call holds its stream's buffers until it returns,
  * so calls from several threads on one stream are safe (their launches do not interleave).
  * seb_workspace_bytes: bytes currently held; seb_workspace_release: synchronise the streams that
- * own scratch and free all of it (the next call re-allocates). */
+ * own scratch and free all of it (the next call re-allocates).  A phased probe holds ≈8.3 bytes per
+ * key (its compacted packed words and group records); the scratch of a context's (or a registry's)
+ * own streams is freed by seb_ctx_destroy (seb_registry_free). */
 uint64_t seb_workspace_bytes(void);
 int seb_workspace_release(void);
 
