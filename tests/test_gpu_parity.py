@@ -323,6 +323,36 @@ def test_probe_paths_and_phase_counts(seb, golden, torch_cuda):
             assert got[shift + ragged] == 7, (phases, shift)  # nothing written past the batch
 
 
+@pytest.mark.parametrize("phases", [2, 3, 5])
+def test_phased_probe_small_batches(seb, torch_cuda, phases, probe_compact):
+    """Phased probes of batches that leave groups of 64 keys (and a wave's 4 groups) partly empty:
+    1 to 4097 keys, fixed 16-B keys and packed residues, against the oracle; nothing is written
+    past the batch."""
+    torch = torch_cuda
+    n_build = 100_000
+    m, k = oc.params(n_build, 0.01)
+    bkeys = kg.key16(np.arange(n_build))
+    bits = oc.build(m, k, bkeys, n_build, stride=16)
+    words, got_bits = dev_build_bits(seb, torch, seb.dev_keys(to_dev(torch, bkeys), n=n_build, stride=16), m, k)
+    assert np.array_equal(got_bits, bits)
+    with seb.option("probe_phases", phases):
+        for n in (1, 2, 63, 64, 65, 129, 255, 256, 257, 4097):
+            q = kg.key16(kg.probe_indices(n_build, count=n))
+            want = oc.probe(bits, m, k, q, n, stride=16)
+            qd = seb.dev_keys(to_dev(torch, q), n=n, stride=16)
+            out = torch.full((n + 8,), 7, dtype=torch.uint8, device="cuda")
+            seb.dev_probe(qd, words, m, k, out[:n])
+            packed = torch.zeros(n, dtype=torch.int64, device="cuda")
+            seb.dev_pack_residues(qd, m, k, packed)
+            out2 = torch.full((n + 8,), 7, dtype=torch.uint8, device="cuda")
+            seb.dev_probe_packed(packed, n, words, m, k, out2[:n])
+            torch.cuda.synchronize()
+            for o in (out, out2):
+                got = o.cpu().numpy()
+                assert np.array_equal(got[:n], want), (n, phases)
+                assert (got[n:] == 7).all(), (n, phases)
+
+
 def test_multi_packed_matches_multi(seb, golden, torch_cuda):
     """The C5 multi-filter probe over packed residues equals the probe over the keys (golden C5
     digest for 64 filters, u64 masks) and the oracle for 8 filters with a ragged batch; mixed
