@@ -6,7 +6,8 @@
 `--gpus N` with N > 1 and no launcher environment spawns the N rank processes itself
 (launch_ranks: the parent never touches the GPU); under torchrun WORLD_SIZE must equal --gpus.
 
-c2c3 (default, the metric's config): one step on every GPU = clear + build one SSTable filter
+c2c3 (default, the metric's config): one step on every GPU = build a new SSTable filter (its
+words written whole by seb_dev_build_fresh, no separate clear; --fresh-build 0: clear + build)
 from 10M x 16-B keys @1% FPR (BASELINE C2; m = 95,850,584, k = 7) and probe a 10M-key batch
 against it (C3, 50% present).  Rank g builds the filter of its own SSTable (keys key16(g*n + i));
 the probe batch arrives on rank 0 and is RCCL-broadcast to every GPU ahead of the step that
@@ -95,6 +96,9 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true",
                     help="c2c3 at N=1: skip the secondary lines (lsm, lsm_wide, flush) run as child processes")
     ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--fresh-build", type=int, default=1,
+                    help="1: each step builds a new filter with seb_dev_build_fresh (written whole, no clear); "
+                         "0: seb_dev_clear + seb_dev_build")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--lsm-order", default="batch", choices=["batch", "sorted"],
                     help="lsm configs: probe the batch as generated, or key-sorted (a locality experiment; "
@@ -147,7 +151,7 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
     st.wbufs = [seb.new_words(m, device=dev) for _ in range(2 if args.overlap else 1)]
     st.out = torch.empty(n, dtype=torch.uint8, device=dev)
     nb = (m + 7) // 8
-    st.kernel_bytes = {"build": 16.0 * n + 2 * nb, "probe": 16.0 * n + nb + n}
+    st.kernel_bytes = {"build": 16.0 * n + (1 if args.fresh_build else 2) * nb, "probe": 16.0 * n + nb + n}
     st.units_per_step = 2.0 * n * world
     # N > 1: every rank's filter has the same (m, k) (one SSTable size), so the batch travels as
     # 8-byte packed residues instead of 16-byte keys (80 MB over xGMI instead of 160 MB), hashed
@@ -193,8 +197,11 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
 
     def build(j):
         w = st.wbufs[j % len(st.wbufs)]
-        seb.dev_clear(w, m)
-        seb.dev_build(st.kb, w, m, k)
+        if args.fresh_build:  # a new filter: written whole, no clear (seb_dev_build_fresh)
+            seb.dev_build_fresh(st.kb, w, m, k)
+        else:
+            seb.dev_clear(w, m)
+            seb.dev_build(st.kb, w, m, k)
 
     def probe(j, buf, target):
         w = st.wbufs[j % len(st.wbufs)]
@@ -318,7 +325,7 @@ def setup_c4(args, seb, kg, torch, dev, rank, world, dist):
     st.wbufs = [seb.new_words(m, device=dev) for _ in range(2 if args.overlap else 1)]
     st.out = torch.empty(n, dtype=torch.uint8, device=dev)
     nb = (m + 7) // 8
-    st.kernel_bytes = {"build": float(bo[-1]) + 8.0 * (n + 1) + 2 * nb,
+    st.kernel_bytes = {"build": float(bo[-1]) + 8.0 * (n + 1) + (1 if args.fresh_build else 2) * nb,
                        "probe": float(po[-1]) + 8.0 * (n + 1) + nb + n}
     st.units_per_step = 2.0 * n * world
     st.workload = ("C4: per GPU build + probe 10M variable-length keys 8-256 B (zipf s=1.1, mean 39.95 B) @1% FPR "
@@ -327,8 +334,11 @@ def setup_c4(args, seb, kg, torch, dev, rank, world, dist):
 
     def build(j):
         w = st.wbufs[j % len(st.wbufs)]
-        seb.dev_clear(w, m)
-        seb.dev_build(st.kb, w, m, k)
+        if args.fresh_build:
+            seb.dev_build_fresh(st.kb, w, m, k)
+        else:
+            seb.dev_clear(w, m)
+            seb.dev_build(st.kb, w, m, k)
 
     def parity(j):
         if n != 10_000_000 or rank != 0:

@@ -103,6 +103,11 @@ int seb_device_check(int device);
 int seb_dev_clear(uint32_t *words, uint64_t num_bits, void *stream);
 int seb_dev_build(const seb_keys *keys, uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
                   void *stream);
+/* A new filter from `keys` (NewBloomFilter + Add per key): `words` (seb_words_bytes) need not be
+ * cleared; every word is written.  The radix-partitioned build writes them whole instead of
+ * clearing and OR-ing; other build paths clear first. */
+int seb_dev_build_fresh(const seb_keys *keys, uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
+                        void *stream);
 /* Same, with caller-owned scratch (graph-capture friendly: no allocation inside the call).
  * seb_dev_build_workspace_size gives the bytes needed for n keys (0: this build needs none). */
 uint64_t seb_dev_build_workspace_size(uint64_t n, uint64_t num_bits, uint32_t num_hashes);

@@ -61,14 +61,16 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t *w
 // ---- scatter: one workgroup per super-tile of R rounds x kRoundKeys keys.  Each round
 // counting-sorts its positions by bucket in LDS, then appends each bucket run to the
 // fixed-capacity region (bucket b, tile t) in HBM.  A run that would overflow its region (never
-// for hash-distributed keys: cap = mean + 8 sigma + 32) is OR-ed straight into the filter with
-// device-scope atomics instead, which k_bkt_apply's read-modify-write OR preserves.
+// for hash-distributed keys: cap = mean + 8 sigma + 32) is OR-ed with device-scope atomics into
+// `ovw` instead: the filter itself, which k_bkt_apply's read-modify-write OR preserves, or for a
+// fresh build the overflow bitmap that apply folds in.  counts[b][t] is the run's full length, so
+// apply can tell an overflowed bucket (count > cap).
 // LDS: sorted[THREADS*KPT7*7] u32 | cursor[nb] | fill[nb] | wsum[16] | ovf
 template <typename Src, int KFIX, int THREADS, int KPT7>
 __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, ModArg md, uint32_t nb, uint32_t tile_keys,
                                                              uint32_t ntiles, uint32_t cap, uint16_t *__restrict__ regions,
                                                              uint32_t *__restrict__ counts,
-                                                             uint32_t *__restrict__ words) {
+                                                             uint32_t *__restrict__ ovw) {
     extern __shared__ uint32_t smem[];
     constexpr uint32_t kPos = (uint32_t)THREADS * KPT7 * 7;  // positions sorted per round
     uint32_t *sorted = smem;
@@ -213,7 +215,7 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, Mo
                 if (e - (b * ntiles + t) * cap < cap)
                     regions[e] = (uint16_t)p;
                 else
-                    __hip_atomic_fetch_or(words + (p >> 5), 1u << (p & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_or(ovw + (p >> 5), 1u << (p & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();
@@ -224,20 +226,31 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, Mo
         if (threadIdx.x == 0) *ovf = 0u;
         __syncthreads();
     }
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) counts[(uint64_t)b * ntiles + t] = min(fill[b], cap);
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) counts[(uint64_t)b * ntiles + t] = fill[b];
 }
 
 // ---- apply: one workgroup per bucket; stream its ntiles regions (16-B loads, 8 positions per
-// lane), ds_or into an 8 KiB LDS image, OR the image into the filter words it owns.
-template <int THREADS>
+// lane), ds_or into an 8 KiB LDS image, OR the image into the filter words it owns.  FRESH (a new
+// filter, its words never cleared): every word of the bucket, padding included, is written
+// instead, and a bucket whose runs overflowed folds in (and re-zeroes) its words of the overflow
+// bitmap `ovf`, which is all zero between builds.
+template <int THREADS, bool FRESH>
 __global__ __launch_bounds__(THREADS) void k_bkt_apply(const uint16_t *__restrict__ regions,
                                                    const uint32_t *__restrict__ counts, uint32_t ntiles, uint32_t cap,
-                                                   uint32_t *__restrict__ words, uint64_t nwords) {
+                                                   uint32_t *__restrict__ words, uint64_t nwords,
+                                                   uint32_t *__restrict__ ovf) {
     __shared__ uint32_t img[kBktWords];
     __shared__ uint32_t cnt[kMaxTiles];
+    __shared__ uint32_t spilled;
     const uint32_t b = blockIdx.x;
     for (uint32_t j = threadIdx.x; j < kBktWords; j += blockDim.x) img[j] = 0u;
-    for (uint32_t t = threadIdx.x; t < ntiles; t += blockDim.x) cnt[t] = min(counts[(uint64_t)b * ntiles + t], cap);
+    if (threadIdx.x == 0) spilled = 0u;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
+        const uint32_t c = counts[(uint64_t)b * ntiles + t];
+        if (c > cap) spilled = 1u;
+        cnt[t] = min(c, cap);
+    }
     __syncthreads();
     const uint32_t chunks = cap / 8;  // cap is a multiple of 8: regions are 16-B aligned
     const uint32_t pairs = ntiles * chunks;
@@ -259,9 +272,22 @@ __global__ __launch_bounds__(THREADS) void k_bkt_apply(const uint16_t *__restric
     }
     __syncthreads();
     const uint64_t w0 = (uint64_t)b * kBktWords;
-    for (uint32_t j = threadIdx.x; j < kBktWords; j += blockDim.x) {
-        const uint32_t v = img[j];
-        if (v && w0 + j < nwords) words[w0 + j] |= v;
+    if constexpr (FRESH) {  // nwords: the allocated words (padding included)
+        const bool sp = spilled != 0u;
+        for (uint32_t j = threadIdx.x; j < kBktWords; j += blockDim.x)
+            if (w0 + j < nwords) {
+                uint32_t v = img[j];
+                if (sp) {
+                    v |= ovf[w0 + j];
+                    ovf[w0 + j] = 0u;
+                }
+                words[w0 + j] = v;
+            }
+    } else {
+        for (uint32_t j = threadIdx.x; j < kBktWords; j += blockDim.x) {
+            const uint32_t v = img[j];
+            if (v && w0 + j < nwords) words[w0 + j] |= v;
+        }
     }
 }
 
@@ -325,11 +351,13 @@ uint64_t bucketed_workspace_bytes(uint64_t n, uint64_t m, uint32_t k) {
 
 // One launch pair (scatter + apply) per chunk of at most bucketed_max_keys keys; `chunk(k0, n)`
 // calls fn with the key source of keys [k0, k0 + n).
+// ovf != null: a fresh build (see k_bkt_apply); the first chunk writes the words, later chunks OR.
 template <typename Chunk>
 static hipError_t run_bucketed(uint64_t n, const ModArg &md, uint32_t *words, void *ws, uint64_t ws_bytes,
-                               hipStream_t s, Chunk &&chunk) {
+                               hipStream_t s, uint32_t *ovf, Chunk &&chunk) {
     const uint64_t maxk = bucketed_max_keys(md.k);
     for (uint64_t k0 = 0; k0 < n; k0 += maxk) {  // OR-accumulative: split large batches
+        const bool fresh = ovf && k0 == 0;
         const uint64_t sn = n - k0 < maxk ? n - k0 : maxk;
         const BktPlan p = plan_bucketed(sn, md.m, md.k);
         if (p.bytes > ws_bytes || p.ntiles > kMaxTiles) return hipErrorInvalidValue;
@@ -348,10 +376,14 @@ static hipError_t run_bucketed(uint64_t n, const ModArg &md, uint32_t *words, vo
             hipError_t a = hipFuncSetAttribute((const void *)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (a != hipSuccess) return a;
             hipLaunchKernelGGL(scat, dim3(p.ntiles), dim3(kScatterThreads), lds, s, src, sn, md, p.nb, p.tile_keys,
-                               p.ntiles, p.cap, regions, counts, words);
+                               p.ntiles, p.cap, regions, counts, fresh ? ovf : words);
             // apply: 1024 threads per bucket (256 and 512 measured slower)
-            hipLaunchKernelGGL(k_bkt_apply<1024>, dim3(p.nb), dim3(1024), 0, s, regions, counts, p.ntiles, p.cap, words,
-                               nwords);
+            if (fresh)
+                hipLaunchKernelGGL((k_bkt_apply<1024, true>), dim3(p.nb), dim3(1024), 0, s, regions, counts, p.ntiles,
+                                   p.cap, words, (md.m + 127) / 128 * 4, ovf);
+            else
+                hipLaunchKernelGGL((k_bkt_apply<1024, false>), dim3(p.nb), dim3(1024), 0, s, regions, counts, p.ntiles,
+                                   p.cap, words, nwords, nullptr);
             return hipGetLastError();
         });
         if (e != hipSuccess) return e;
@@ -360,9 +392,9 @@ static hipError_t run_bucketed(uint64_t n, const ModArg &md, uint32_t *words, vo
 }
 
 hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModArg &md, void *ws, uint64_t ws_bytes,
-                                 hipStream_t s) {
+                                 hipStream_t s, uint32_t *ovf) {
     if (kb.n == 0 || md.k == 0) return hipSuccess;
-    return run_bucketed(kb.n, md, words, ws, ws_bytes, s, [&](uint64_t k0, uint64_t sn, auto &&fn) {
+    return run_bucketed(kb.n, md, words, ws, ws_bytes, s, ovf, [&](uint64_t k0, uint64_t sn, auto &&fn) {
         KeyBatch sub = kb;
         sub.n = sn;
         if (kb.hashes)
@@ -376,10 +408,10 @@ hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModA
 }
 
 hipError_t launch_build_bucketed_packed(const uint64_t *packed, uint64_t n, uint32_t *words, const ModArg &md,
-                                        void *ws, uint64_t ws_bytes, hipStream_t s) {
+                                        void *ws, uint64_t ws_bytes, hipStream_t s, uint32_t *ovf) {
     if (n == 0) return hipSuccess;
     if (md.k != 7 || md.m >= (1ull << kPackBits)) return hipErrorInvalidValue;
-    return run_bucketed(n, md, words, ws, ws_bytes, s,
+    return run_bucketed(n, md, words, ws, ws_bytes, s, ovf,
                         [&](uint64_t k0, uint64_t, auto &&fn) { return fn(KeysPacked{packed + k0}); });
 }
 

@@ -222,7 +222,8 @@ extern "C" int seb_dev_clear(uint32_t *words, uint64_t m, void *stream) {
 // on the same stream therefore enqueues after the first call's launches, and a grow (stream sync
 // + free) can never free a buffer that another thread has been handed but not yet launched on.
 struct WsEntry {
-    int tag;  // 0: build / key preparation; 1: packed residues; 2: compacted probe rows; 3: MultiGet key-range order
+    int tag;  // 0: build / key preparation; 1: packed residues; 2: compacted probe rows; 3: MultiGet key-range order;
+              // 4: the fresh build's overflow bitmap (kept all zero)
     void *p;
     uint64_t bytes;
 };
@@ -286,7 +287,9 @@ static int ws_alloc(void **p, uint64_t bytes) {
     return SEB_OK;
 }
 
-static int cached_workspace(hipStream_t s, uint64_t bytes, void **out, int tag = 0) {
+// zero: a new (or regrown) buffer is cleared on the stream before first use (the fresh build's
+// overflow bitmap, which its users leave all zero).
+static int cached_workspace(hipStream_t s, uint64_t bytes, void **out, int tag = 0, bool zero = false) {
     if (t_ws_depth == 0) return fail(SEB_ERR_INVALID, "internal: library scratch requested outside a WsCall scope");
     int dev = 0;
     HIP_OR_FAIL(hipGetDevice(&dev));
@@ -305,6 +308,7 @@ static int cached_workspace(hipStream_t s, uint64_t bytes, void **out, int tag =
             int rc = ws_alloc(&e.p, bytes);
             if (rc) return rc;
             e.bytes = bytes;
+            if (zero) HIP_OR_FAIL(hipMemsetAsync(e.p, 0, bytes, s));
             *out = e.p;
             return SEB_OK;
         }
@@ -312,6 +316,7 @@ static int cached_workspace(hipStream_t s, uint64_t bytes, void **out, int tag =
     int rc = ws_alloc(&p, bytes);
     if (rc) return rc;
     sl->bufs.push_back({tag, p, bytes});
+    if (zero) HIP_OR_FAIL(hipMemsetAsync(p, 0, bytes, s));
     *out = p;
     return SEB_OK;
 }
@@ -391,14 +396,19 @@ static bool want_prehash_packed(const KeyBatch &kb, const ModArg &md) {
 // large variable-length batches are pre-hashed first.  `ws` / `ws_bytes` may be null/0, in which
 // case `grow` supplies scratch.
 // fresh: `words` holds nothing yet (a new filter); the image build then writes it without a clear,
+// and so does the bucketed build given `ovf` (an all-zero overflow bitmap of seb_words_bytes(m));
 // every other path clears it first.
 template <typename Grow>
 static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStream_t s, void *ws, uint64_t ws_bytes,
-                          Grow &&grow, bool fresh = false) {
-    if (kb.n == 0 || md.k == 0) return SEB_OK;
+                          Grow &&grow, bool fresh = false, uint32_t *ovf = nullptr) {
+    if (kb.n == 0 || md.k == 0) {
+        if (fresh) HIP_OR_FAIL(launch_clear_words(words, seb_words_bytes(md.m), s));
+        return SEB_OK;
+    }
     const int algo = choose_build_algo(kb.n, md.m, md.k);
     const bool bucketed = algo == 2;
-    if (fresh && algo != 4) HIP_OR_FAIL(launch_clear_words(words, seb_words_bytes(md.m), s));
+    if (!(fresh && bucketed)) ovf = nullptr;
+    if (fresh && algo != 4 && !ovf) HIP_OR_FAIL(launch_clear_words(words, seb_words_bytes(md.m), s));
     if (bucketed && want_prehash_packed(kb, md)) {  // scratch: [packed residues | bucketed]
         const uint64_t pack_b = (kb.n * 8 + 255) & ~255ull;
         const uint64_t need = pack_b + bucketed_workspace_bytes(kb.n, md.m, md.k);
@@ -409,7 +419,7 @@ static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStr
         }
         HIP_OR_FAIL(launch_hash_varlen_packed(kb, md, (uint64_t *)ws, s));
         HIP_OR_FAIL(launch_build_bucketed_packed((const uint64_t *)ws, kb.n, words, md, (uint8_t *)ws + pack_b,
-                                                 ws_bytes - pack_b, s));
+                                                 ws_bytes - pack_b, s, ovf));
         return SEB_OK;
     }
     const uint64_t head = prehash_bytes(kb);
@@ -425,7 +435,7 @@ static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStr
         kb.hashes = (const uint4 *)ws;
     }
     if (bucketed) {
-        HIP_OR_FAIL(launch_build_bucketed(kb, words, md, (uint8_t *)ws + head, ws_bytes - head, s));
+        HIP_OR_FAIL(launch_build_bucketed(kb, words, md, (uint8_t *)ws + head, ws_bytes - head, s, ovf));
         return SEB_OK;
     }
     if (algo == 4) {
@@ -536,6 +546,25 @@ extern "C" int seb_dev_build(const seb_keys *keys, uint32_t *words, uint64_t m, 
     hipStream_t s = (hipStream_t)stream;
     return build_dispatch(key_batch(keys), words, mod_arg(m, k), s, nullptr, 0,
                           [&](uint64_t need, void **out) { return cached_workspace(s, need, out); });
+}
+
+extern "C" int seb_dev_build_fresh(const seb_keys *keys, uint32_t *words, uint64_t m, uint32_t k, void *stream) {
+    WsCall ws_call;
+    enter();
+    int rc;
+    if ((rc = check_keys(keys, "seb_dev_build_fresh")) || (rc = check_filter_args(m, k, "seb_dev_build_fresh")))
+        return rc;
+    if (!words) return fail(SEB_ERR_INVALID, "seb_dev_build_fresh: null words");
+    hipStream_t s = (hipStream_t)stream;
+    const KeyBatch kb = key_batch(keys);
+    const ModArg md = mod_arg(m, k);
+    void *ovf = nullptr;
+    if (kb.n && choose_build_algo(kb.n, md.m, md.k) == 2 &&
+        (rc = cached_workspace(s, seb_words_bytes(m), &ovf, 4, true)))
+        return rc;
+    return build_dispatch(kb, words, md, s, nullptr, 0,
+                          [&](uint64_t need, void **out) { return cached_workspace(s, need, out); }, true,
+                          (uint32_t *)ovf);
 }
 
 extern "C" int seb_dev_probe(const seb_keys *keys, const uint32_t *words, uint64_t m, uint32_t k, uint8_t *out,

@@ -133,10 +133,12 @@ hipError_t launch_clear_words(uint32_t *words, uint64_t bytes, hipStream_t s);
 bool bucketed_supported(uint64_t m, uint32_t k);
 uint64_t bucketed_workspace_bytes(uint64_t n, uint64_t m, uint32_t k);
 // Build from packed residues (k == 7, m < 2^kPackBits); same workspace as launch_build_bucketed.
+// ovf != null: a fresh build: `words` (seb_words_bytes) need no clear and are written whole;
+// `ovf` is an all-zero bitmap of the same size, left all zero again.
 hipError_t launch_build_bucketed_packed(const uint64_t *packed, uint64_t n, uint32_t *words, const ModArg &md,
-                                        void *ws, uint64_t ws_bytes, hipStream_t s);
+                                        void *ws, uint64_t ws_bytes, hipStream_t s, uint32_t *ovf = nullptr);
 hipError_t launch_build_bucketed(const KeyBatch &kb, uint32_t *words, const ModArg &md, void *ws, uint64_t ws_bytes,
-                                 hipStream_t s);
+                                 hipStream_t s, uint32_t *ovf = nullptr);
 // 1 = atomic, 2 = bucketed, 3 = LDS-resident (atomic merge), 4 = LDS images + OR kernel, for a
 // batch of n keys into an m-bit filter.
 int choose_build_algo(uint64_t n, uint64_t m, uint32_t k);

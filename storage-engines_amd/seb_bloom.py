@@ -64,6 +64,7 @@ _SIGS = {
     "seb_device_check": (_i, [_i]),
     "seb_dev_clear": (_i, [_vp, _u64, _vp]),
     "seb_dev_build": (_i, [C.POINTER(seb_keys), _vp, _u64, _u32, _vp]),
+    "seb_dev_build_fresh": (_i, [C.POINTER(seb_keys), _vp, _u64, _u32, _vp]),
     "seb_dev_probe": (_i, [C.POINTER(seb_keys), _vp, _u64, _u32, _vp, _vp]),
     "seb_dev_probe_multi": (_i, [C.POINTER(seb_keys), C.POINTER(seb_filter_ref), _u32, _vp, _u32, _vp]),
     "seb_dev_build_many": (_i, [C.POINTER(seb_keys), C.POINTER(_u64), C.POINTER(seb_filter_ref), _u32, _vp]),
@@ -490,6 +491,11 @@ def dev_clear(words, m: int, stream=None) -> None:
 
 def dev_build(keys: seb_keys, words, m: int, k: int, stream=None) -> None:
     check(lib().seb_dev_build(C.byref(keys), words.data_ptr(), m, k, _stream(stream)))
+
+
+def dev_build_fresh(keys: seb_keys, words, m: int, k: int, stream=None) -> None:
+    """A new filter from the keys: `words` need not be cleared (every word is written)."""
+    check(lib().seb_dev_build_fresh(C.byref(keys), words.data_ptr(), m, k, _stream(stream)))
 
 
 def dev_build_workspace_size(n: int, m: int, k: int) -> int:

@@ -1641,6 +1641,54 @@ def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
         seb.set_option("build_algo", 0)
 
 
+@pytest.mark.parametrize("algo", [0, 1, 2, 3, 4])
+def test_fresh_build_overwrites_garbage(seb, golden, torch_cuda, algo):
+    """seb_dev_build_fresh: words full of garbage (never cleared) become the filter of the keys, bit
+    for bit, padding zero: the C2 golden at 10M (radix-partitioned: written whole) and 100K keys
+    (the small-filter paths clear first); twice in a row on one buffer."""
+    torch = torch_cuda
+    with seb.option("build_algo", algo):
+        for n in (10_000_000, 100_000):
+            row = next(r for r in golden["fixed16"] if r["n"] == n)
+            m, k = row["m"], row["k"]
+            if algo in (3, 4) and seb.words_bytes(m) > 160 * 1024:
+                continue
+            kd = seb.dev_keys(to_dev(torch, kg.key16(np.arange(n))), n=n, stride=16)
+            words = seb.new_words(m)
+            for rep in range(2):
+                words.view(torch.uint8).fill_(0xA5 if rep == 0 else 0x5A)
+                seb.dev_build_fresh(kd, words, m, k)
+                torch.cuda.synchronize()
+                raw = words.cpu().numpy().view(np.uint8)
+                bits = raw[: (m + 7) // 8]
+                assert sha(bn.encode(bits, m, k)) == row["encode_sha256"], (algo, n, rep)
+                assert not raw[(m + 7) // 8:].any(), (algo, n, rep)
+
+
+@pytest.mark.parametrize("case", ["duplicates", "skewed"])
+def test_fresh_build_overflow(seb, torch_cuda, case):
+    """A fresh radix-partitioned build whose runs overflow their regions: the overflowed positions
+    go to the overflow bitmap, which apply folds into the (never cleared) words and leaves zero:
+    the next fresh build on the same stream, of ordinary keys, equals the oracle too."""
+    torch = torch_cuda
+    rng = np.random.default_rng(9)
+    n, m, k = 400_000, 3_834_024, 7
+    keys = np.tile(kg.key16(np.array([42])), (n, 1)) if case == "duplicates" else kg.key16(rng.integers(0, 50, n))
+    uniq = np.unique(keys, axis=0)
+    ref = oc.build(m, k, np.ascontiguousarray(uniq).ravel(), len(uniq), stride=16)
+    plain = kg.key16(np.arange(n))
+    ref2 = oc.build(m, k, plain, n, stride=16)
+    with seb.option("build_algo", 2):
+        words = seb.new_words(m)
+        for ks, want in ((keys, ref), (plain, ref2), (keys, ref), (plain, ref2)):
+            words.view(torch.uint8).fill_(0xFF)
+            seb.dev_build_fresh(seb.dev_keys(to_dev(torch, ks), n=n, stride=16), words, m, k)
+            torch.cuda.synchronize()
+            raw = words.cpu().numpy().view(np.uint8)
+            assert np.array_equal(raw[: (m + 7) // 8], want)
+            assert not raw[(m + 7) // 8:].any()
+
+
 # ------------------------------------------------ sharded build of one filter (§8(e)) ----
 
 def test_or_slices_kernel(seb, torch_cuda):
