@@ -342,6 +342,23 @@ static void ws_drop_stream(int dev, hipStream_t s) {
     sl->dead = true;
 }
 
+// Drop this stream's scratch buffer `tag` (after a failed call that may have left it dirty, such as
+// the fresh build's overflow bitmap); the next request allocates (and zeroes) a new one.
+static void ws_discard(hipStream_t s, int tag) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return (void)hipGetLastError();
+    WsSlot *sl = ws_slot(dev, s);
+    std::lock_guard<std::recursive_mutex> g(sl->mu);
+    for (auto &e : sl->bufs)
+        if (e.tag == tag && e.p) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(e.p);
+            e.p = nullptr;
+            e.bytes = 0;
+        }
+    (void)hipGetLastError();
+}
+
 // Slots are never deleted, so the pointers stay valid after g_ws_mu is dropped (a call holding a
 // slot's lock may take g_ws_mu for another request, so the two are never held in that order here).
 static std::vector<WsSlot *> ws_slots_snapshot() {
@@ -562,9 +579,11 @@ extern "C" int seb_dev_build_fresh(const seb_keys *keys, uint32_t *words, uint64
     if (kb.n && choose_build_algo(kb.n, md.m, md.k) == 2 &&
         (rc = cached_workspace(s, seb_words_bytes(m), &ovf, 4, true)))
         return rc;
-    return build_dispatch(kb, words, md, s, nullptr, 0,
-                          [&](uint64_t need, void **out) { return cached_workspace(s, need, out); }, true,
-                          (uint32_t *)ovf);
+    rc = build_dispatch(kb, words, md, s, nullptr, 0,
+                        [&](uint64_t need, void **out) { return cached_workspace(s, need, out); }, true,
+                        (uint32_t *)ovf);
+    if (rc && ovf) ws_discard(s, 4);  // the bitmap may no longer be all zero
+    return rc;
 }
 
 extern "C" int seb_dev_probe(const seb_keys *keys, const uint32_t *words, uint64_t m, uint32_t k, uint8_t *out,
