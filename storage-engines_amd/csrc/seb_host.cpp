@@ -502,6 +502,13 @@ static bool want_phased(uint64_t n, const ModArg &md, const uint8_t *out) {
 static int probe_dispatch(KeyBatch kb, const uint32_t *words, const ModArg &md, uint8_t *out, hipStream_t s) {
     void *ws;
     int rc;
+    if (want_phased(kb.n, md, out) && want_prehash_packed(kb, md) && options().probe_compact) {
+        // the pre-hash with phase 0 fused in: compacted rows (tag 2) only, no dense packed batch
+        void *rows;
+        if ((rc = cached_workspace(s, probe_compact_bytes(kb.n), &rows, 2))) return rc;
+        HIP_OR_FAIL(launch_probe_compact_varlen(kb, words, md, out, rows, s));
+        return SEB_OK;
+    }
     if (want_phased(kb.n, md, out) && want_prehash_packed(kb, md)) {  // pre-hash to packed, all phases from it
         void *packed;
         if ((rc = cached_workspace(s, kb.n * 8, &packed, 1))) return rc;

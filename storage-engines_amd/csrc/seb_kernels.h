@@ -184,6 +184,11 @@ hipError_t launch_probe_phased(const KeyBatch *kb, uint64_t n, const uint32_t *w
 uint64_t probe_compact_bytes(uint64_t n);
 hipError_t launch_probe_compact(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, void *ws,
                                 hipStream_t s);
+// The same from a variable-length batch, phase 0 fused into the LDS-staged pre-hash.
+hipError_t launch_probe_compact_varlen(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out,
+                                       void *ws, hipStream_t s);
+hipError_t launch_hash_varlen_phase0(const KeyBatch &kb, const ModArg &md, const uint32_t *words, uint64_t *rows,
+                                     ulonglong2 *recs, uint32_t hi, hipStream_t s);
 // The same from a batch of packed residues (the pre-hashed variable-length batch, a broadcast batch).
 hipError_t launch_probe_compact_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
                                        uint8_t *out, void *ws, hipStream_t s);

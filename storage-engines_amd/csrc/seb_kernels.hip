@@ -1092,7 +1092,7 @@ static hipError_t run_probe_compact(uint64_t n, const uint32_t *words, const Mod
                            md, rows, recs, bound(1));
         return hipGetLastError();
     };
-    hipError_t e = phase0(launch0);
+    hipError_t e = phase0(launch0, rows, recs, bound(1));
     if (e != hipSuccess) return e;
     // 4 groups per wave iteration (1, 2 and 8 measured slower)
     constexpr int G = 4;
@@ -1111,12 +1111,22 @@ static hipError_t run_probe_compact(uint64_t n, const uint32_t *words, const Mod
 
 hipError_t launch_probe_compact(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out, void *ws,
                                 hipStream_t s) {
-    return run_probe_compact(kb.n, words, md, out, ws, s, [&](auto &&launch0) { return with_src(kb, launch0); });
+    return run_probe_compact(kb.n, words, md, out, ws, s,
+                             [&](auto &&launch0, uint64_t *, ulonglong2 *, uint32_t) { return with_src(kb, launch0); });
 }
 
 hipError_t launch_probe_compact_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
                                        uint8_t *out, void *ws, hipStream_t s) {
-    return run_probe_compact(n, words, md, out, ws, s, [&](auto &&launch0) { return launch0(KeysPacked{packed}); });
+    return run_probe_compact(n, words, md, out, ws, s, [&](auto &&launch0, uint64_t *, ulonglong2 *, uint32_t) {
+        return launch0(KeysPacked{packed});
+    });
+}
+
+hipError_t launch_probe_compact_varlen(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out,
+                                       void *ws, hipStream_t s) {
+    return run_probe_compact(kb.n, words, md, out, ws, s, [&](auto &&, uint64_t *rows, ulonglong2 *recs, uint32_t hi) {
+        return launch_hash_varlen_phase0(kb, md, words, rows, recs, hi, s);
+    });
 }
 
 // Phases of the phased probe: probe_phases, or one per 4 MiB of filter (one XCD's L2).

@@ -144,23 +144,67 @@ __device__ __forceinline__ void put_hash(void *out, uint64_t i, uint64_t h1, uin
 // the other waves are done) are hashed by the last 2 * NS waves, a pair per 64 keys, one wave per
 // FNV chain: each runs half the instructions.  The FNV-1 wave hands its hashes to the FNV-1a
 // wave through LDS for the packed output; the 16-B output is written in halves.
-template <uint32_t KEYS, uint32_t WIN, bool PACK, uint32_t NS = 0>
+// P0 (with PACK): the compacted phased probe's phase 0 fused in (k_probe_c0's job for a pre-hashed
+// batch): the packed words stay in LDS in key order, then each wave takes one group of 64 keys,
+// tests the positions in range 0 [0, p0.hi) and stores the live keys' words compacted in the
+// group's row and the group's {mask0, live} record, so the dense packed batch never reaches HBM.
+struct Phase0Arg {
+    const uint32_t *words;
+    uint64_t *rows;
+    ulonglong2 *recs;
+    uint32_t hi;
+};
+
+// Every thread of the workgroup arrives here; waves 0 .. KEYS/64 - 1 each take the group of keys
+// k0 + 64 * wave + lane (k0 is a multiple of 64).
+template <uint32_t KEYS>
+__device__ __forceinline__ void varlen_phase0(const uint64_t *xpk, uint64_t k0, uint32_t cnt, const ModArg &md,
+                                              const Phase0Arg &p0) {
+    __syncthreads();  // every key's packed word is in xpk
+    const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    if (wid >= KEYS / 64 || 64 * wid >= cnt) return;  // wave-uniform; no barrier follows
+    const uint32_t j = 64 * wid + lane;
+    const bool valid = j < cnt;
+    const uint64_t pw = valid ? xpk[j] : 0ull;
+    uint32_t pos[7];
+    packed_positions(pw, (uint32_t)md.m, (uint32_t)md.c, pos);
+    uint32_t acc = valid ? 1u : 0u;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        const uint32_t w = pos[q] >> 5;
+        if ((acc & 1u) && w < p0.hi) acc &= p0.words[w] >> (pos[q] & 31);
+    }
+    const uint64_t alive = __ballot(acc & 1u);
+    const uint64_t g = (k0 >> 6) + wid;
+    if (acc & 1u) __builtin_nontemporal_store(pw, p0.rows + g * 64 + lanes_below(alive));
+    if (lane == 0) p0.recs[g] = make_ulonglong2(alive, alive);
+}
+
+template <uint32_t KEYS, uint32_t WIN, bool PACK, uint32_t NS = 0, bool P0 = false>
 __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *__restrict__ data,
                                                       const uint64_t *__restrict__ off, uint64_t n,
-                                                      void *__restrict__ hashes, ModArg md) {
+                                                      void *__restrict__ hashes, ModArg md, Phase0Arg p0) {
     constexpr uint32_t kHashLds = KEYS * WIN;
     static_assert(kHashLds % 16 == 0 && kHashLds + 16 < 65536, "window offsets are 16-bit");
+    static_assert(!P0 || (PACK && KEYS % 64 == 0), "phase 0 takes packed words in whole groups of 64 keys");
     __shared__ uint4 stage[kHashLds / 16 + 1];  // +16 B: the funnel walk reads one dword past a key
     __shared__ uint32_t cur[kLenBuckets];
     __shared__ uint32_t slot_key[KEYS];  // sorted slot -> start byte in the window << 16 | length
     __shared__ uint16_t slot_idx[KEYS];  // sorted slot -> key within the workgroup
     __shared__ uint64_t xh2[NS ? 64 * NS : 1];  // the FNV-1 waves' hashes for the FNV-1a waves
     __shared__ uint32_t xflag[NS ? NS : 1];
+    __shared__ uint64_t xpk[P0 ? KEYS : 1];     // P0: the packed words in key order
     const uint32_t t = threadIdx.x;
     const uint64_t k0 = (uint64_t)blockIdx.x * KEYS;
     const uint64_t k1 = k0 + KEYS < n ? k0 + KEYS : n;
     const uint32_t cnt = (uint32_t)(k1 - k0);
     const bool mine = t < cnt;
+    auto emit = [&](uint32_t j, uint64_t h1, uint64_t h2) {  // key k0 + j
+        if constexpr (P0)
+            xpk[j] = pack_residue(h1, h2, md);
+        else
+            put_hash<PACK>(hashes, k0 + j, h1, h2, md);
+    };
     const uint64_t ks = mine ? off[k0 + t] : 0, ke = mine ? off[k0 + t + 1] : 0;
     const uintptr_t s0 = (uintptr_t)(data + off[k0]);
     const uintptr_t s1 = (uintptr_t)(data + off[k1]);
@@ -170,8 +214,10 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
         if (mine) {
             uint64_t h1, h2;
             fnv_range(data, ks, ke, h1, h2);
-            put_hash<PACK>(hashes, k0 + t, h1, h2, md);
+            emit(t, h1, h2);
         }
+        if constexpr (P0)
+            varlen_phase0<KEYS>(xpk, k0, cnt, md, p0);
         return;
     }
     if (t < kLenBuckets) cur[t] = 0u;
@@ -212,20 +258,22 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
     }
     __syncthreads();
     const uint32_t *lds = (const uint32_t *)stage;
+    bool tail = false;
     if constexpr (NS > 0) {
         if (cnt == KEYS && t >= KEYS - 64 * NS) {  // the longest keys: a wave pair per 64, one per chain
+            tail = true;
             const uint32_t w = (t - (KEYS - 64 * NS)) >> 6, c = w >> 1, lane = t & 63;
             const uint32_t q = KEYS - 64 * NS + 64 * c + lane;
             const uint32_t sk = slot_key[q];
-            const uint64_t i = k0 + slot_idx[q];
+            const uint32_t j = slot_idx[q];
             if ((w & 1u) == 0u) {  // FNV-1a (hash1)
                 const uint64_t h1 = funnel_one<true>(lds, sk >> 16, sk & 0xffffu);
                 if constexpr (PACK) {
                     while (__hip_atomic_load(&xflag[c], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
                         __builtin_amdgcn_s_sleep(1);
-                    put_hash<PACK>(hashes, i, h1, xh2[64 * c + lane], md);
+                    emit(j, h1, xh2[64 * c + lane]);
                 } else {
-                    ((uint2 *)hashes)[2 * i] = make_uint2((uint32_t)h1, (uint32_t)(h1 >> 32));
+                    ((uint2 *)hashes)[2 * (k0 + j)] = make_uint2((uint32_t)h1, (uint32_t)(h1 >> 32));
                 }
             } else {  // FNV-1 (hash2)
                 const uint64_t h2 = funnel_one<false>(lds, sk >> 16, sk & 0xffffu);
@@ -236,33 +284,42 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
                     if (lane == 0)
                         __hip_atomic_store(&xflag[c], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 } else {
-                    ((uint2 *)hashes)[2 * i + 1] = make_uint2((uint32_t)h2, (uint32_t)(h2 >> 32));
+                    ((uint2 *)hashes)[2 * (k0 + j) + 1] = make_uint2((uint32_t)h2, (uint32_t)(h2 >> 32));
                 }
             }
-            return;
+            if constexpr (!P0) return;
         }
     }
-    if (!mine) return;  // cnt lanes hash the cnt sorted slots
-    const uint32_t sk = slot_key[t];
-    Funnel f;
-    f.init(lds, sk >> 16, sk & 0xffffu);
-    f.walk(lds);
-    uint64_t h1, h2;
-    f.finish(lds, h1, h2);
-    put_hash<PACK>(hashes, k0 + slot_idx[t], h1, h2, md);
+    if (mine && !tail) {  // cnt lanes hash the cnt sorted slots
+        const uint32_t sk = slot_key[t];
+        Funnel f;
+        f.init(lds, sk >> 16, sk & 0xffffu);
+        f.walk(lds);
+        uint64_t h1, h2;
+        f.finish(lds, h1, h2);
+        emit(slot_idx[t], h1, h2);
+    }
+    if constexpr (P0) varlen_phase0<KEYS>(xpk, k0, cnt, md, p0);
 }
 
 // 448 keys per 512-thread workgroup, the top 64 split over two chain waves, a 64-B window per key
 // (256/384/512/1024-key workgroups and 48-80-B windows measured slower).
 constexpr uint32_t kVarKeys = 448, kVarWin = 64, kVarSplit = 1;
 
-template <bool PACK>
-static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const ModArg &md, hipStream_t s) {
+template <bool PACK, bool P0 = false>
+static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const ModArg &md, hipStream_t s,
+                                        Phase0Arg p0 = {}) {
     if (!kb.offsets || kb.n == 0) return hipSuccess;
     const uint64_t ntiles = (kb.n + kVarKeys - 1) / kVarKeys;
-    hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, kVarSplit>), dim3((unsigned)ntiles),
-                       dim3(kVarKeys + 64 * kVarSplit), 0, s, kb.data, kb.offsets, kb.n, out, md);
+    hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, kVarSplit, P0>), dim3((unsigned)ntiles),
+                       dim3(kVarKeys + 64 * kVarSplit), 0, s, kb.data, kb.offsets, kb.n, out, md, p0);
     return hipGetLastError();
+}
+
+hipError_t launch_hash_varlen_phase0(const KeyBatch &kb, const ModArg &md, const uint32_t *words, uint64_t *rows,
+                                     ulonglong2 *recs, uint32_t hi, hipStream_t s) {
+    if (md.k != 7 || md.m >= (1ull << kPackBits)) return hipErrorInvalidValue;
+    return launch_hash_varlen_any<true, true>(kb, nullptr, md, s, Phase0Arg{words, rows, recs, hi});
 }
 
 hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s) {

@@ -556,9 +556,11 @@ def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed):
 @pytest.mark.parametrize("k", [7, 8])
 @pytest.mark.parametrize("algo", [1, 2])
 def test_varlen_prehash_packed_paths(seb, torch_cuda, k, algo, probe_compact):
-    """Pre-hash to packed residues (k = 7: bucketed build from KeysPacked, phased probe from packed
-    words, pack_residues / emit_packed over variable-length keys) against the oracle, and the
-    16-B hash path (k = 8); a 2-range filter so the k = 7 probe runs phased."""
+    """Pre-hash to packed residues (k = 7: bucketed build from KeysPacked; the phased probe with
+    phase 0 fused into the pre-hash (compacted) or from the dense packed words; pack_residues /
+    emit_packed over variable-length keys) against the oracle, and the 16-B hash path (k = 8); a
+    2-range filter so the k = 7 probe runs phased; keys up to 3000 B, so some workgroups take the
+    pre-hash's straight-from-HBM path."""
     torch = torch_cuda
     packed = k == 7
     rng = np.random.default_rng(11 + packed)
