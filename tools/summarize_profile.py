@@ -31,10 +31,11 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STEP_KERNELS = {  # per config: timed step name -> kernels launched by that step
-    "c2c3": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned", "k_clear_words"),
+    "c2c3": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "k_clear_words"),
              "probe": ("k_probe",)},
-    "c4": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "fillBufferAligned", "k_hash_varlen"),
-           "probe": ("k_probe", "k_hash_varlen")},
+    # the pre-hash is k_hash_varlen<..., false> for the build and <..., true> (phase 0 fused) for the probe
+    "c4": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "1u, false>"),
+           "probe": ("k_probe", "1u, true>")},
     "c5": {"probe": ("k_probe_interleaved", "k_interleave", "k_probe_multi")},
     "lsm": {"probe": ("k_multiget", "k_mg_")},
     "lsm_wide": {"probe": ("k_multiget", "k_mg_")},
@@ -103,7 +104,7 @@ def main():
             elif c == "WRITE_SIZE":
                 write += v
         wide = WIDE_STREAMS.get(a.config, {}).get(step, a.key_bytes)
-        if any("k_probe_c0" in k for k in kernels) and a.config in WIDE_STREAMS:
+        if step == "probe" and any("k_probe_cp" in k for k in kernels) and a.config in WIDE_STREAMS:
             wide -= 2 * 8 * N  # compacted phases read their rows 8 B per lane: no wide packed stream
         read = fetch * 1024 + wide / 2
         steps[step] = {"hbm_bytes_per_launch": int(read + write * 1024), "read_bytes": int(read),
