@@ -145,7 +145,7 @@ __device__ __forceinline__ void put_hash(void *out, uint64_t i, uint64_t h1, uin
 // FNV chain: each runs half the instructions.  The FNV-1 wave hands its hashes to the FNV-1a
 // wave through LDS for the packed output; the 16-B output is written in halves.
 // P0 (with PACK): the compacted phased probe's phase 0 fused in (k_probe_c0's job for a pre-hashed
-// batch): the packed words stay in LDS in key order, then each wave takes one group of 64 keys,
+// batch): the packed words go to LDS in key order, then each wave takes one group of 64 keys,
 // tests the positions in range 0 [0, p0.hi) and stores the live keys' words compacted in the
 // group's row and the group's {mask0, live} record, so the dense packed batch never reaches HBM.
 struct Phase0Arg {
@@ -155,12 +155,15 @@ struct Phase0Arg {
     uint32_t hi;
 };
 
-// Every thread of the workgroup arrives here; waves 0 .. KEYS/64 - 1 each take the group of keys
+// Every thread of the workgroup arrives here (has: it hashed key k0 + my_j); the packed words go to
+// xpk (the staging window), then waves 0 .. KEYS/64 - 1 each take the group of keys
 // k0 + 64 * wave + lane (k0 is a multiple of 64).
 template <uint32_t KEYS>
-__device__ __forceinline__ void varlen_phase0(const uint64_t *xpk, uint64_t k0, uint32_t cnt, const ModArg &md,
-                                              const Phase0Arg &p0) {
-    __syncthreads();  // every key's packed word is in xpk
+__device__ __forceinline__ void varlen_phase0(uint64_t *xpk, bool has, uint32_t my_j, uint64_t my_pw, uint64_t k0,
+                                              uint32_t cnt, const ModArg &md, const Phase0Arg &p0) {
+    __syncthreads();  // every key is hashed: the staging window is free
+    if (has) xpk[my_j] = my_pw;
+    __syncthreads();  // every key's packed word is in xpk, in key order
     const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     if (wid >= KEYS / 64 || 64 * wid >= cnt) return;  // wave-uniform; no barrier follows
     const uint32_t j = 64 * wid + lane;
@@ -186,24 +189,31 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
                                                       void *__restrict__ hashes, ModArg md, Phase0Arg p0) {
     constexpr uint32_t kHashLds = KEYS * WIN;
     static_assert(kHashLds % 16 == 0 && kHashLds + 16 < 65536, "window offsets are 16-bit");
-    static_assert(!P0 || (PACK && KEYS % 64 == 0), "phase 0 takes packed words in whole groups of 64 keys");
+    static_assert(!P0 || (PACK && KEYS % 64 == 0 && KEYS * 8 <= kHashLds), "phase 0: whole groups of 64 keys, words in the window");
     __shared__ uint4 stage[kHashLds / 16 + 1];  // +16 B: the funnel walk reads one dword past a key
     __shared__ uint32_t cur[kLenBuckets];
     __shared__ uint32_t slot_key[KEYS];  // sorted slot -> start byte in the window << 16 | length
     __shared__ uint16_t slot_idx[KEYS];  // sorted slot -> key within the workgroup
     __shared__ uint64_t xh2[NS ? 64 * NS : 1];  // the FNV-1 waves' hashes for the FNV-1a waves
     __shared__ uint32_t xflag[NS ? NS : 1];
-    __shared__ uint64_t xpk[P0 ? KEYS : 1];     // P0: the packed words in key order
     const uint32_t t = threadIdx.x;
     const uint64_t k0 = (uint64_t)blockIdx.x * KEYS;
     const uint64_t k1 = k0 + KEYS < n ? k0 + KEYS : n;
     const uint32_t cnt = (uint32_t)(k1 - k0);
     const bool mine = t < cnt;
+    // P0: a thread keeps its key's packed word until every key is hashed, then the words go to the
+    // (by then unused) staging window in key order: no LDS of its own, so 5 workgroups still fit a CU
+    uint32_t my_j = 0;
+    uint64_t my_pw = 0;
+    bool has = false;
     auto emit = [&](uint32_t j, uint64_t h1, uint64_t h2) {  // key k0 + j
-        if constexpr (P0)
-            xpk[j] = pack_residue(h1, h2, md);
-        else
+        if constexpr (P0) {
+            my_j = j;
+            my_pw = pack_residue(h1, h2, md);
+            has = true;
+        } else {
             put_hash<PACK>(hashes, k0 + j, h1, h2, md);
+        }
     };
     const uint64_t ks = mine ? off[k0 + t] : 0, ke = mine ? off[k0 + t + 1] : 0;
     const uintptr_t s0 = (uintptr_t)(data + off[k0]);
@@ -217,7 +227,7 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
             emit(t, h1, h2);
         }
         if constexpr (P0)
-            varlen_phase0<KEYS>(xpk, k0, cnt, md, p0);
+            varlen_phase0<KEYS>((uint64_t *)stage, has, my_j, my_pw, k0, cnt, md, p0);
         return;
     }
     if (t < kLenBuckets) cur[t] = 0u;
@@ -299,7 +309,7 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
         f.finish(lds, h1, h2);
         emit(slot_idx[t], h1, h2);
     }
-    if constexpr (P0) varlen_phase0<KEYS>(xpk, k0, cnt, md, p0);
+    if constexpr (P0) varlen_phase0<KEYS>((uint64_t *)stage, has, my_j, my_pw, k0, cnt, md, p0);
 }
 
 // 448 keys per 512-thread workgroup, the top 64 split over two chain waves, a 64-B window per key
