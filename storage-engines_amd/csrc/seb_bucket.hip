@@ -5,12 +5,12 @@
 // profiles/r01), which caps the build at ~27 G bit-sets/s.  This path instead partitions the
 // n*k bit positions by 64 Ki-bit bucket (one 8 KiB LDS image each) and sets the bits in LDS:
 //
-//   A  k_bkt_count    tile of keys per workgroup -> per-(tile, bucket) counts      [ntiles][nb]
-//   B  k_bkt_scan_*   exclusive scan in bucket-major order -> global run offsets    [nb][ntiles]
-//   C  k_bkt_scatter  re-hash the tile, counting-sort its positions by bucket in LDS, write each
-//                     bucket run (u16 in-bucket bit index) contiguously to its global offset
-//   D  k_bkt_apply    one workgroup per bucket: stream its contiguous run, ds_or into an 8 KiB
-//                     LDS image, OR the image into the filter words (the workgroup owns them)
+//   k_bkt_scatter  one workgroup per super-tile of keys: hash a round of keys, counting-sort its
+//                  positions by bucket in LDS, append each bucket's run (u16 in-bucket bit index)
+//                  to the fixed-capacity region (bucket, tile); the run lengths go to counts
+//   k_bkt_apply    one workgroup per bucket: stream its ntiles regions, ds_or into an 8 KiB LDS
+//                  image, then OR the image into the filter words the workgroup owns, or for a
+//                  fresh build write them whole (no clear beforehand)
 //
 // The result is the same bit array bit for bit (OR is order-independent).  Requires m <= 2^28
 // (<= 4096 buckets) and n*k < 2^32 per launch; the host splits larger batches.
