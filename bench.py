@@ -165,7 +165,9 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
     packed = world > 1 and args.bcast == "packed" and k == 7 and m < (1 << 29)
     per_step = world > 1 and args.bcast_per_step
     st.workload = ("C2+C3: per GPU build one filter from 10M x 16B keys @1% FPR (m=95,850,584, k=7) "
-                   "+ probe a 10M-key batch (50% present)")
+                   + ("(a new filter: every word written by the build, no separate clear) " if args.fresh_build
+                      else "(clear + build) ")
+                   + "+ probe a 10M-key batch (50% present)")
     if world == 1:
         st.workload += ", resident in HBM (one GPU: no broadcast)"
     elif per_step:
