@@ -846,21 +846,26 @@ def test_multi_filter_probe(seb, golden, torch_cuda, which):
     assert np.array_equal(mm.cpu().numpy(), ref.astype(np.uint8))
 
 
-@pytest.mark.parametrize("interleave", [0, 1])
-def test_multi_filter_interleaved_vs_direct(seb, golden, torch_cuda, interleave):
-    """The interleaved (bit-transposed) table path and the per-filter path give identical masks."""
+@pytest.mark.parametrize("interleave,aligned", [(0, True), (1, True), (1, False)])
+def test_multi_filter_interleaved_vs_direct(seb, golden, torch_cuda, interleave, aligned):
+    """The interleaved (bit-transposed) table path and the per-filter path give identical masks; the
+    table is built by wave ballots from 16-B aligned filters and entry by entry otherwise (word
+    arrays starting 4 bytes into their buffers)."""
     torch = torch_cuda
     row = golden["multi"][1]  # 64 filters x 2000 keys
     nf, per, npr, m, k = row["filters"], row["keys_per_filter"], row["probes"], row["m"], row["k"]
     keys = to_dev(torch, kg.key16(np.arange(nf * per)))
-    filters = [(seb.new_words(m), m, k) for _ in range(nf)]
+    nw = seb.words_bytes(m) // 4
+    filters = [((seb.new_words(m) if aligned else torch.zeros(nw + 4, dtype=torch.int32, device="cuda")[1:nw + 1]),
+                m, k) for _ in range(nf)]
     seb.dev_build_many(seb.dev_keys(keys, n=nf * per, stride=16), [f * per for f in range(nf + 1)], filters)
     q = np.arange(npr, dtype=np.int64)
     half = q // 2
     kd = seb.dev_keys(to_dev(torch, kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q))),
                       n=npr, stride=16)
     with seb.option("multi_interleave", interleave):
-        for dt, nsub in ((torch.int64, 64), (torch.int32, 32), (torch.int16, 16), (torch.uint8, 8)):
+        for dt, nsub in ((torch.int64, 64), (torch.int32, 32), (torch.int16, 16), (torch.uint8, 8), (torch.int64, 37),
+                         (torch.uint8, 5)):
             mask = torch.zeros(npr, dtype=dt, device="cuda")
             seb.dev_probe_multi(kd, filters[:nsub], mask)
             torch.cuda.synchronize()
