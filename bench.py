@@ -58,7 +58,8 @@ GOLDEN_ROUTE_BEGIN = "0afec9b77141e0845ef7750736ed4667d1d1adf3df91c0ab47e85c0930
 GOLDEN_MANY = "18f390ebd4082f2282f8f6352c2e02f946e855b57078fcd4f21e81956050baa7"  # sha256 of the 64 C5 filter digests
 GOLDEN_WAL = "7d661e321c2804cebf541abd9c1a34463b70fe27fce3c5459a71408ac91b3e01"  # sha256(u32 CRCs), 2M records
 OPTIONS = ("build_algo", "multi_interleave", "multiget_order", "multiget_l0_group", "varlen_prehash_min_keys", "bucket_min_keys",
-           "lds_min_keys", "many_splits", "probe_phases", "probe_compact", "grid_cap", "workspace_limit_mib")
+           "lds_min_keys", "many_splits", "probe_phases", "probe_compact", "grid_cap", "workspace_limit_mib",
+           "cpu_fallback")
 
 
 def gather_ceiling():
@@ -88,8 +89,8 @@ def parse():
     ap.add_argument("--time-every", type=int, default=4,
                     help="record the build/probe launch timers on every Nth timed step (and the last)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "lsm", "lsm_wide", "route", "wal",
-                                                           "many", "c2_sharded", "c3_partitioned", "flush"])
+    ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "c5_2d", "lsm", "lsm_wide", "route",
+                                                           "wal", "many", "c2_sharded", "c3_partitioned", "flush"])
     ap.add_argument("--keys", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
@@ -105,9 +106,12 @@ def parse():
                          "its answers are not checked against the golden digest)")
     ap.add_argument("--bcast", default="packed", choices=["packed", "keys"],
                     help="c2c3/c5, N > 1: broadcast 8-B packed residues (hashed once on rank 0) or the 16-B keys")
-    ap.add_argument("--bcast-per-step", action="store_true",
-                    help="c2c3/c5, N > 1: broadcast a probe batch in every step (pipelined two steps ahead) "
-                         "instead of once before the timed steps")
+    ap.add_argument("--batch", default="step", choices=["step", "resident"],
+                    help="c2c3/c5, N > 1: 'step' (default, the headline) broadcasts a new probe batch from rank 0 "
+                         "in every timed step (pipelined two steps ahead); 'resident' broadcasts it once before "
+                         "the timed steps (measured as the line's resident_batch secondary as well)")
+    ap.add_argument("--c5-groups", type=int, default=None,
+                    help="c5_2d: key groups R (default: the world size, i.e. every GPU holds all 64 filters)")
     ap.add_argument("--overlap", type=int, default=0,
                     help="c2c3/c4: build step j+1 (second filter buffer, own stream) while step j probes")
     for o in OPTIONS:
@@ -132,6 +136,7 @@ class Setup:
     bcast_lead = 1        # batch j + lead is broadcast during step j (dist_probe.BroadcastPipeline)
     bcast_prologue = None # rank 0, before the loop: produce(b, buf) fills the buffer of batch b < lead
     pmc_key = None        # profiles/pmc_r01.json entry whose per-launch traffic applies (None: config name)
+    pipe = None           # a ready pipeline (c5_2d's dist_probe.GridPipeline) instead of a broadcast one
 
 
 def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
@@ -155,15 +160,15 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
     st.units_per_step = 2.0 * n * world
     # N > 1: every rank's filter has the same (m, k) (one SSTable size), so the batch travels as
     # 8-byte packed residues instead of 16-byte keys (80 MB over xGMI instead of 160 MB), hashed
-    # once on rank 0.  Default: the batch is RCCL-broadcast once, before the timed steps, and is
-    # resident on every GPU while they run, as it is on the one GPU at N = 1 (value counts inputs
-    # already in HBM); the broadcast is timed on its own (result["broadcast"]).  Rank 0 probes the
-    # keys, as at N = 1; the other ranks probe the packed words.  --bcast-per-step broadcasts a batch
-    # in every step instead: rank 0 produces batch j+2's packed words inside its own probe
-    # (seb_dev_probe_emit_packed) and broadcasts them right after.  Every rank tests all 10M keys
-    # against its own filter in every step.
+    # once on rank 0.  Default (--batch step, the headline): a new batch is RCCL-broadcast in every
+    # step, so the xGMI transfer is inside the timed region: rank 0 produces batch j+2's packed
+    # words inside its own probe of batch j (seb_dev_probe_emit_packed) and broadcasts them right
+    # after, on the communication stream, while the next step computes.  --batch resident
+    # broadcasts one batch before the timed steps and every rank probes it resident, as the one GPU
+    # does at N = 1 (the line's resident_batch secondary); rank 0 probes the keys, the others the
+    # packed words.  Every rank tests all 10M keys against its own filter in every step.
     packed = world > 1 and args.bcast == "packed" and k == 7 and m < (1 << 29)
-    per_step = world > 1 and args.bcast_per_step
+    per_step = world > 1 and args.batch == "step"
     st.workload = ("C2+C3: per GPU build one filter from 10M x 16B keys @1% FPR (m=95,850,584, k=7) "
                    + ("(a new filter: every word written by the build, no separate clear) " if args.fresh_build
                       else "(clear + build) ")
@@ -390,11 +395,12 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
     # N > 1: the 64 filters share (m, k), so the batch travels as 8-B packed residues (80 MB per step
     # instead of 160 MB of keys): rank 0 packs batch j+2 in step j (seb_dev_pack_residues) and every
     # rank probes the packed words of batch j (seb_dev_probe_multi_packed).
-    # Default at N > 1: the batch is broadcast once before the timed steps and resident on every
-    # GPU (as at N = 1); the planes are gathered to rank 0 in every step.  --bcast-per-step: a new
-    # batch broadcast in every step (pipelined two steps ahead).
+    # Default at N > 1 (--batch step): a new batch is broadcast in every step (pipelined two steps
+    # ahead), so the transfer is inside the timed region; --batch resident broadcasts it once before
+    # the timed steps (the resident_batch secondary).  The planes are gathered to rank 0 in every
+    # step either way.
     packed = world > 1 and args.bcast == "packed" and k == 7 and m < (1 << 29)
-    per_step = world > 1 and args.bcast_per_step
+    per_step = world > 1 and args.batch == "step"
     if packed and per_step:
         st.bcast_lead = 2
         st.packed = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(st.bcast_lead + 1)]
@@ -440,6 +446,85 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
         mask = dp.assemble_mask(st.planes if world > 1 else [st.plane], nf)
         ok = sha(mask.astype("<u8").tobytes()) == GOLDEN_C5
         return "bit-exact (sha256 of the 10M u64 masks matches tests/golden c5)" if ok else "MISMATCH masks"
+
+    st.probe, st.parity = probe, parity
+    return st
+
+
+def setup_c5_2d(args, seb, kg, torch, dev, rank, world, dist):
+    """C5 over a key x filter grid (dist_probe.KeyFilterGrid): the ranks form R key groups x
+    F = N / R filter slots (R = --c5-groups, default N: every GPU holds all 64 filters).  In every
+    step rank 0 packs a new 10M-key batch (8-B residues) and sends each key group only its 1/R of
+    it (RCCL point to point), each rank probes its shard against its 64/F filters, and the planes
+    come back to rank 0 in the same grouped exchange (the other direction of each link).  At N = 1
+    this is C5 itself.  Total work fixed as N grows: strong scaling; value = batch keys / s."""
+    import dist_probe as dp
+
+    st = Setup()
+    nf, per, n = 64, 100_000, args.keys
+    m, k = seb.params(per, 0.01)
+    st.m, st.k, st.n = m, k, n
+    groups = args.c5_groups or world
+    grid = dp.KeyFilterGrid(nf, rank, world, groups)
+    shard = grid.shard
+    fkeys = torch.from_numpy(kg.key16(shard.lo * per + np.arange(shard.count * per))).to(dev)
+    st.local = [(seb.new_words(m, device=dev), m, k) for _ in range(shard.count)]
+    if shard.count:
+        seb.dev_build_many(seb.dev_keys(fkeys, n=shard.count * per, stride=16),
+                           [j * per for j in range(shard.count + 1)], st.local)
+    torch.cuda.synchronize()
+    if rank == 0:
+        q = np.arange(n, dtype=np.int64)
+        half = q // 2
+        st.pbuf = torch.from_numpy(kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q))).to(dev)
+        st.pk = seb.dev_keys(st.pbuf, n=n, stride=16)
+    nb = (m + 7) // 8
+    st.units_per_step = float(n)
+    st.scaling = "strong"
+    st.workload = (f"C5 as a key x filter grid: 64 SSTable filters (100K keys each, m={m:,}, k={k}); {groups} key "
+                   f"group(s) x {world // groups} filter slot(s); a new 10M-key batch every step, rank 0 sends each "
+                   "group its key shard as 8-B packed residues (RCCL point to point) and gets the u64 mask planes "
+                   "back in the same exchange")
+    st.parallelism = f"key groups {groups} x filter slots {world // groups}"
+    if world == 1:
+        st.plane = torch.zeros(n, dtype=torch.int64, device=dev)
+        st.kernel_bytes = {"probe": 16.0 * n + nf * nb + 8.0 * n}
+
+        def probe(j, buf, target):
+            seb.dev_probe_multi(st.pk, st.local, st.plane)
+
+        def parity(j):
+            if n != 10_000_000:
+                return None
+            ok = sha(st.plane.cpu().numpy().astype("<i8").tobytes()) == GOLDEN_C5
+            return "bit-exact (sha256 of the 10M u64 masks matches tests/golden c5)" if ok else "MISMATCH masks"
+
+        st.probe, st.parity = probe, parity
+        return st
+    if not (k == 7 and m < (1 << 29)):
+        raise SystemExit("c5_2d at N > 1 sends packed residues: needs k == 7 and m < 2^29")
+    mode = "p2p" if args.dist_backend == "nccl" else "collective"  # gloo cannot send device tensors p2p
+    ex = dp.GridExchange(grid, n, (), torch.int64, dev, nbufs=3, mode=mode)
+    produce = (lambda b, buf: seb.dev_pack_residues(st.pk, m, k, buf[:n])) if rank == 0 else None
+    st.pipe = dp.GridPipeline(ex, lead=2, produce=produce)
+    cnt = ex.hi - ex.lo
+    st.kernel_bytes = {"probe": (24.0 * n if rank == 0 else 0.0) + 8.0 * cnt + shard.count * nb
+                       + ex.pdtype.itemsize * cnt}
+    st.parallelism += f", {mode} exchange"
+
+    def probe(j, buf, target):
+        if rank == 0:  # the broadcast root's packing pass: batch j + 2, sent at the end of this step
+            seb.dev_pack_residues(st.pk, m, k, target[:n])
+        plane = ex.plane(j)
+        if shard.count and buf.shape[0]:
+            seb.dev_probe_multi_packed(buf, buf.shape[0], st.local, plane)
+
+    def parity(j):
+        if n != 10_000_000 or rank != 0:
+            return None
+        ok = sha(ex.mask(j).cpu().numpy().astype("<i8").tobytes()) == GOLDEN_C5
+        return ("bit-exact (sha256 of the 10M u64 masks assembled on rank 0 matches tests/golden c5)" if ok
+                else "MISMATCH masks")
 
     st.probe, st.parity = probe, parity
     return st
@@ -725,6 +810,7 @@ def run_flush(args):
                                "then per-Get single-key MayContain on 1 and 8 threads (harness/flush_bench.c)",
                    "sizes": sizes, "threads": threads, "fpr": 0.01},
         "sizes": res["sizes"],
+        "cpu_fallbacks": res.get("cpu_fallbacks"),
     }
     if not args.no_cpu_baseline:
         from oracle import oracle_c as oc
@@ -806,10 +892,116 @@ def main():
         if v is not None:
             seb.set_option(o, v)
 
-    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "lsm": setup_lsm, "lsm_wide": setup_lsm,
-             "route": setup_route, "many": setup_many, "wal": setup_wal, "c2_sharded": setup_c2_sharded,
-             "c3_partitioned": setup_c3_partitioned}[args.config]
+    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "c5_2d": setup_c5_2d, "lsm": setup_lsm,
+             "lsm_wide": setup_lsm, "route": setup_route, "many": setup_many, "wal": setup_wal,
+             "c2_sharded": setup_c2_sharded, "c3_partitioned": setup_c3_partitioned}[args.config]
     st = setup(args, seb, kg, torch, dev, rank, world, dist)
+    run = timed_run(args, st, seb, torch, dist, world, rank, dev)
+    # Parity of the last timed step's outputs, checked after the timed region: a large pageable
+    # D2H (.cpu()) delays the next kernel launch by ~20 ms on this runtime (tools/dbg_sharded_timing.py),
+    # which must not land inside the timed steps.
+    torch.cuda.synchronize()
+    parity = st.parity(args.warmup + args.steps - 1)
+    elapsed, kern_ms, bcast, overlap = run["elapsed"], run["kern_ms"], run["bcast"], run["overlap"]
+    value = st.units_per_step * args.steps / elapsed / 1e6
+    resident = None
+    if world > 1 and args.config in ("c2c3", "c5") and args.batch == "step" and not args.no_secondary:
+        # the same job with the batch broadcast once and resident during the steps
+        import copy
+
+        a2 = copy.copy(args)
+        a2.batch = "resident"
+        st2 = setup(a2, seb, kg, torch, dev, rank, world, dist)
+        r2 = timed_run(a2, st2, seb, torch, dist, world, rank, dev)
+        torch.cuda.synchronize()
+        resident = {"value": round(st2.units_per_step * a2.steps / r2["elapsed"] / 1e6, 2), "unit": st2.unit,
+                    "ms_per_step": round(r2["elapsed"] * 1000.0 / a2.steps, 4),
+                    "kernel_ms": {k: round(v, 4) for k, v in r2["kern_ms"].items()},
+                    "parity": st2.parity(a2.warmup + a2.steps - 1), "broadcast": r2["bcast"],
+                    "note": "secondary: one batch RCCL-broadcast before the timed steps and probed resident in "
+                            "every step (its broadcast timed on its own); the headline value broadcasts a new "
+                            "batch inside every step"}
+    result = None
+    if rank == 0:
+        kern = {name: (ms, st.kernel_bytes[name]) for name, ms in kern_ms.items()}
+        dom = max(kern, key=lambda x: kern[x][0])
+        traffic = None  # PMC-measured HBM bytes of the dominant step (the newest round's profile that has it)
+        for pmc_path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")), reverse=True):
+            with open(pmc_path) as f:
+                traffic = json.load(f).get(st.pmc_key or args.config, {}).get(dom, {}).get("hbm_bytes_per_launch")
+            if traffic is not None:
+                break
+        ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
+        result = {
+            "metric": METRIC if args.config in ("c2c3", "c4", "c5", "c5_2d", "lsm", "lsm_wide", "c2_sharded",
+                                                "c3_partitioned")
+            else f"{args.config} {st.unit}",
+            "value": round(value, 2), "unit": st.unit, "n_gpus": world, "devices": min(world, ndev),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),
+            "higher_is_better": True, "scaling": st.scaling, "vs_baseline": None, "dtype": st.dtype,
+            "data": "synthetic (reference key format user%010d+2B, common/benchmark/keygen.go:89-109)",
+            "config": {"workload": st.workload, "keys_per_gpu": st.n, "fpr": 0.01, "num_bits": st.m,
+                       "num_hashes": st.k, "parallelism": st.parallelism},
+            **{f"{name}_gkeys_s": round(st.n / (ms * 1e-3) / 1e9, 3) for name, ms in kern_ms.items()},
+            **{f"{name}_ms": round(ms, 4) for name, ms in kern_ms.items()},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": int(kern[dom][1]),
+                         "time_source": "mean HIP-event launch time of the dominant call over the sampled "
+                                        "timed steps (launch_timers), on its launch stream; not the wall-clock step",
+                         "other": {d: {"ms": round(v[0], 4), "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 2)}
+                                   for d, v in kern.items()}},
+            "parity": parity,
+            **({"broadcast": bcast} if bcast else {}),
+            **({"resident_batch": resident} if resident else {}),
+            "launch_timers": f"HIP events (no system fence) around build and probe on every {args.time_every}th "
+                             "timed step and the last; ms_per_step is the wall clock of all steps",
+            "options": {**{o: seb.get_option(o) for o in OPTIONS}, "overlap": int(overlap)},
+            "cpu_fallbacks": seb.fallback_count(),
+        }
+        if args.config == "c2c3":
+            # SURVEY.md 8(d)'s secondary sector model: every bit touch one 64-B DRAM transaction (no
+            # early exit), the build also writing each touched sector back.  Most touches are L2 hits
+            # here (phased probe, bucketed build), so these rates exceed the HBM peak and are not a
+            # fraction of it (DESIGN.md 6); the probe's bound is the gather model below.
+            spk = {"build": 16 + 2 * 64 * st.k, "probe": 16 + 64 * st.k}
+            result["roofline"]["sector_model"] = {
+                "S": 64, "bytes_per_key": spk,
+                "GB/s": {d: round(st.n * spk[d] / (kern_ms[d] * 1e-3) / 1e9, 1) for d in spk if d in kern_ms},
+                "note": "modelled bytes, most of them L2 hits; not comparable to the HBM peak"}
+        if args.config in ("c2c3", "lsm", "lsm_wide"):
+            # The probe's real bound (DESIGN 5.3, 5.7): filter-word gathers, counted offline per
+            # call with the oracle (tools/gather_count.py, tools/gather_count_lsm.py), against the
+            # measured L2-resident ceiling.
+            gpath = os.path.join(ROOT, "profiles", "gathers_c2c3.json")
+            ceil, csrc = gather_ceiling()
+            if world == 1 and "probe" in kern_ms and ceil and os.path.exists(gpath) and args.lsm_order == "batch":
+                with open(gpath) as f:
+                    gc = json.load(f).get(args.config, {}).get("probe")
+                if gc and gc["n"] == st.n:
+                    cnt = gc.get("gathers_phased", gc.get("gathers"))
+                    rate = cnt / (kern_ms["probe"] * 1e-3) / 1e9
+                    result["roofline"]["gather_model"] = {
+                        "gathers_per_call": cnt, "Ggathers_s": round(rate, 1),
+                        "ceiling_Ggathers_s": ceil, "frac": round(rate / ceil, 3),
+                        "count_source": "profiles/gathers_c2c3.json", "ceiling_source": csrc}
+        if world == 1 and args.config == "c2c3" and not args.no_host_inclusive:
+            result["host_inclusive"] = host_inclusive(seb, st.build_host, st.probe_host, st.m, st.k)
+        if world == 1 and not args.no_cpu_baseline and args.config in ("c2c3", "c4"):
+            result["cpu_baseline"] = cpu_baseline(args, st.n, st.m, st.k)
+        if world == 1 and args.config == "c2c3" and not args.no_secondary:
+            result["secondary"] = secondary_lines()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if result is not None:
+        print(json.dumps(result), flush=True)
+
+
+def timed_run(args, st, seb, torch, dist, world, rank, dev):
+    """W untimed warm-up steps, then exactly K timed steps between a barrier + synchronize on
+    both sides; the max over ranks of the wall time, the sampled launch durations and (a resident
+    batch at N > 1) the batch's broadcast timed on its own."""
     torch.cuda.synchronize()
     overlap = bool(args.overlap) and st.build is not None
     sp = torch.cuda.current_stream()                          # probe (and broadcast) stream
@@ -822,8 +1014,8 @@ def main():
     # probes them on torch's nccl stream, so the xGMI transfer overlaps compute; a rank's probe of
     # batch j waits on the GPU (a stream wait, not the host) for that broadcast
     # (dist_probe.BroadcastPipeline; its ordering is tested on CPU in tests/test_dist.py).
-    pipe = None
-    if st.broadcast_bufs is not None:
+    pipe = st.pipe
+    if pipe is None and st.broadcast_bufs is not None:
         import dist_probe as dp
 
         pipe = dp.BroadcastPipeline(st.broadcast_bufs, st.bcast_lead, rank, produce=st.bcast_prologue)
@@ -844,7 +1036,7 @@ def main():
         return t
 
     def step(j, record):
-        if pipe is not None:
+        if pipe is not None and hasattr(pipe, "begin_step"):
             pipe.begin_step(j)
         b_end = None
         if st.build is not None:
@@ -890,13 +1082,13 @@ def main():
         # launch durations are sampled on every --time-every'th step (and the last): each timer
         # record costs ~4.7 us of command-processor time between two kernels
         step(j, (j - args.warmup) % args.time_every == 0 or j == args.warmup + args.steps - 1)
+    if pipe is not None:  # the last steps' transfers (planes back to rank 0, the next batches) are in the time
+        pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if pipe is not None:
-        pipe.drain()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -921,83 +1113,7 @@ def main():
         bcast = {"bytes": int(nbytes), "ms": round(float(t.item()) * 1e3, 4),
                  "GB/s": round(nbytes / float(t.item()) / 1e9, 2), "backend": args.dist_backend,
                  "note": "RCCL broadcast of the probe batch from rank 0, once per batch, outside the timed steps"}
-    # Parity of the last timed step's outputs, checked after the timed region: a large pageable
-    # D2H (.cpu()) delays the next kernel launch by ~20 ms on this runtime (tools/dbg_sharded_timing.py),
-    # which must not land inside the timed steps.
-    torch.cuda.synchronize()
-    parity = st.parity(args.warmup + args.steps - 1)
-    value = st.units_per_step * args.steps / elapsed / 1e6
-    result = None
-    if rank == 0:
-        kern = {name: (ms, st.kernel_bytes[name]) for name, ms in kern_ms.items()}
-        dom = max(kern, key=lambda x: kern[x][0])
-        traffic = None  # PMC-measured HBM bytes of the dominant step (the newest round's profile that has it)
-        for pmc_path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")), reverse=True):
-            with open(pmc_path) as f:
-                traffic = json.load(f).get(st.pmc_key or args.config, {}).get(dom, {}).get("hbm_bytes_per_launch")
-            if traffic is not None:
-                break
-        ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
-        result = {
-            "metric": METRIC if args.config in ("c2c3", "c4", "c5", "lsm", "lsm_wide", "c2_sharded",
-                                                             "c3_partitioned")
-            else f"{args.config} {st.unit}",
-            "value": round(value, 2), "unit": st.unit, "n_gpus": world, "devices": min(world, ndev),
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),
-            "higher_is_better": True, "scaling": st.scaling, "vs_baseline": None, "dtype": st.dtype,
-            "data": "synthetic (reference key format user%010d+2B, common/benchmark/keygen.go:89-109)",
-            "config": {"workload": st.workload, "keys_per_gpu": st.n, "fpr": 0.01, "num_bits": st.m,
-                       "num_hashes": st.k, "parallelism": st.parallelism},
-            **{f"{name}_gkeys_s": round(st.n / (ms * 1e-3) / 1e9, 3) for name, ms in kern_ms.items()},
-            **{f"{name}_ms": round(ms, 4) for name, ms in kern_ms.items()},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": int(kern[dom][1]),
-                         "other": {d: {"ms": round(v[0], 4), "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 2)}
-                                   for d, v in kern.items()}},
-            "parity": parity,
-            **({"broadcast": bcast} if bcast else {}),
-            "launch_timers": f"HIP events (no system fence) around build and probe on every {args.time_every}th "
-                             "timed step and the last; ms_per_step is the wall clock of all steps",
-            "options": {**{o: seb.get_option(o) for o in OPTIONS}, "overlap": int(overlap)},
-        }
-        if args.config == "c2c3":
-            # SURVEY.md 8(d)'s secondary sector model: every bit touch one 64-B DRAM transaction (no
-            # early exit), the build also writing each touched sector back.  Most touches are L2 hits
-            # here (phased probe, bucketed build), so these rates exceed the HBM peak and are not a
-            # fraction of it (DESIGN.md 6); the probe's bound is the gather model below.
-            spk = {"build": 16 + 2 * 64 * st.k, "probe": 16 + 64 * st.k}
-            result["roofline"]["sector_model"] = {
-                "S": 64, "bytes_per_key": spk,
-                "GB/s": {d: round(st.n * spk[d] / (kern_ms[d] * 1e-3) / 1e9, 1) for d in spk if d in kern_ms},
-                "note": "modelled bytes, most of them L2 hits; not comparable to the HBM peak"}
-        if args.config in ("c2c3", "lsm", "lsm_wide"):
-            # The probe's real bound (DESIGN 5.3, 5.7): filter-word gathers, counted offline per
-            # call with the oracle (tools/gather_count.py, tools/gather_count_lsm.py), against the
-            # measured L2-resident ceiling.
-            gpath = os.path.join(ROOT, "profiles", "gathers_c2c3.json")
-            ceil, csrc = gather_ceiling()
-            if world == 1 and "probe" in kern_ms and ceil and os.path.exists(gpath) and args.lsm_order == "batch":
-                with open(gpath) as f:
-                    gc = json.load(f).get(args.config, {}).get("probe")
-                if gc and gc["n"] == st.n:
-                    cnt = gc.get("gathers_phased", gc.get("gathers"))
-                    rate = cnt / (kern_ms["probe"] * 1e-3) / 1e9
-                    result["roofline"]["gather_model"] = {
-                        "gathers_per_call": cnt, "Ggathers_s": round(rate, 1),
-                        "ceiling_Ggathers_s": ceil, "frac": round(rate / ceil, 3),
-                        "count_source": "profiles/gathers_c2c3.json", "ceiling_source": csrc}
-        if world == 1 and args.config == "c2c3" and not args.no_host_inclusive:
-            result["host_inclusive"] = host_inclusive(seb, st.build_host, st.probe_host, st.m, st.k)
-        if world == 1 and not args.no_cpu_baseline and args.config in ("c2c3", "c4"):
-            result["cpu_baseline"] = cpu_baseline(args, st.n, st.m, st.k)
-        if world == 1 and args.config == "c2c3" and not args.no_secondary:
-            result["secondary"] = secondary_lines()
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    if result is not None:
-        print(json.dumps(result), flush=True)
+    return {"elapsed": elapsed, "kern_ms": kern_ms, "bcast": bcast, "overlap": overlap}
 
 
 SECONDARY = (("c4", ["--steps", "10", "--warmup", "3", "--no-cpu-baseline"]),

@@ -14,7 +14,11 @@
  *
  * Errors: every int-returning function returns SEB_OK (0) or a negative SEB_ERR_* code, and
  * seb_last_error() gives a thread-local message.  The reference has no error returns (bad input
- * panics or yields nil); the Go shim turns a negative code into the same panic.
+ * panics or yields nil); the Go shim turns a negative code into the same panic.  The Go API
+ * mirror (seb_filter_*) does not fail for want of a device: a build or batched probe whose device
+ * path returns SEB_ERR_DEVICE / SEB_ERR_NOMEM is done on the filter's host copy instead (option
+ * "cpu_fallback", default on), counted by seb_fallback_count().  Every other entry point
+ * (device-resident, host-buffer, registry) reports the error.
  */
 #ifndef SEB_BLOOM_H
 #define SEB_BLOOM_H
@@ -73,6 +77,10 @@ int seb_abi_version(void);
 /* Process-wide tuning knobs (results never change, only speed):
  *   "build_algo"      0 auto, 1 device-scope atomic OR, 2 radix-partitioned LDS build, 3 the whole
  *                     filter in one CU's LDS (word array <= 160 KiB), keys split over workgroups
+ *                     (atomic merge), 4 LDS images of the whole filter + an OR kernel (<= 160 KiB)
+ *                     Auto: 4 from lds_min_keys keys while the word array fits 160 KiB (3 when
+ *                     the words are not 16-B aligned), 2 from bucket_min_keys keys for larger
+ *                     filters, 1 below those
  *   "bucket_min_keys" auto build_algo: radix-partitioned from this many keys on
  *   "lds_min_keys"    auto build_algo: LDS-resident filter (<= 160 KiB) from this many keys on
  *   "many_splits"     batched small-filter build: workgroups per filter (0 = auto)
@@ -87,8 +95,12 @@ int seb_abi_version(void);
  *                     bit-interleaved table, one gather per position for all of them (1, default)
  *   "varlen_prehash_min_keys"  variable-length batches of this many keys are pre-hashed in LDS
  *   "grid_cap"        maximum workgroups of the grid-stride kernels
- *   "workspace_limit_mib"  cap on library scratch (0 = none); a request above it fails with
- *                     SEB_ERR_NOMEM (MultiGet's key-range order then falls back to batch order)
+ *   "workspace_limit_mib"  cap on library scratch and a context's build scratch (0 = none); a
+ *                     request above it fails with SEB_ERR_NOMEM (MultiGet's key-range order then
+ *                     falls back to batch order; the Go API mirror's build to its CPU fallback)
+ *   "cpu_fallback"    Go API mirror: on a device failure build / probe on the host copy (1, default)
+ *                     or return the error (0)
+ *   "fault_inject"    test only: the Go API mirror's device path fails with SEB_ERR_DEVICE (0/1)
  * Environment variables SEB_<NAME> (upper case) set the initial values. */
 int seb_set_option(const char *name, int64_t value);
 int seb_get_option(const char *name, int64_t *value);
@@ -104,8 +116,10 @@ int seb_dev_clear(uint32_t *words, uint64_t num_bits, void *stream);
 int seb_dev_build(const seb_keys *keys, uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
                   void *stream);
 /* A new filter from `keys` (NewBloomFilter + Add per key): `words` (seb_words_bytes) need not be
- * cleared; every word is written.  The radix-partitioned build writes them whole instead of
- * clearing and OR-ing; other build paths clear first. */
+ * cleared; every word is written.  The radix-partitioned build and the LDS image build write them
+ * whole instead of clearing and OR-ing; other build paths clear first.  Device builds take word
+ * arrays aligned to 4 B; 16-B aligned ones (any hipMalloc / torch allocation) take the 16-B
+ * clear and the image build, others hipMemsetAsync and the LDS-filter build. */
 int seb_dev_build_fresh(const seb_keys *keys, uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
                         void *stream);
 /* Same, with caller-owned scratch (graph-capture friendly: no allocation inside the call).
@@ -221,6 +235,9 @@ uint64_t seb_filter_num_bits(const seb_filter *f);
 uint32_t seb_filter_num_hashes(const seb_filter *f);
 uint64_t seb_filter_pending(seb_filter *f);
 int seb_filter_flush(seb_filter *f);
+/* How many Go-API-mirror builds / batched probes ran on the host copy because the device path
+ * failed (the "cpu_fallback" option); 0 on a healthy GPU. */
+uint64_t seb_fallback_count(void);
 
 /* ------------------ device-resident filter registry + batched LSM lookup ---- */
 /* One registry per LSM instance.  seb_registry_put decodes an SSTable's bloom block (the bytes

@@ -139,6 +139,8 @@ static const OptionDesc kOptions[] = {
     SEB_OPT(probe_compact, 0, 1),
     SEB_OPT(grid_cap, 1, 1 << 30),
     SEB_OPT(workspace_limit_mib, 0, 1 << 30),
+    SEB_OPT(cpu_fallback, 0, 1),
+    SEB_OPT(fault_inject, 0, 1),
 };
 #undef SEB_OPT
 
@@ -418,14 +420,22 @@ static bool want_prehash_packed(const KeyBatch &kb, const ModArg &md) {
 template <typename Grow>
 static int build_dispatch(KeyBatch kb, uint32_t *words, const ModArg &md, hipStream_t s, void *ws, uint64_t ws_bytes,
                           Grow &&grow, bool fresh = false, uint32_t *ovf = nullptr) {
+    // The clear kernel and the image build's OR kernel store 16 B per lane: word arrays that are
+    // only 4-B aligned are cleared by hipMemsetAsync and built by the LDS-filter build instead.
+    const bool a16 = ((uintptr_t)words & 15) == 0;
+    auto clear = [&]() -> hipError_t {
+        return a16 ? launch_clear_words(words, seb_words_bytes(md.m), s)
+                   : hipMemsetAsync(words, 0, seb_words_bytes(md.m), s);
+    };
     if (kb.n == 0 || md.k == 0) {
-        if (fresh) HIP_OR_FAIL(launch_clear_words(words, seb_words_bytes(md.m), s));
+        if (fresh) HIP_OR_FAIL(clear());
         return SEB_OK;
     }
-    const int algo = choose_build_algo(kb.n, md.m, md.k);
+    int algo = choose_build_algo(kb.n, md.m, md.k);
+    if (algo == 4 && !a16) algo = 3;
     const bool bucketed = algo == 2;
     if (!(fresh && bucketed)) ovf = nullptr;
-    if (fresh && algo != 4 && !ovf) HIP_OR_FAIL(launch_clear_words(words, seb_words_bytes(md.m), s));
+    if (fresh && algo != 4 && !ovf) HIP_OR_FAIL(clear());
     if (bucketed && want_prehash_packed(kb, md)) {  // scratch: [packed residues | bucketed]
         const uint64_t pack_b = (kb.n * 8 + 255) & ~255ull;
         const uint64_t need = pack_b + bucketed_workspace_bytes(kb.n, md.m, md.k);
@@ -860,8 +870,13 @@ extern "C" int seb_timer_destroy(void *ev) {
 struct DevBuf {
     void *p = nullptr;
     uint64_t cap = 0;
-    int reserve(uint64_t bytes) {
+    // limited: scratch that workspace_limit_mib caps (a context's build scratch)
+    int reserve(uint64_t bytes, bool limited = false) {
         if (bytes <= cap) return SEB_OK;
+        const uint64_t lim = options().workspace_limit_mib;
+        if (limited && lim && bytes > (lim << 20))
+            return fail(SEB_ERR_NOMEM, "workspace %llu B > workspace_limit_mib %llu", (unsigned long long)bytes,
+                        (unsigned long long)lim);
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
@@ -1047,7 +1062,7 @@ static int build_device_from_host(seb_ctx *c, const seb_keys *kb, uint32_t *dwor
         if (rc) return rc;
         rc = build_dispatch(dk, dwords, md, c->s_comp, c->ws.p, c->ws.cap, [&](uint64_t need, void **out) -> int {
             HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));  // previous chunks may still use it
-            int r = c->ws.reserve(need);
+            int r = c->ws.reserve(need, true);
             *out = c->ws.p;
             return r;
         }, fresh && j == 0);
@@ -1201,6 +1216,12 @@ struct CtxLease {  // borrow a context from the process pool (concurrent filters
     }
 };
 
+static inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
+}
+
 // A lock for the filter handle: one atomic exchange to take it uncontended (Add takes it once per
 // key, so a pthread mutex's call + fence pair showed in the per-key cost), a bounded spin, then
 // yields (a waiter may be waiting on a GPU build that takes milliseconds).
@@ -1210,7 +1231,7 @@ struct FilterLock {
         for (int spin = 0; held.exchange(true, std::memory_order_acquire); ++spin) {
             while (held.load(std::memory_order_relaxed)) {
                 if (++spin > 64) std::this_thread::yield();
-                else __builtin_ia32_pause();
+                else cpu_relax();
             }
         }
     }
@@ -1385,7 +1406,11 @@ static int usable(seb_filter *f, const char *who) {
 }
 
 // OR host keys into the filter's device words on a pooled context; returns when the build is done.
-static int build_into_filter(seb_filter *f, const seb_keys *kb) {
+// `fresh`: the filter is a New with nothing built, and its device words are taken without a clear
+// (the build writes them whole or clears them itself); host_zero stays set until the build
+// succeeded (build_into_filter drops such a device copy on failure, so a retry starts clean).
+static int build_into_filter_device(seb_filter *f, const seb_keys *kb, bool fresh) {
+    if (options().fault_inject) return fail(SEB_ERR_DEVICE, "BloomFilter build: injected device fault (fault_inject)");
     CtxLease L(f->device);
     if (L.rc) return L.rc;
     std::lock_guard<std::mutex> g(L.c->mu);
@@ -1393,10 +1418,8 @@ static int build_into_filter(seb_filter *f, const seb_keys *kb) {
     int rc;
     // a new filter's first build writes its words whole (image build) or clears them first: no
     // separate memset of the device copy
-    const bool fresh = f->host_zero && !f->dwords;
     if ((rc = ensure_device_copy(f, L.c->s_comp, !fresh))) return rc;
     f->host_ok = false;  // the device copy is about to move ahead of the host copy
-    f->host_zero = false;
     f->readable.store(false, std::memory_order_relaxed);
     // Small builds skip the DMA engine, whose copies started ~8 us (keys in) and ~16 us (bits out)
     // after the work before them ended (profiles/r03_flush_trace.txt).  Keys: a device-scope-atomic
@@ -1426,7 +1449,7 @@ static int build_into_filter(seb_filter *f, const seb_keys *kb) {
         rc = build_dispatch(dk, f->dwords, md, c->s_comp, c->ws.p, c->ws.cap,
                             [&](uint64_t need, void **out) -> int {
                                 HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));
-                                int r = c->ws.reserve(need);
+                                int r = c->ws.reserve(need, true);
                                 *out = c->ws.p;
                                 return r;
                             }, fresh);
@@ -1445,6 +1468,96 @@ static int build_into_filter(seb_filter *f, const seb_keys *kb) {
     HIP_OR_FAIL(hipStreamSynchronize(c->s_comp));
     if (zc_bits && f->nbytes) memcpy(f->host.data(), c->hbits.p, f->nbytes);
     f->host_ok = mirror;
+    f->host_zero = false;
+    return SEB_OK;
+}
+
+// The boundary's CPU fallback (SURVEY.md 8(b) error row): the Go API has no error returns
+// (lsm/bloom.go:19-41,70-77,96-102 never fail on valid input), so a build or batched probe whose
+// device path fails for want of a device or of memory is done on the filter's host copy instead,
+// with the same arithmetic as host_may_contain.  Every use is counted (seb_fallback_count); the
+// GPU tests and smoke() assert that the count stays 0, so the parity they show is the HIP path's.
+static std::atomic<uint64_t> g_fallbacks{0};
+
+extern "C" uint64_t seb_fallback_count(void) { return g_fallbacks.load(std::memory_order_relaxed); }
+
+static bool device_failure(int rc) { return rc == SEB_ERR_DEVICE || rc == SEB_ERR_NOMEM; }
+
+// lsm/bloom.go:70-77 for one key on the host copy: positions stepped as in host_may_contain
+// ((h1 + i*h2) mod m with u64 wraparound, :58-67), LSB-first byte ORs (:73-75).
+static void host_add_key(seb_filter *f, const uint8_t *key, uint64_t len) {
+    uint8_t *bits = f->host.data();
+    const uint64_t m = f->m, c = f->c_m;
+    const uint32_t k = f->k;
+    uint64_t h1 = 0xcbf29ce484222325ull, h2 = 0xcbf29ce484222325ull;
+    const uint64_t P = 0x100000001b3ull;
+    for (uint64_t i = 0; i < len; ++i) {
+        h1 = (h1 ^ key[i]) * P;
+        h2 = (h2 * P) ^ key[i];
+    }
+    uint64_t r = host_mod(h1, m, f->mu_m);
+    const uint64_t b = host_mod(h2, m, f->mu_m);
+    uint64_t s = h1;
+    for (uint32_t i = 0; i < k; ++i) {
+        bits[r >> 3] |= (uint8_t)(1u << (r & 7));
+        const uint64_t s2 = s + h2;
+        const bool wrap = s2 < s;
+        s = s2;
+        uint64_t t = r + b;
+        if (t < r || t >= m) t -= m;
+        if (wrap) t = t >= c ? t - c : t + (m - c);
+        r = t;
+    }
+}
+
+static const uint8_t *host_key(const seb_keys *kb, uint64_t i, uint64_t *len) {
+    if (kb->offsets) {
+        *len = kb->offsets[i + 1] - kb->offsets[i];
+        return kb->data + kb->offsets[i];
+    }
+    *len = kb->stride;
+    return kb->data + i * (uint64_t)kb->stride;
+}
+
+// Give the device word array back (after its stream work ended): a copy that is garbage (a fresh
+// build that failed) or stale (the host copy moved ahead in a fallback).  The next device use
+// uploads the host copy again (ensure_device_copy).
+static void drop_device_copy(seb_filter *f) {
+    if (!f->dwords) return;
+    (void)hipSetDevice(f->device);
+    (void)hipDeviceSynchronize();  // nothing queued may still write the buffer the pool hands out next
+    if (!g_words_pool.give(f->device, f->dwords, f->dbytes)) (void)hipFree(f->dwords);
+    (void)hipGetLastError();
+    f->dwords = nullptr;
+    f->dbytes = 0;
+}
+
+static int build_into_filter(seb_filter *f, const seb_keys *kb) {
+    const bool fresh = f->host_zero && !f->dwords;
+    const bool host_was_ok = f->host_ok;
+    int rc = build_into_filter_device(f, kb, fresh);
+    if (rc == SEB_OK) return SEB_OK;
+    if (fresh) {  // its device words were never cleared: back to a New's state, so a retry starts from zeros
+        drop_device_copy(f);
+        if (f->nbytes) memset(f->host.data(), 0, f->nbytes);
+        f->host_ok = true;
+    }
+    // Otherwise the device copy (authoritative while host_ok is false) holds the old bits ORed with
+    // part of this batch at most, and the batch stays pending: a retry ORs it whole.
+    if (!device_failure(rc) || !options().cpu_fallback || !(fresh || host_was_ok) || f->nbytes < seb_num_bytes(f->m))
+        return rc;  // no usable host copy to fall back on (a large filter whose device copy is ahead)
+    // The host copy holds the bits before this build, or (a D2H that ran before the failure) those
+    // ORed with some of this batch's: OR-ing the whole batch into it gives the right filter.
+    for (uint64_t i = 0; i < kb->n; ++i) {
+        uint64_t len;
+        const uint8_t *key = host_key(kb, i, &len);
+        host_add_key(f, key, len);
+    }
+    drop_device_copy(f);
+    f->host_ok = true;
+    f->host_zero = false;
+    g_fallbacks.fetch_add(1, std::memory_order_relaxed);
+    (void)hipGetLastError();
     return SEB_OK;
 }
 
@@ -1546,6 +1659,17 @@ extern "C" int seb_filter_add_batch(seb_filter *f, const seb_keys *kb) {
     return SEB_OK;
 }
 
+static int probe_filter_device(seb_filter *f, const seb_keys *kb, uint8_t *out) {
+    if (options().fault_inject) return fail(SEB_ERR_DEVICE, "BloomFilter probe: injected device fault (fault_inject)");
+    CtxLease L(f->device);
+    if (L.rc) return L.rc;
+    std::lock_guard<std::mutex> g2(L.c->mu);
+    HIP_OR_FAIL(hipSetDevice(f->device));
+    int rc;
+    if ((rc = ensure_device_copy(f, L.c->s_comp))) return rc;
+    return probe_device_to_host(L.c, kb, f->dwords, mod_arg(f->m, f->k), out);
+}
+
 extern "C" int seb_filter_may_contain_batch(seb_filter *f, const seb_keys *kb, uint8_t *out) {
     WsCall ws_call;
     if (!f) return fail(SEB_ERR_INVALID, "BloomFilter.MayContain: null filter");
@@ -1556,12 +1680,16 @@ extern "C" int seb_filter_may_contain_batch(seb_filter *f, const seb_keys *kb, u
     FilterGuard g(f->mu);
     if ((rc = usable(f, "BloomFilter.MayContain"))) return rc;
     if ((rc = flush_locked(f))) return rc;
-    CtxLease L(f->device);
-    if (L.rc) return L.rc;
-    std::lock_guard<std::mutex> g2(L.c->mu);
-    HIP_OR_FAIL(hipSetDevice(f->device));
-    if ((rc = ensure_device_copy(f, L.c->s_comp))) return rc;
-    return probe_device_to_host(L.c, kb, f->dwords, mod_arg(f->m, f->k), out);
+    rc = probe_filter_device(f, kb, out);
+    if (rc == SEB_OK || !device_failure(rc) || !options().cpu_fallback || !f->host_ok) return rc;
+    for (uint64_t i = 0; i < kb->n; ++i) {  // the boundary's CPU fallback (see build_into_filter)
+        uint64_t len;
+        const uint8_t *key = host_key(kb, i, &len);
+        out[i] = (uint8_t)host_may_contain(f, key, len);
+    }
+    g_fallbacks.fetch_add(1, std::memory_order_relaxed);
+    (void)hipGetLastError();
+    return SEB_OK;
 }
 
 static int sync_host_locked(seb_filter *f);

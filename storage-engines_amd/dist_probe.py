@@ -15,6 +15,13 @@ every SSTable filter of the node at once (BASELINE config C5):
 Filters are independent, so the data path has exactly one collective in (broadcast) and one
 out (gather of answers); there is no reduction.  The compute function is injected so the same
 orchestration runs on the GPU (libseb_bloom, nccl) and in CPU tests (the oracle, gloo).
+
+That split (the north star's) makes every GPU test every key, so its probe does not shrink as
+GPUs are added, and the whole batch crosses xGMI into every rank.  `KeyFilterGrid` is the 2-D
+alternative (bench.py --config c5_2d): the ranks form R key groups x F filter slots; the root
+sends each group only its 1/R of the batch, each rank probes that shard against its 64/F filters,
+and the planes come back to the root.  With R = world every GPU holds all 64 filters (7.7 MB) and
+tests 1/world of the keys; the root's links carry 1/world of the batch each way.
 """
 from __future__ import annotations
 
@@ -193,3 +200,253 @@ class BroadcastPipeline:
         for b in sorted(self.handles):
             self._wait(b)
 
+
+
+# ------------------------------------------------ C5 as a key x filter grid (--config c5_2d) ----
+
+@dataclass(frozen=True)
+class KeyFilterGrid:
+    """`world` ranks as `groups` key groups x F = world / groups filter slots.
+
+    Rank r is in key group r // F and filter slot r % F.  Key group g owns the contiguous batch
+    shard key_bounds(n, g); filter slot s holds filters FilterShard(num_filters, s, F).  The batch
+    lives on rank 0 (the root, group 0, slot 0)."""
+
+    num_filters: int
+    rank: int
+    world: int
+    groups: int
+
+    def __post_init__(self):
+        if self.groups < 1 or self.world % self.groups:
+            raise ValueError(f"{self.groups} key groups do not divide {self.world} ranks")
+
+    @property
+    def slots(self) -> int:
+        return self.world // self.groups
+
+    def group_of(self, r: int) -> int:
+        return r // self.slots
+
+    def slot_of(self, r: int) -> int:
+        return r % self.slots
+
+    @property
+    def group(self) -> int:
+        return self.group_of(self.rank)
+
+    @property
+    def shard(self) -> FilterShard:
+        """This rank's filters."""
+        return FilterShard(self.num_filters, self.slot_of(self.rank), self.slots)
+
+    def key_bounds(self, n: int, g: int) -> tuple[int, int]:
+        return n * g // self.groups, n * (g + 1) // self.groups
+
+    def width(self, n: int) -> int:
+        """Rows of the largest key shard (every shard fits a buffer of this many rows)."""
+        return -(-n // self.groups)
+
+    def filter_lo(self, r: int) -> int:
+        return FilterShard.bounds(self.num_filters, self.slots, self.slot_of(r))[0]
+
+    def filter_count(self, r: int) -> int:
+        lo, hi = FilterShard.bounds(self.num_filters, self.slots, self.slot_of(r))
+        return hi - lo
+
+
+class GridExchange:
+    """Buffers and the per-batch exchange of the key x filter grid on one rank.
+
+    Per batch: the root sends key group g's shard to every rank of group g, every rank probes its
+    shard against its filters into a plane, and the planes go back to the root, which holds the
+    batch's u64 masks (bit f = filter f) in `mask`.
+
+    Two transports, the same data:
+      * "p2p" (RCCL): one grouped batch_isend_irecv per step holding both directions, so the
+        root's outgoing shards (of a later batch) and its incoming planes use the two directions of
+        each xGMI link at once.  The root receives a one-slot-per-key (F = 1) plane straight into
+        its slice of `mask`.
+      * "collective": dist.scatter + dist.gather of equal-width pieces (gloo, which cannot move
+        device tensors point to point; the one-GPU rehearsals and CPU tests).
+    The root's batch buffers carry `groups` spare rows, so every shard is a view of `width` rows
+    (the collective path's equal pieces; receivers ignore the rows past their shard)."""
+
+    def __init__(self, grid: KeyFilterGrid, n: int, row_shape: tuple, dtype, device, nbufs: int = 1,
+                 mode: str = "p2p", group=None):
+        if mode not in ("p2p", "collective"):
+            raise ValueError(mode)
+        self.grid, self.n, self.mode, self.group = grid, n, mode, group
+        self.rank, self.world = grid.rank, grid.world
+        self.lo, self.hi = grid.key_bounds(n, grid.group)
+        self.width = grid.width(n)
+        self.pdtype = grid.shard.plane_dtype()
+        rows = n + grid.groups if self.rank == 0 else self.width
+        self.bufs = [torch.zeros((rows, *row_shape), dtype=dtype, device=device) for _ in range(nbufs)]
+        self.direct = mode == "p2p" and grid.slots == 1 and self.pdtype == torch.int64
+        self.masks = ([torch.zeros(max(n, 1), dtype=torch.int64, device=device) for _ in range(2)]
+                      if self.rank == 0 else None)
+        own_plane = not (self.rank == 0 and self.direct)
+        self.planes = ([torch.zeros(self.width, dtype=self.pdtype, device=device) for _ in range(2)]
+                       if own_plane else None)
+        self.recv = ([[torch.zeros(self.width, dtype=self.pdtype, device=device) for _ in range(self.world)]
+                      for _ in range(2)] if self.rank == 0 and not self.direct else None)
+
+    # ---------------------------------------------------------------- views of one batch ----
+    def shard_view(self, buf: torch.Tensor) -> torch.Tensor:
+        """This rank's keys of the batch in `buf` (root: its own shard of the whole batch)."""
+        if self.rank == 0:
+            return buf[self.lo: self.hi]
+        return buf[: self.hi - self.lo]
+
+    def plane(self, j: int) -> torch.Tensor:
+        """Where this rank's probe of step j writes its plane (hi - lo keys)."""
+        if self.planes is None:  # the root, one filter slot: straight into its mask slice
+            return self.masks[j % 2][self.lo: self.hi]
+        return self.planes[j % 2][: self.hi - self.lo]
+
+    def mask(self, j: int) -> torch.Tensor:
+        return self.masks[j % 2][: self.n]
+
+    # ----------------------------------------------------------------------- exchange ----
+    def _pieces(self, buf: torch.Tensor) -> list:
+        out = []
+        for r in range(self.world):
+            lo, _ = self.grid.key_bounds(self.n, self.grid.group_of(r))
+            out.append(buf[lo: lo + self.width])
+        return out
+
+    def exchange(self, send_buf: torch.Tensor | None, recv_buf: torch.Tensor | None, plane_step: int | None) -> list:
+        """Issue one step's transfers, asynchronously: the shards of the batch in `send_buf` (root)
+        into `recv_buf` (other ranks), and (plane_step not None) the planes of that step to the
+        root.  Returns the works to wait on."""
+        works = []
+        if self.mode == "p2p":
+            ops = []
+            if send_buf is not None or recv_buf is not None:
+                if self.rank == 0:
+                    for r in range(1, self.world):
+                        lo, hi = self.grid.key_bounds(self.n, self.grid.group_of(r))
+                        if hi > lo:
+                            ops.append(dist.P2POp(dist.isend, send_buf[lo:hi], r, group=self.group))
+                elif self.hi > self.lo:
+                    ops.append(dist.P2POp(dist.irecv, recv_buf[: self.hi - self.lo], 0, group=self.group))
+            if plane_step is not None:
+                if self.rank == 0:
+                    for r in range(1, self.world):
+                        lo, hi = self.grid.key_bounds(self.n, self.grid.group_of(r))
+                        if hi > lo:
+                            dst = (self.masks[plane_step % 2][lo:hi] if self.direct
+                                   else self.recv[plane_step % 2][r][: hi - lo])
+                            ops.append(dist.P2POp(dist.irecv, comm_view(dst), r, group=self.group))
+                elif self.hi > self.lo:
+                    ops.append(dist.P2POp(dist.isend, comm_view(self.plane(plane_step)), 0, group=self.group))
+            if ops:
+                works += dist.batch_isend_irecv(ops)
+            return works
+        if send_buf is not None or recv_buf is not None:
+            pieces = self._pieces(send_buf) if self.rank == 0 else None
+            if self.rank == 0:  # the root keeps its own shard in place; scatter still needs a target
+                if getattr(self, "_root_piece", None) is None:
+                    self._root_piece = torch.empty_like(pieces[0])
+                mine = self._root_piece
+            else:
+                mine = recv_buf[: self.width]
+            works.append(dist.scatter(mine, scatter_list=pieces, src=0, group=self.group, async_op=True))
+        if plane_step is not None:
+            src = self.planes[plane_step % 2] if self.planes is not None else None
+            if src is None:  # root with a direct plane in the collective mode cannot happen (direct needs p2p)
+                raise AssertionError("direct planes need the p2p transport")
+            dst = [comm_view(p) for p in self.recv[plane_step % 2]] if self.rank == 0 else None
+            works.append(dist.gather(comm_view(src), gather_list=dst, dst=0, group=self.group, async_op=True))
+        return works
+
+    def assemble(self, j: int) -> None:
+        """Root, after step j's plane transfers are complete: OR every rank's plane into the u64
+        masks of its key shard at its filters' bit offset (nothing to do for direct planes)."""
+        if self.rank != 0 or self.direct:
+            return
+        mask = self.masks[j % 2]
+        mask[: self.n].zero_()
+        for r in range(self.world):
+            lo, hi = self.grid.key_bounds(self.n, self.grid.group_of(r))
+            cnt = self.grid.filter_count(r)
+            if hi == lo or cnt == 0:
+                continue
+            plane = (self.planes[j % 2] if r == 0 else self.recv[j % 2][r])[: hi - lo].to(torch.int64)
+            if cnt < 64:
+                plane = plane & ((1 << cnt) - 1)
+            mask[lo:hi] |= plane << self.grid.filter_lo(r)
+
+
+def grid_probe(batch: torch.Tensor | None, n: int, row_shape: tuple, dtype, local_filters, grid: KeyFilterGrid,
+               probe_fn: ProbeFn, mode: str = "p2p", device="cpu", group=None) -> np.ndarray | None:
+    """One batch through the key x filter grid, synchronously: `batch` (n rows, root only) is
+    split by key group, each rank probes its shard against its filters with `probe_fn`, and the
+    root returns the u64 masks (None on the other ranks)."""
+    ex = GridExchange(grid, n, row_shape, dtype, device, nbufs=1, mode=mode, group=group)
+    if grid.rank == 0 and n:
+        ex.bufs[0][:n].copy_(batch)
+    for w in ex.exchange(ex.bufs[0] if grid.rank == 0 else None, ex.bufs[0] if grid.rank else None, None):
+        w.wait()
+    plane = ex.plane(0)
+    plane.zero_()
+    if ex.hi > ex.lo and grid.shard.count:
+        probe_fn(ex.shard_view(ex.bufs[0]), local_filters, plane)
+    for w in ex.exchange(None, None, 0):
+        w.wait()
+    if grid.rank != 0:
+        return None
+    ex.assemble(0)
+    return ex.mask(0).cpu().numpy().view(np.uint64).copy()
+
+
+class GridPipeline:
+    """The grid exchange of bench.py --config c5_2d at N > 1, one new batch per step.
+
+    The root writes batch j + lead during step j (`root_target(j)`: its packing pass) and, at the
+    end of step j, one exchange sends that batch's shards and brings step j's planes back, so the
+    transfers run on the communication stream while step j + 1 computes.  Batch b lives in
+    bufs[b % (lead + 1)].  `acquire(j)` (top of step j) waits for every exchange issued up to the
+    end of step j - lead: that delivered batch j, freed the plane buffer step j reuses and, on the
+    root, the batch buffer it overwrites next.  With nccl the wait is a stream wait; with gloo a
+    host wait."""
+
+    def __init__(self, ex: GridExchange, lead: int = 2, produce: Callable[[int, torch.Tensor], None] | None = None):
+        if len(ex.bufs) != lead + 1:
+            raise ValueError("need lead + 1 batch buffers")
+        self.ex, self.lead, self.produce = ex, lead, produce
+        self.works: dict[int, list] = {}
+
+    def _buf(self, b: int) -> torch.Tensor:
+        return self.ex.bufs[b % len(self.ex.bufs)]
+
+    def prologue(self) -> None:
+        for b in range(self.lead):
+            if self.ex.rank == 0 and self.produce is not None:
+                self.produce(b, self._buf(b))
+            self.works[b - self.lead] = self.ex.exchange(self._buf(b) if self.ex.rank == 0 else None,
+                                                         self._buf(b) if self.ex.rank else None, None)
+
+    def _wait_through(self, s: int) -> None:
+        for key in sorted(x for x in self.works if x <= s):
+            for w in self.works.pop(key):
+                w.wait()
+            if key >= 0:
+                self.ex.assemble(key)
+
+    def acquire(self, j: int) -> torch.Tensor:
+        """This rank's shard of batch j (after its transfer)."""
+        self._wait_through(j - self.lead)
+        return self.ex.shard_view(self._buf(j))
+
+    def root_target(self, j: int) -> torch.Tensor:
+        return self._buf(j + self.lead)
+
+    def end_step(self, j: int) -> None:
+        b = j + self.lead
+        self.works[j] = self.ex.exchange(self._buf(b) if self.ex.rank == 0 else None,
+                                         self._buf(b) if self.ex.rank else None, j)
+
+    def drain(self) -> None:
+        self._wait_through(max(self.works, default=-1))

@@ -11,6 +11,12 @@
 // launch).  MayContain crosses once per call and is answered on the library's host copy of the
 // bits, lock-free (seb_filter_may_contain).
 //
+// Errors: the Go API has no error returns.  A device that is busy, out of HBM or absent does not
+// reach the callers: the library builds / probes on its host copy of the filter instead (the
+// "cpu_fallback" option, counted by seb_fallback_count), so a flush or compaction worker keeps
+// running where the reference would.  libPanic is left for what the reference also panics on
+// (a decoded filter too short for its numBits, sizing outside Go's defined range).
+//
 // Not compiled in this repository's pipeline: no Go toolchain exists in the build image or on
 // the GPU box (see DESIGN.md).  storage-engines_amd/harness/sstable_replay.c exercises the C call
 // sequence of per-key Adds, and harness/flush_bench.c (bench.py --config flush) times both that

@@ -226,6 +226,7 @@ int main(int argc, char **argv) {
             return 1;
         }
     }
-    printf("]}\n");
+    /* every build and batched probe ran on the GPU, none through the boundary's CPU fallback */
+    printf("], \"cpu_fallbacks\": %" PRIu64 "}\n", seb_fallback_count());
     return 0;
 }

@@ -9,8 +9,11 @@ parity tests read like the reference's own call sequences:
     (*BloomFilter).Encode()            lsm/bloom.go:96   -> .encode()
     DecodeBloomFilter(data)            lsm/bloom.go:105  -> BloomFilter.decode(data)  (None if < 12 B)
 
-Every computation runs in the HIP library on the GPU.  There is no CPU fallback: if the
-library is missing or no gfx950 device is present, calls raise SebError.
+Every computation runs in the HIP library on the GPU: if the library is missing, or no gfx950
+device is present, the device-resident and batch calls raise SebError.  The one exception is the
+drop-in boundary's (SURVEY.md 8(b) error row): the Go API mirror (`BloomFilter`) keeps working on
+its host copy when its device path fails, as the Go API has no error returns; `fallback_count()`
+counts those uses and the GPU tests and smoke() assert it stays 0.
 """
 from __future__ import annotations
 
@@ -93,6 +96,7 @@ _SIGS = {
     "seb_filter_num_hashes": (_u32, [_vp]),
     "seb_filter_pending": (_u64, [_vp]),
     "seb_filter_flush": (_i, [_vp]),
+    "seb_fallback_count": (_u64, []),
     "seb_registry_new": (_vp, [_i]),
     "seb_registry_free": (None, [_vp]),
     "seb_registry_put": (_i, [_vp, _u64, _i, _vp, _u64, _vp, _u64, _vp, _u64]),
@@ -197,6 +201,11 @@ class option:
 
     def __exit__(self, *exc):
         set_option(self.name, self.old)
+
+
+def fallback_count() -> int:
+    """Go-API-mirror builds / probes that ran on the host copy because the device path failed."""
+    return int(lib().seb_fallback_count())
 
 
 def device_check(device: int = 0) -> None:

@@ -32,3 +32,18 @@ def seb():
     if not os.path.exists(seb_bloom.LIB_PATH):
         seb_bloom.build_library()
     return seb_bloom
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _hip_path_only():
+    """On a GPU, no Go-API-mirror call may have fallen back to the host copy (seb_fallback_count):
+    the parity the GPU tests show is the HIP path's.  tests/test_fallback.py forces fallbacks in
+    child processes only."""
+    yield
+    mod = sys.modules.get("seb_bloom")
+    if mod is None or mod._lib is None:
+        return
+    import torch
+
+    if torch.cuda.is_available():
+        assert mod.fallback_count() == 0, f"{mod.fallback_count()} CPU fallbacks on a GPU run"

@@ -288,3 +288,127 @@ def test_partitioned_probe_of_one_filter(world, nq, dst):
             assert np.array_equal(results[r], want)
         else:
             assert results[r] is None
+
+
+# ------------------------------------ C5 as a key x filter grid (bench.py --config c5_2d) ----
+
+def _c5_batch(nf, per, nprobe, salt=0):
+    """The C5 probe rule: even q present in filter (q/2) mod nf, odd q absent; `salt`
+    shifts the batch so the pipeline test's batches differ."""
+    qq = np.arange(nprobe) + salt
+    half = qq // 2
+    return kg.key16(np.where(qq % 2 == 0, (half % nf) * per + half // nf, nf * per + qq))
+
+
+def _grid_worker(rank, world, port, nf, per, nprobe, groups, mode, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        grid = dp.KeyFilterGrid(nf, rank, world, groups)
+        local = _filters(nf, per)[grid.shard.lo: grid.shard.hi]
+        batch = torch.from_numpy(_c5_batch(nf, per, nprobe)) if rank == 0 else None
+        mask = dp.grid_probe(batch, nprobe, (16,), torch.uint8, local, grid, _oracle_probe_fn, mode=mode)
+        q.put((rank, mask))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return results
+
+
+# (world, filters, key groups, transport): full key split (R = world), a 2-D grid (3 ranks can
+# only be 3x1 or 1x3), 40 filters over 2 slots (int32 planes) and a ragged batch
+@pytest.mark.parametrize("world,nf,groups,mode", [(2, 8, 2, "p2p"), (2, 8, 2, "collective"), (3, 8, 3, "p2p"),
+                                                  (3, 40, 1, "p2p"), (3, 64, 3, "collective"),
+                                                  (2, 64, 1, "collective"), (2, 64, 2, "p2p")])
+def test_grid_probe_matches_oracle(world, nf, groups, mode):
+    """dist_probe.KeyFilterGrid / grid_probe: the batch split over key groups, filters over the
+    slots of a group, planes back to the root = the oracle's multi-filter MayContain masks."""
+    per, nprobe = 2000, 3001
+    results = _run(_grid_worker, world, nf, per, nprobe, groups, mode)
+    ref = oc.probe_multi(_filters(nf, per), _c5_batch(nf, per, nprobe), nprobe, stride=16)
+    assert np.array_equal(results[0], ref)
+    for r in range(1, world):
+        assert results[r] is None
+    qq = np.arange(nprobe)
+    owner = (qq // 2) % nf
+    assert np.all(((ref[0::2] >> owner[0::2].astype(np.uint64)) & np.uint64(1)) == 1)
+
+
+def _grid_pipe_worker(rank, world, port, nf, per, nprobe, groups, mode, steps, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        grid = dp.KeyFilterGrid(nf, rank, world, groups)
+        local = _filters(nf, per)[grid.shard.lo: grid.shard.hi]
+        lead = 2
+        ex = dp.GridExchange(grid, nprobe, (16,), torch.uint8, "cpu", nbufs=lead + 1, mode=mode)
+
+        def produce(b, buf):
+            buf[:nprobe].copy_(torch.from_numpy(_c5_batch(nf, per, nprobe, salt=b)))
+
+        pipe = dp.GridPipeline(ex, lead=lead, produce=produce)
+        pipe.prologue()
+        got = {}
+        for j in range(steps):
+            shard = pipe.acquire(j)
+            if rank == 0 and j >= lead:
+                got[j - lead] = ex.mask(j - lead).numpy().copy()  # complete after acquire(j)
+            if rank == 0:
+                produce(j + lead, pipe.root_target(j))
+            plane = ex.plane(j)
+            plane.zero_()
+            if grid.shard.count and shard.shape[0]:
+                _oracle_probe_fn(shard, local, plane)
+            pipe.end_step(j)
+        pipe.drain()
+        if rank == 0:
+            for j in range(max(steps - lead, 0), steps):
+                got[j] = ex.mask(j).numpy().copy()
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,groups,mode", [(2, 2, "p2p"), (3, 3, "collective"), (2, 1, "p2p")])
+def test_grid_pipeline_each_step_its_own_batch(world, groups, mode):
+    """bench.py c5_2d's pipelined exchange (dist_probe.GridPipeline): a new batch every step, its
+    shards sent two steps ahead while the planes of the step before come back; the root's masks
+    of every step equal the oracle's for that step's batch."""
+    nf, per, nprobe, steps = 8, 1500, 1201, 6
+    results = _run(_grid_pipe_worker, world, nf, per, nprobe, groups, mode, steps)
+    filters = _filters(nf, per)
+    got = results[0]
+    assert sorted(got) == list(range(steps))
+    for j in range(steps):
+        ref = oc.probe_multi(filters, _c5_batch(nf, per, nprobe, salt=j), nprobe, stride=16)
+        assert np.array_equal(got[j].view(np.uint64), ref), j
+
+
+def test_key_filter_grid_partition():
+    for world, groups in ((1, 1), (2, 2), (2, 1), (4, 2), (8, 8), (8, 4), (8, 1), (3, 3)):
+        seen = {}
+        for r in range(world):
+            g = dp.KeyFilterGrid(64, r, world, groups)
+            assert g.group == r // (world // groups)
+            for f in range(g.shard.lo, g.shard.hi):
+                seen.setdefault(g.group, []).append(f)
+        assert all(sorted(v) == list(range(64)) for v in seen.values()) and len(seen) == groups
+    g = dp.KeyFilterGrid(64, 0, 8, 8)
+    n = 10_000_001
+    assert [g.key_bounds(n, x) for x in range(8)][-1][1] == n and g.width(n) == 1_250_001
+    with pytest.raises(ValueError):
+        dp.KeyFilterGrid(64, 0, 6, 4)
