@@ -59,7 +59,7 @@ GOLDEN_MANY = "18f390ebd4082f2282f8f6352c2e02f946e855b57078fcd4f21e81956050baa7"
 GOLDEN_WAL = "7d661e321c2804cebf541abd9c1a34463b70fe27fce3c5459a71408ac91b3e01"  # sha256(u32 CRCs), 2M records
 OPTIONS = ("build_algo", "multi_interleave", "multiget_order", "multiget_l0_group", "varlen_prehash_min_keys", "bucket_min_keys",
            "lds_min_keys", "many_splits", "probe_phases", "probe_compact", "grid_cap", "workspace_limit_mib",
-           "cpu_fallback")
+           "varlen_tail", "cpu_fallback")
 
 
 def gather_ceiling():
@@ -504,6 +504,7 @@ def setup_c5_2d(args, seb, kg, torch, dev, rank, world, dist):
     if not (k == 7 and m < (1 << 29)):
         raise SystemExit("c5_2d at N > 1 sends packed residues: needs k == 7 and m < 2^29")
     mode = "p2p" if args.dist_backend == "nccl" else "collective"  # gloo cannot send device tensors p2p
+    dist.barrier()  # a collective first: every rank joins the communicator before the first grouped p2p call
     ex = dp.GridExchange(grid, n, (), torch.int64, dev, nbufs=3, mode=mode)
     produce = (lambda b, buf: seb.dev_pack_residues(st.pk, m, k, buf[:n])) if rank == 0 else None
     st.pipe = dp.GridPipeline(ex, lead=2, produce=produce)
@@ -812,6 +813,18 @@ def run_flush(args):
         "sizes": res["sizes"],
         "cpu_fallbacks": res.get("cpu_fallbacks"),
     }
+    # Roofline of the whole drop-in call (no single kernel dominates a 50K-key flush: DESIGN 6.1):
+    # the keys in and the bits out, over the shim pattern's end-to-end time, host memory to host
+    # memory; against HBM and against the PCIe link the bytes cross.
+    alg = 16 * flush["n"] + (flush["encode_len"] - 12)
+    t_us = flush["shim_us"]["total"]
+    ach = alg / (t_us * 1e-6) / 1e9
+    result["roofline"] = {"bound": "hbm", "kernel": "seb_filter_add_batch + Encode (end to end)", "achieved": round(ach, 2),
+                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 6),
+                          "pcie_peak": 63.0, "pcie_frac": round(ach / 63.0, 4), "traffic": None,
+                          "algorithmic_bytes_per_launch": int(alg),
+                          "time_source": "sizes[n=50000].shim_us.total: wall clock of the buffered-Add build + "
+                                         "Encode, host memory in and out"}
     if not args.no_cpu_baseline:
         from oracle import oracle_c as oc
 
@@ -925,11 +938,12 @@ def main():
     if rank == 0:
         kern = {name: (ms, st.kernel_bytes[name]) for name, ms in kern_ms.items()}
         dom = max(kern, key=lambda x: kern[x][0])
-        traffic = None  # PMC-measured HBM bytes of the dominant step (the newest round's profile that has it)
+        traffic = traffic_src = None  # PMC-measured HBM bytes of the dominant step (the newest round's profile that has it)
         for pmc_path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")), reverse=True):
             with open(pmc_path) as f:
                 traffic = json.load(f).get(st.pmc_key or args.config, {}).get(dom, {}).get("hbm_bytes_per_launch")
             if traffic is not None:
+                traffic_src = f"{os.path.relpath(pmc_path, ROOT)}[{st.pmc_key or args.config}][{dom}]"
                 break
         ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
         result = {
@@ -946,6 +960,7 @@ def main():
             **{f"{name}_ms": round(ms, 4) for name, ms in kern_ms.items()},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": int(kern[dom][1]),
                          "time_source": "mean HIP-event launch time of the dominant call over the sampled "
                                         "timed steps (launch_timers), on its launch stream; not the wall-clock step",
@@ -969,10 +984,10 @@ def main():
                 "S": 64, "bytes_per_key": spk,
                 "GB/s": {d: round(st.n * spk[d] / (kern_ms[d] * 1e-3) / 1e9, 1) for d in spk if d in kern_ms},
                 "note": "modelled bytes, most of them L2 hits; not comparable to the HBM peak"}
-        if args.config in ("c2c3", "lsm", "lsm_wide"):
+        if args.config in ("c2c3", "lsm", "lsm_wide", "c5"):
             # The probe's real bound: filter-word gathers, counted offline per
-            # call with the oracle (tools/gather_count.py, tools/gather_count_lsm.py), against the
-            # measured L2-resident ceiling.
+            # call with the oracle (tools/gather_count.py, tools/gather_count_lsm.py,
+            # tools/gather_count_c5.py), against the measured L2-resident ceiling.
             gpath = os.path.join(ROOT, "profiles", "gathers_c2c3.json")
             ceil, csrc = gather_ceiling()
             if world == 1 and "probe" in kern_ms and ceil and os.path.exists(gpath) and args.lsm_order == "batch":
@@ -1143,9 +1158,16 @@ def secondary_lines():
                                cfg, "registry MultiGet Mkeys/s (10M keys)"),
                 "value": line.get("value"), "unit": line.get("unit"),
                 "ms_per_step": line.get("ms_per_step"), "parity": line.get("parity")}
-        gm = line.get("roofline", {}).get("gather_model")
-        if gm:
-            item["gather_model"] = {k: gm[k] for k in ("gathers_per_call", "Ggathers_s", "ceiling_Ggathers_s", "frac")}
+        rl = line.get("roofline")
+        if rl:  # the child's dominant-kernel roofline, recomputable from its fields and profiles/
+            item["roofline"] = {k: rl[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
+                                                   "traffic_source", "algorithmic_bytes_per_launch", "time_source")
+                                if k in rl}
+            item["kernel_ms"] = {k[:-3]: v for k, v in line.items() if k.endswith("_ms") and k != "ms_per_step"}
+            gm = rl.get("gather_model")
+            if gm:
+                item["gather_model"] = {k: gm[k] for k in ("gathers_per_call", "Ggathers_s", "ceiling_Ggathers_s", "frac",
+                                                           "count_source")}
         if cfg == "flush":
             item["sizes"] = [{"n": z["n"], "shim_us": z["shim_us"]["total"], "per_key_add_us": z["build_us"]["total"],
                               "may_contain_ns_1t": z["may_contain"]["ns_per_call_1t"],

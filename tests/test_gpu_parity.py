@@ -474,18 +474,21 @@ def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
     assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
+@pytest.mark.parametrize("tail", [1, 2])
 @pytest.mark.parametrize("algo", [0, 2])
-def test_c4_prehash_golden(seb, golden, torch_cuda, algo):
+def test_c4_prehash_golden(seb, golden, torch_cuda, algo, tail):
     """C4's zipf lengths (the spans fit the LDS window, so the sorted and split-chain hashing
     paths run rather than the overflow fallback), pre-hashed to 16-B hashes (LDS-resident build,
-    unphased probe) and to packed residues (bucketed build), reproduce the C4 golden digests."""
+    unphased probe) and to packed residues (bucketed build), reproduce the C4 golden digests;
+    with the chain waves' fill (varlen_tail 2: up to 3 keys per chain-wave lane, the one-key
+    waves taking the t-th longest key left) and without it (1)."""
     torch = torch_cuda
     n = 100000
     row = next(r for r in golden["varlen"] if r["n"] == n)
     m, k = row["m"], row["k"]
     data, off = kg.varlen_keys(np.arange(n))
     pdata, poff = kg.varlen_keys(kg.probe_indices(n))
-    with seb.option("varlen_prehash_min_keys", 0), seb.option("build_algo", algo):
+    with seb.option("varlen_prehash_min_keys", 0), seb.option("build_algo", algo), seb.option("varlen_tail", tail):
         kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
         words, bits = dev_build_bits(seb, torch, kd, m, k)
         assert sha(bn.encode(bits, m, k)) == row["encode_sha256"]
@@ -522,11 +525,13 @@ def test_varlen_processing_order_invisible(seb, torch_cuda, prehash_min, build_a
         assert np.array_equal(out.cpu().numpy(), oc.probe(ref, m, k, pd, n, offsets=off))
 
 
+@pytest.mark.parametrize("tail", [1, 2])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed):
-    """The pre-hash (448-key workgroups, 64-B window per key, split-chain tail waves) hashes like
-    the oracle over lengths that mix empty, sub-word, bucket-edge and window-overflowing keys,
-    and a ragged last workgroup."""
+def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed, tail):
+    """The pre-hash (448-key workgroups, 64-B window per key, split-chain tail waves with and
+    without the fill) hashes like the oracle over lengths that mix empty, sub-word, bucket-edge
+    and window-overflowing keys, and a ragged last workgroup; the answers of a half-present batch
+    equal the oracle's key by key."""
     torch = torch_cuda
     rng = np.random.default_rng(seed)
     n = 40000 + 77
@@ -538,7 +543,11 @@ def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed):
     data = rng.integers(0, 256, int(off[-1]) + 1, dtype=np.uint8)[1:]  # odd base offset in the host copy
     m, k = oc.params(n, 0.01)
     ref = oc.build(m, k, data, n, offsets=off)
-    with seb.option("varlen_prehash_min_keys", 0):
+    pd = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    pd[: int(off[n // 2])] = data[: int(off[n // 2])]  # first half present
+    want = oc.probe(ref, m, k, pd, n, offsets=off)
+    with seb.option("varlen_prehash_min_keys", 0), seb.option("varlen_tail", tail):
+        pkd = seb.dev_keys(to_dev(torch, pd), to_dev(torch, off))
         dd = torch.zeros(int(off[-1]) + 64, dtype=torch.uint8, device="cuda")
         offd = to_dev(torch, off)
         for shift in (0, 3):  # key bytes at an unaligned device address too
@@ -551,6 +560,9 @@ def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed):
             seb.dev_probe(kd, words, m, k, out)
             torch.cuda.synchronize()
             assert bool(out.all()), shift
+        seb.dev_probe(pkd, words, m, k, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want)
 
 
 @pytest.mark.parametrize("k", [7, 8])

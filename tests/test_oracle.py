@@ -186,3 +186,34 @@ def test_gather_count_tool(tmp_path):
     with open(os.path.join(root, "profiles", "gathers_c2c3.json")) as f:
         full = json.load(f)["c2c3"]["probe"]
     assert full["n"] == 10_000_000 and full["positives"] == 5_233_107 and full["ranges"] == 3
+
+
+def test_gather_count_c5_tool(tmp_path):
+    """tools/gather_count_c5.py (the C5 line's gather_model): the keys whose 64-filter mask stays
+    non-zero are exactly the keys the oracle's multi-filter probe answers 'maybe' for, and the
+    committed 10M count is the one the bench reads."""
+    import json
+    import subprocess
+    import sys
+
+    import keygen as kg
+    from oracle import oracle_c as oc
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "g.json"
+    n = 20_000
+    subprocess.run([sys.executable, os.path.join(root, "tools", "gather_count_c5.py"), "--n", str(n), "--out", str(out)],
+                   check=True, capture_output=True)
+    r = json.loads(out.read_text())["c5"]["probe"]
+    nf, per = 64, 100_000
+    m, k = oc.params(per, 0.01)
+    filters = [(oc.build(m, k, kg.key16(f * per + np.arange(per)), per, stride=16), m, k) for f in range(nf)]
+    q = np.arange(n)
+    half = q // 2
+    mask = oc.probe_multi(filters, kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q)), n,
+                          stride=16)
+    assert r["keys_with_a_maybe"] == int((mask != 0).sum())
+    assert n * 7 >= r["gathers"] >= n  # at least one gather per key, at most k
+    with open(os.path.join(root, "profiles", "gathers_c2c3.json")) as f:
+        full = json.load(f)["c5"]["probe"]
+    assert full["n"] == 10_000_000 and full["filters"] == 64 and full["slices"] == 4
