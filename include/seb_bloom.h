@@ -95,8 +95,7 @@ int seb_abi_version(void);
  *                     bit-interleaved table, one gather per position for all of them (1, default)
  *   "varlen_prehash_min_keys"  variable-length batches of this many keys are pre-hashed in LDS
  *   "varlen_tail"     pre-hash: the 64 longest keys of a workgroup run on two waves, one per FNV
- *                     chain, each lane then also taking up to two more keys that fit its gap to the
- *                     longest (2, default), or without that fill (1)
+ *                     chain (1, default), or one key per lane like the others (0)
  *   "grid_cap"        maximum workgroups of the grid-stride kernels
  *   "workspace_limit_mib"  cap on library scratch and a context's build scratch (0 = none); a
  *                     request above it fails with SEB_ERR_NOMEM (MultiGet's key-range order then

@@ -139,14 +139,11 @@ __device__ __forceinline__ void put_hash(void *out, uint64_t i, uint64_t h1, uin
         ((uint4 *)out)[i] = make_uint4((uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32));
 }
 
-// TAIL > 0 (KEYS = 448, 512 threads): a full workgroup's 64 longest keys (the last slots of the
-// length order, which otherwise set the workgroup's lifetime and hold its LDS after the other
-// waves are done) are hashed by the last two waves, lane for lane the same key, one wave per FNV
-// chain: each runs half the instructions.  The FNV-1 wave hands its hashes to the FNV-1a wave
-// through LDS for the packed output; the 16-B output is written in halves.
-// TAIL == 2 adds the fill (tail_plan): each of those 64 lanes then hashes up to kTailFill more
-// keys, the longest remaining ones that fit the gap between its head and the longest key, so the
-// chain waves' lanes run about equally long and the one-key-per-lane waves lose their longest keys.
+// NS > 0 (KEYS = 512 - 64 * NS, 512 threads): a full workgroup's 64 * NS longest keys (the last
+// slots of the length order, which otherwise set the workgroup's lifetime and hold its LDS after
+// the other waves are done) are hashed by the last 2 * NS waves, a pair per 64 keys, one wave per
+// FNV chain: each runs half the instructions.  The FNV-1 wave hands its hashes to the FNV-1a
+// wave through LDS for the packed output; the 16-B output is written in halves.
 // P0 (with PACK): the compacted phased probe's phase 0 fused in (k_probe_c0's job for a pre-hashed
 // batch): the packed words go to LDS in key order, then each wave takes one group of 64 keys,
 // tests the positions in range 0 [0, p0.hi) and stores the live keys' words compacted in the
@@ -158,131 +155,14 @@ struct Phase0Arg {
     uint32_t hi;
 };
 
-constexpr uint32_t kTailFill = 2;   // fill passes: up to 2 more keys per chain-wave lane
-constexpr uint32_t kFillMinDw = 2;  // keys under 2 dwords are not worth a lane's per-key overhead
-constexpr uint32_t kNoSlot = 0xffffffffu;
-
-__device__ __forceinline__ uint32_t dw_bucket(uint32_t sk) {  // a sorted slot's dword-length bucket
-    const uint32_t dw = ((sk & 0xffffu) + 3) >> 2;
-    return dw > 64 ? 64u : dw;
-}
-
-// The fill's candidate set: the 384 keys after the 64 longest of a full workgroup, longest first
-// (candidate c is sorted slot 447 - 64 - c), as a 384-bit used mask held by every lane.
-__device__ __forceinline__ uint32_t used_below(const uint64_t (&used)[6], uint32_t x) {
-    uint32_t r = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < 6; ++w) {
-        uint64_t m = used[w];
-        if (x <= 64 * w) m = 0;
-        else if (x < 64 * w + 64) m &= (1ull << (x - 64 * w)) - 1;
-        r += (uint32_t)__popcll(m);
-    }
-    return r;
-}
-
-__device__ __forceinline__ uint32_t select_bit(uint64_t v, uint32_t r) {  // position of set bit r of v
-    uint32_t pos = 0;
-#pragma unroll
-    for (uint32_t sh = 32; sh; sh >>= 1) {
-        const uint32_t c = (uint32_t)__popcll(v & ((1ull << sh) - 1));
-        if (r >= c) {
-            r -= c;
-            v >>= sh;
-            pos += sh;
-        }
-    }
-    return pos;
-}
-
-// The k-th candidate (0-based) not yet taken.
-__device__ __forceinline__ uint32_t select_unused(const uint64_t (&used)[6], uint32_t k) {
-    uint32_t c = kNoSlot, cum = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < 6; ++w) {
-        const uint64_t fr = ~used[w];
-        const uint32_t f = (uint32_t)__popcll(fr);
-        if (c == kNoSlot && k < cum + f) c = 64 * w + select_bit(fr, k - cum);
-        cum += f;
-    }
-    return c;
-}
-
-__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) v |= __shfl_xor(v, o, 64);
-    return v;
-}
-
-// The fill plan of a full workgroup's two chain waves (both compute it, identically).  Lane l's
-// head is sorted slot 384 + l (lane 0: the shortest of the 64 longest keys, the largest gap to
-// the longest, slot 447).  Each pass, the lanes in order take the longest free candidate that fits
-// their remaining gap, distinct from the other lanes' (the recurrence c_l = max(c_prev + 1, g_l)
-// over the lanes that fit anything, as a prefix maximum); keys[1 + p] is the slot taken in pass p
-// or kNoSlot.  Lengths are dword buckets, the units of the work.
-__device__ __forceinline__ void tail_plan(const uint32_t *slot_key, uint32_t lane, uint32_t (&keys)[1 + kTailFill],
-                                          uint64_t (&used)[6]) {
-    constexpr uint32_t kCand = 384;
-    auto size = [&](uint32_t c) { return dw_bucket(slot_key[kCand - 1 - c]); };
-    const uint32_t longest = dw_bucket(slot_key[447]);
-    uint32_t load = dw_bucket(slot_key[kCand + lane]);
-    keys[0] = kCand + lane;
-    uint32_t nc = 0;  // candidates of at least kFillMinDw dwords: a prefix of the candidate order
-    {
-        uint32_t lo = 0, hi = kCand;
-#pragma unroll
-        for (int it = 0; it < 9; ++it)
-            if (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (size(mid) < kFillMinDw) hi = mid;
-                else lo = mid + 1;
-            }
-        nc = lo;
-    }
-#pragma unroll
-    for (uint32_t w = 0; w < 6; ++w) used[w] = 0;
-    uint32_t nused = 0;
-#pragma unroll
-    for (uint32_t pass = 0; pass < kTailFill; ++pass) {
-        const uint32_t gap = longest - load;
-        uint32_t lo = 0, hi = nc;  // g: the first candidate that fits the gap
-#pragma unroll
-        for (int it = 0; it < 9; ++it)
-            if (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (size(mid) <= gap) hi = mid;
-                else lo = mid + 1;
-            }
-        const bool fit = lo < nc && used_below(used, nc) - used_below(used, lo) < nc - lo;  // a free one fits
-        const uint64_t fits = __ballot(fit);
-        const int kv = (int)lanes_below(fits);
-        int x = fit ? (int)(lo - used_below(used, lo)) - kv : INT_MIN;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o, 64);
-            if ((int)lane >= o) x = max(x, y);
-        }
-        const uint32_t cc = (uint32_t)(kv + x);  // this lane's rank among the free candidates
-        const bool ok = fit && cc < nc - nused;
-        const uint32_t c = ok ? select_unused(used, cc) : kNoSlot;
-        keys[1 + pass] = ok ? kCand - 1 - c : kNoSlot;
-        if (ok) load += size(c);
-#pragma unroll
-        for (uint32_t w = 0; w < 6; ++w) used[w] |= wave_or64(ok && (c >> 6) == w ? 1ull << (c & 63) : 0ull);
-        nused += (uint32_t)__popcll(__ballot(ok));
-    }
-}
-
-// Every thread of the workgroup arrives here; its hashed keys' packed words (n of them, key
-// indices j[]) go to xpk (the staging window), then waves 0 .. KEYS/64 - 1 each take the group of
-// keys k0 + 64 * wave + lane (k0 is a multiple of 64).
-template <uint32_t KEYS, uint32_t NK>
-__device__ __forceinline__ void varlen_phase0(uint64_t *xpk, const uint32_t (&my_j)[NK], const uint64_t (&my_pw)[NK],
-                                              uint64_t k0, uint32_t cnt, const ModArg &md, const Phase0Arg &p0) {
+// Every thread of the workgroup arrives here (has: it hashed key k0 + my_j); the packed words go to
+// xpk (the staging window), then waves 0 .. KEYS/64 - 1 each take the group of keys
+// k0 + 64 * wave + lane (k0 is a multiple of 64).
+template <uint32_t KEYS>
+__device__ __forceinline__ void varlen_phase0(uint64_t *xpk, bool has, uint32_t my_j, uint64_t my_pw, uint64_t k0,
+                                              uint32_t cnt, const ModArg &md, const Phase0Arg &p0) {
     __syncthreads();  // every key is hashed: the staging window is free
-#pragma unroll
-    for (uint32_t s = 0; s < NK; ++s)
-        if (my_j[s] != kNoSlot) xpk[my_j[s]] = my_pw[s];
+    if (has) xpk[my_j] = my_pw;
     __syncthreads();  // every key's packed word is in xpk, in key order
     const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     if (wid >= KEYS / 64 || 64 * wid >= cnt) return;  // wave-uniform; no barrier follows
@@ -303,42 +183,34 @@ __device__ __forceinline__ void varlen_phase0(uint64_t *xpk, const uint32_t (&my
     if (lane == 0) p0.recs[g] = make_ulonglong2(alive, alive);
 }
 
-template <uint32_t KEYS, uint32_t WIN, bool PACK, uint32_t TAIL = 0, bool P0 = false>
-__global__ __launch_bounds__(TAIL ? 512 : KEYS) void k_hash_varlen(const uint8_t *__restrict__ data,
-                                                                   const uint64_t *__restrict__ off, uint64_t n,
-                                                                   void *__restrict__ hashes, ModArg md, Phase0Arg p0) {
+template <uint32_t KEYS, uint32_t WIN, bool PACK, uint32_t NS = 0, bool P0 = false>
+__global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *__restrict__ data,
+                                                      const uint64_t *__restrict__ off, uint64_t n,
+                                                      void *__restrict__ hashes, ModArg md, Phase0Arg p0) {
     constexpr uint32_t kHashLds = KEYS * WIN;
-    constexpr uint32_t NK = TAIL == 2 ? 1 + kTailFill : 1;  // keys a lane may hash
     static_assert(kHashLds % 16 == 0 && kHashLds + 16 < 65536, "window offsets are 16-bit");
-    static_assert(!TAIL || KEYS == 448, "the chain waves: 64 keys, two waves, 512 threads");
     static_assert(!P0 || (PACK && KEYS % 64 == 0 && KEYS * 8 <= kHashLds), "phase 0: whole groups of 64 keys, words in the window");
     __shared__ uint4 stage[kHashLds / 16 + 1];  // +16 B: the funnel walk reads one dword past a key
-    // the length sort's bucket counters; after the sort: the fill's used mask (6 words), the
-    // handover flags (TAIL == 2)
-    __shared__ uint64_t cur64[(kLenBuckets + 1) / 2];
-    uint32_t *cur = (uint32_t *)cur64;
+    __shared__ uint32_t cur[kLenBuckets];
     __shared__ uint32_t slot_key[KEYS];  // sorted slot -> start byte in the window << 16 | length
     __shared__ uint16_t slot_idx[KEYS];  // sorted slot -> key within the workgroup
-    __shared__ uint64_t xh2[TAIL ? (TAIL == 2 ? 128 : 64) : 1];  // the FNV-1 wave's hashes for the FNV-1a wave
-    __shared__ uint32_t xflag[TAIL == 1 ? 1 : 1];
+    __shared__ uint64_t xh2[NS ? 64 * NS : 1];  // the FNV-1 waves' hashes for the FNV-1a waves
+    __shared__ uint32_t xflag[NS ? NS : 1];
     const uint32_t t = threadIdx.x;
     const uint64_t k0 = (uint64_t)blockIdx.x * KEYS;
     const uint64_t k1 = k0 + KEYS < n ? k0 + KEYS : n;
     const uint32_t cnt = (uint32_t)(k1 - k0);
     const bool mine = t < cnt;
-    // P0: a thread keeps its keys' packed words until every key is hashed, then the words go to the
+    // P0: a thread keeps its key's packed word until every key is hashed, then the words go to the
     // (by then unused) staging window in key order: no LDS of its own, so 5 workgroups still fit a CU
-    uint32_t my_j[NK];
-    uint64_t my_pw[NK];
-#pragma unroll
-    for (uint32_t s = 0; s < NK; ++s) {
-        my_j[s] = kNoSlot;
-        my_pw[s] = 0;
-    }
-    auto emit = [&](uint32_t s, uint32_t j, uint64_t h1, uint64_t h2) {  // key k0 + j, the lane's s-th
+    uint32_t my_j = 0;
+    uint64_t my_pw = 0;
+    bool has = false;
+    auto emit = [&](uint32_t j, uint64_t h1, uint64_t h2) {  // key k0 + j
         if constexpr (P0) {
-            my_j[s] = j;
-            my_pw[s] = pack_residue(h1, h2, md);
+            my_j = j;
+            my_pw = pack_residue(h1, h2, md);
+            has = true;
         } else {
             put_hash<PACK>(hashes, k0 + j, h1, h2, md);
         }
@@ -352,13 +224,14 @@ __global__ __launch_bounds__(TAIL ? 512 : KEYS) void k_hash_varlen(const uint8_t
         if (mine) {
             uint64_t h1, h2;
             fnv_range(data, ks, ke, h1, h2);
-            emit(0, t, h1, h2);
+            emit(t, h1, h2);
         }
-        if constexpr (P0) varlen_phase0<KEYS>((uint64_t *)stage, my_j, my_pw, k0, cnt, md, p0);
+        if constexpr (P0)
+            varlen_phase0<KEYS>((uint64_t *)stage, has, my_j, my_pw, k0, cnt, md, p0);
         return;
     }
     if (t < kLenBuckets) cur[t] = 0u;
-    if (t < 1) xflag[t] = 0u;
+    if (t < NS) xflag[t] = 0u;
     for (uint32_t c = t; c < (uint32_t)chunks; c += blockDim.x) stage[c] = ((const uint4 *)base)[c];
     const uint32_t len = (uint32_t)(ke - ks);
     const uint32_t dw = (len + 3) >> 2;
@@ -395,131 +268,54 @@ __global__ __launch_bounds__(TAIL ? 512 : KEYS) void k_hash_varlen(const uint8_t
     }
     __syncthreads();
     const uint32_t *lds = (const uint32_t *)stage;
-    const bool full = TAIL && cnt == KEYS;
-    const uint32_t lane = t & 63;
-    if constexpr (TAIL == 2) {
-        // the chain waves plan the fill; the first writes the used mask for the one-key waves and
-        // clears the handover flags (the sort's counters are dead), then everyone proceeds
-        uint32_t keys[NK];
-        uint64_t used[6];
-        uint32_t *flags = (uint32_t *)(cur64 + 6);  // [0..2]: h2 of step s ready; [3]: step 0's slot read
-        if (full && t >= 384) {
-            tail_plan(slot_key, lane, keys, used);
-            if (t < 448 && lane < 6) cur64[lane] = used[lane];
-            if (t < 448 && lane < 4) flags[lane] = 0u;
-        }
-        __syncthreads();
-        if (full && t < 384) {  // one key per lane: the t-th longest key not taken by the fill
-#pragma unroll
-            for (uint32_t w = 0; w < 6; ++w) used[w] = cur64[w];
-            const uint32_t nrem = 384 - used_below(used, 384);
-            if (t < nrem) {
-                const uint32_t sq = 383 - select_unused(used, t);
-                const uint32_t sk = slot_key[sq];
-                Funnel f;
-                f.init(lds, sk >> 16, sk & 0xffffu);
-                f.walk(lds);
-                uint64_t h1, h2;
-                f.finish(lds, h1, h2);
-                emit(0, slot_idx[sq], h1, h2);
-            }
-        } else if (full) {  // the chain waves: a lane's head, then its fill keys, one chain each
-            const bool chain_a = t < 448;  // FNV-1a (hash1); the other wave FNV-1 (hash2)
-#pragma unroll
-            for (uint32_t s = 0; s < NK; ++s) {
-                const uint32_t sq = keys[s];
-                const bool has = sq != kNoSlot;
-                const uint32_t sk = has ? slot_key[sq] : 0u;
-                const uint32_t j = has ? slot_idx[sq] : 0u;
-                if (chain_a) {
-                    const uint64_t h1 = has ? funnel_one<true>(lds, sk >> 16, sk & 0xffffu) : 0ull;
-                    if constexpr (PACK) {
-                        while (__hip_atomic_load(&flags[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-                            __builtin_amdgcn_s_sleep(1);
-                        const uint64_t h2 = xh2[64 * (s & 1) + lane];
-                        if (s == 0) {
-                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                            __builtin_amdgcn_wave_barrier();
-                            if (lane == 0) __hip_atomic_store(&flags[3], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
-                        if (has) emit(s, j, h1, h2);
-                    } else if (has) {
-                        ((uint2 *)hashes)[2 * (k0 + j)] = make_uint2((uint32_t)h1, (uint32_t)(h1 >> 32));
-                    }
+    bool tail = false;
+    if constexpr (NS > 0) {
+        if (cnt == KEYS && t >= KEYS - 64 * NS) {  // the longest keys: a wave pair per 64, one per chain
+            tail = true;
+            const uint32_t w = (t - (KEYS - 64 * NS)) >> 6, c = w >> 1, lane = t & 63;
+            const uint32_t q = KEYS - 64 * NS + 64 * c + lane;
+            const uint32_t sk = slot_key[q];
+            const uint32_t j = slot_idx[q];
+            if ((w & 1u) == 0u) {  // FNV-1a (hash1)
+                const uint64_t h1 = funnel_one<true>(lds, sk >> 16, sk & 0xffffu);
+                if constexpr (PACK) {
+                    while (__hip_atomic_load(&xflag[c], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+                        __builtin_amdgcn_s_sleep(1);
+                    emit(j, h1, xh2[64 * c + lane]);
                 } else {
-                    const uint64_t h2 = has ? funnel_one<false>(lds, sk >> 16, sk & 0xffffu) : 0ull;
-                    if constexpr (PACK) {
-                        if (s == 2)  // buffer 0 again: the FNV-1a wave has read step 0's hashes
-                            while (__hip_atomic_load(&flags[3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-                                __builtin_amdgcn_s_sleep(1);
-                        xh2[64 * (s & 1) + lane] = h2;
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                        __builtin_amdgcn_wave_barrier();
-                        if (lane == 0) __hip_atomic_store(&flags[s], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } else if (has) {
-                        ((uint2 *)hashes)[2 * (k0 + j) + 1] = make_uint2((uint32_t)h2, (uint32_t)(h2 >> 32));
-                    }
+                    ((uint2 *)hashes)[2 * (k0 + j)] = make_uint2((uint32_t)h1, (uint32_t)(h1 >> 32));
+                }
+            } else {  // FNV-1 (hash2)
+                const uint64_t h2 = funnel_one<false>(lds, sk >> 16, sk & 0xffffu);
+                if constexpr (PACK) {
+                    xh2[64 * c + lane] = h2;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane == 0)
+                        __hip_atomic_store(&xflag[c], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    ((uint2 *)hashes)[2 * (k0 + j) + 1] = make_uint2((uint32_t)h2, (uint32_t)(h2 >> 32));
                 }
             }
-        }
-        if (!full && mine) {  // a partial workgroup: one key per lane, in length order
-            const uint32_t sk = slot_key[t];
-            Funnel f;
-            f.init(lds, sk >> 16, sk & 0xffffu);
-            f.walk(lds);
-            uint64_t h1, h2;
-            f.finish(lds, h1, h2);
-            emit(0, slot_idx[t], h1, h2);
-        }
-    } else {
-        bool tail = false;
-        if constexpr (TAIL == 1) {
-            if (full && t >= KEYS - 64) {  // the longest keys: a wave pair per 64, one per chain
-                tail = true;
-                const uint32_t w = (t - (KEYS - 64)) >> 6;
-                const uint32_t qq = KEYS - 64 + lane;
-                const uint32_t sk = slot_key[qq];
-                const uint32_t j = slot_idx[qq];
-                if ((w & 1u) == 0u) {  // FNV-1a (hash1)
-                    const uint64_t h1 = funnel_one<true>(lds, sk >> 16, sk & 0xffffu);
-                    if constexpr (PACK) {
-                        while (__hip_atomic_load(&xflag[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-                            __builtin_amdgcn_s_sleep(1);
-                        emit(0, j, h1, xh2[lane]);
-                    } else {
-                        ((uint2 *)hashes)[2 * (k0 + j)] = make_uint2((uint32_t)h1, (uint32_t)(h1 >> 32));
-                    }
-                } else {  // FNV-1 (hash2)
-                    const uint64_t h2 = funnel_one<false>(lds, sk >> 16, sk & 0xffffu);
-                    if constexpr (PACK) {
-                        xh2[lane] = h2;
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                        __builtin_amdgcn_wave_barrier();
-                        if (lane == 0)
-                            __hip_atomic_store(&xflag[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } else {
-                        ((uint2 *)hashes)[2 * (k0 + j) + 1] = make_uint2((uint32_t)h2, (uint32_t)(h2 >> 32));
-                    }
-                }
-                if constexpr (!P0) return;
-            }
-        }
-        if (mine && !tail) {  // cnt lanes hash the cnt sorted slots
-            const uint32_t sk = slot_key[t];
-            Funnel f;
-            f.init(lds, sk >> 16, sk & 0xffffu);
-            f.walk(lds);
-            uint64_t h1, h2;
-            f.finish(lds, h1, h2);
-            emit(0, slot_idx[t], h1, h2);
+            if constexpr (!P0) return;
         }
     }
-    if constexpr (P0) varlen_phase0<KEYS>((uint64_t *)stage, my_j, my_pw, k0, cnt, md, p0);
+    if (mine && !tail) {  // cnt lanes hash the cnt sorted slots
+        const uint32_t sk = slot_key[t];
+        Funnel f;
+        f.init(lds, sk >> 16, sk & 0xffffu);
+        f.walk(lds);
+        uint64_t h1, h2;
+        f.finish(lds, h1, h2);
+        emit(slot_idx[t], h1, h2);
+    }
+    if constexpr (P0) varlen_phase0<KEYS>((uint64_t *)stage, has, my_j, my_pw, k0, cnt, md, p0);
 }
 
-// 448 keys per 512-thread workgroup, the top 64 split over two chain waves with the fill
-// (varlen_tail 2, default) or without it (1), a 64-B window per key (DESIGN.md 5.5 and 8:
-// 256/384/512/1024-key workgroups and 48-80-B windows measured slower).
+// 448 keys per workgroup, a 64-B window per key, the top 64 split over two chain waves
+// (varlen_tail 1, default: 512 threads) or hashed one per lane like the rest (0: 448 threads).
+// 256/384/512/1024-key workgroups, 48-80-B windows, no chain waves and two
+// ways of giving the chain waves' lanes more keys measured slower.
 constexpr uint32_t kVarKeys = 448, kVarWin = 64;
 
 template <bool PACK, bool P0 = false>
@@ -527,12 +323,12 @@ static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const Mo
                                         Phase0Arg p0 = {}) {
     if (!kb.offsets || kb.n == 0) return hipSuccess;
     const uint64_t ntiles = (kb.n + kVarKeys - 1) / kVarKeys;
-    if (options().varlen_tail == 2)
-        hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, 2, P0>), dim3((unsigned)ntiles), dim3(512), 0, s,
-                           kb.data, kb.offsets, kb.n, out, md, p0);
+    if (options().varlen_tail == 0)
+        hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, 0, P0>), dim3((unsigned)ntiles), dim3(kVarKeys), 0,
+                           s, kb.data, kb.offsets, kb.n, out, md, p0);
     else
-        hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, 1, P0>), dim3((unsigned)ntiles), dim3(512), 0, s,
-                           kb.data, kb.offsets, kb.n, out, md, p0);
+        hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, 1, P0>), dim3((unsigned)ntiles),
+                           dim3(kVarKeys + 64), 0, s, kb.data, kb.offsets, kb.n, out, md, p0);
     return hipGetLastError();
 }
 

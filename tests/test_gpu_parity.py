@@ -474,14 +474,13 @@ def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
     assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
-@pytest.mark.parametrize("tail", [1, 2])
+@pytest.mark.parametrize("tail", [0, 1])
 @pytest.mark.parametrize("algo", [0, 2])
 def test_c4_prehash_golden(seb, golden, torch_cuda, algo, tail):
     """C4's zipf lengths (the spans fit the LDS window, so the sorted and split-chain hashing
     paths run rather than the overflow fallback), pre-hashed to 16-B hashes (LDS-resident build,
     unphased probe) and to packed residues (bucketed build), reproduce the C4 golden digests;
-    with the chain waves' fill (varlen_tail 2: up to 3 keys per chain-wave lane, the one-key
-    waves taking the t-th longest key left) and without it (1)."""
+    with the 64 longest keys of a workgroup on two chain waves (varlen_tail 1) and without (0)."""
     torch = torch_cuda
     n = 100000
     row = next(r for r in golden["varlen"] if r["n"] == n)
@@ -525,11 +524,11 @@ def test_varlen_processing_order_invisible(seb, torch_cuda, prehash_min, build_a
         assert np.array_equal(out.cpu().numpy(), oc.probe(ref, m, k, pd, n, offsets=off))
 
 
-@pytest.mark.parametrize("tail", [1, 2])
+@pytest.mark.parametrize("tail", [0, 1])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed, tail):
-    """The pre-hash (448-key workgroups, 64-B window per key, split-chain tail waves with and
-    without the fill) hashes like the oracle over lengths that mix empty, sub-word, bucket-edge
+    """The pre-hash (448-key workgroups, 64-B window per key, with and without the split-chain tail
+    waves) hashes like the oracle over lengths that mix empty, sub-word, bucket-edge
     and window-overflowing keys, and a ragged last workgroup; the answers of a half-present batch
     equal the oracle's key by key."""
     torch = torch_cuda
