@@ -102,8 +102,8 @@ def _child(case, args, q):
             # after that (scratch over workspace_limit_mib) with the fallback off: the Adds stay
             # pending and the retry must start from zeros, not from the recycled buffer's bits.
             n = 300_000
-            old = seb.BloomFilter(n, 0.01)
-            old.add_batch(kg.key16(10_000_000 + np.arange(n)))
+            old = seb.BloomFilter(n, 0.01)  # the same size class; a small batch (atomic build, no scratch)
+            old.add_batch(kg.key16(10_000_000 + np.arange(2000)))
             old.encode()
             old.close()  # its (non-zero) words go to the pool
             seb.set_option("cpu_fallback", 0)
