@@ -58,6 +58,33 @@ __device__ __forceinline__ uint64_t mad_lo(uint32_t a, uint32_t b, uint64_t acc)
     return r;
 }
 
+// a ^ (byte b of w), as ONE v_xor_b32 whose SDWA source select picks the byte (b is a constant
+// once the byte loops are unrolled, and the switch folds away).  Left to itself the compiler
+// shifts bytes 1 and 2 down first (v_lshrrev / v_bfe, then a v_bitop3 that masks and xors): one
+// extra instruction per byte, ≈22 of the ≈150 that both chains of a 16-B key cost.
+__device__ __forceinline__ uint32_t xor_byte(uint32_t a, uint32_t w, int b) {
+    uint32_t r;
+    switch (b) {
+        case 0:
+            asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD"
+                : "=v"(r) : "v"(w), "v"(a));
+            break;
+        case 1:
+            asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+                : "=v"(r) : "v"(w), "v"(a));
+            break;
+        case 2:
+            asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+                : "=v"(r) : "v"(w), "v"(a));
+            break;
+        default:
+            asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+                : "=v"(r) : "v"(w), "v"(a));
+            break;
+    }
+    return r;
+}
+
 // Both FNV chains over a 16-byte key.  Multiplying by P = 2^40 + 435 leaves the low word
 // lo' = low32(lo * 435) independent of the high word, so the low word runs the byte chain alone
 // (one v_mad_u64_u32 gives lo' and the carry c) and the high word, which is linear:
@@ -71,14 +98,13 @@ __device__ __forceinline__ void fnv_key16(const uint4 v, uint64_t &h1, uint64_t 
     uint64_t acc1 = (uint32_t)(kFnvOffset >> 32) * pow435(16), acc2 = acc1;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
-        const uint32_t x = lo1 ^ b;  // FNV-1a (hash1): xor, then multiply
+        const uint32_t x = xor_byte(lo1, w[j >> 2], j & 3);  // FNV-1a (hash1): xor, then multiply
         const uint64_t p = (uint64_t)x * 435u;
         lo1 = (uint32_t)p;
         acc1 = mad_lo((uint32_t)(p >> 32) + (x << 8), pow435(15 - j), acc1);
         const uint64_t q = (uint64_t)lo2 * 435u;  // FNV-1 (hash2): multiply, then xor
         acc2 = mad_lo((uint32_t)(q >> 32) + (lo2 << 8), pow435(15 - j), acc2);
-        lo2 = (uint32_t)q ^ b;
+        lo2 = xor_byte((uint32_t)q, w[j >> 2], j & 3);
     }
     h1 = (acc1 << 32) | lo1;
     h2 = (acc2 << 32) | lo2;
@@ -95,14 +121,13 @@ struct FnvSplit {
         uint32_t d1[4], d2[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t b = (w >> (8 * j)) & 0xffu;
-            const uint32_t x = lo1 ^ b;  // FNV-1a
+            const uint32_t x = xor_byte(lo1, w, j);  // FNV-1a
             const uint64_t p = (uint64_t)x * 435u;
             lo1 = (uint32_t)p;
             d1[j] = (uint32_t)(p >> 32) + (x << 8);
             const uint64_t q = (uint64_t)lo2 * 435u;  // FNV-1
             d2[j] = (uint32_t)(q >> 32) + (lo2 << 8);
-            lo2 = (uint32_t)q ^ b;
+            lo2 = xor_byte((uint32_t)q, w, j);
         }
         const uint64_t t1 = mad_lo(d1[0], pow435(3), mad_lo(d1[1], pow435(2), mad_lo(d1[2], 435u, d1[3])));
         const uint64_t t2 = mad_lo(d2[0], pow435(3), mad_lo(d2[1], pow435(2), mad_lo(d2[2], 435u, d2[3])));

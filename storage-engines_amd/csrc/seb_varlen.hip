@@ -77,11 +77,10 @@ struct FnvOne {
         uint32_t d[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t b = (w >> (8 * j)) & 0xffu;
-            const uint32_t x = A ? lo ^ b : lo;
+            const uint32_t x = A ? xor_byte(lo, w, j) : lo;
             const uint64_t p = (uint64_t)x * 435u;
             d[j] = (uint32_t)(p >> 32) + (x << 8);
-            lo = A ? (uint32_t)p : (uint32_t)p ^ b;
+            lo = A ? (uint32_t)p : xor_byte((uint32_t)p, w, j);
         }
         const uint64_t t = mad_lo(d[0], pow435(3), mad_lo(d[1], pow435(2), mad_lo(d[2], 435u, d[3])));
         acc = mad_lo((uint32_t)acc, pow435(4), t);
