@@ -5,7 +5,7 @@ set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
 export PYTHONUNBUFFERED=1
-O=gpurun_out/r4e
+O=gpurun_out/${1:-r4e}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests -m gpu > $O/gpu_tests.log 2>&1 || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
