@@ -1659,6 +1659,48 @@ def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
         seb.set_option("build_algo", 0)
 
 
+@pytest.mark.parametrize("bins", [1, 2, 3, 4, 5, 6, 7, 0], ids=["bins8", "bins2", "bins2k4", "pipe8", "pipe2", "pipe8k6", "pipe2k6", "counting"])
+@pytest.mark.parametrize("case", ["nb513", "c2m", "nb2274", "duplicates", "skewed"])
+def test_bucketed_scatter_bins(seb, torch_cuda, case, bins):
+    """The radix-partitioned build's two scatters (scatter_bins 1: fixed LDS bins, runs padded to
+    16-B chunks; 0: the counting sort) against the oracle, both as a fresh build into garbage words
+    and OR-ed into a filter: ordinary keys at the smallest and largest bucket counts the bins take
+    (513 and 2274 buckets: shorter rounds below 94M bits) and at C2's m, plus runs that pass their
+    bin and then their region (every key identical: 7 buckets get every position of a tile) or
+    skewed (50 distinct keys)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    m = {"nb513": 33_580_000, "nb2274": 149_000_000}.get(case, 95_850_584)
+    k = 7
+    if case == "duplicates":
+        n = 400_000
+        keys = np.tile(kg.key16(np.array([42])), (n, 1))
+    elif case == "skewed":
+        n = 400_000
+        keys = kg.key16(rng.integers(0, 50, n))
+    else:
+        n = 1_000_003
+        keys = kg.key16(rng.permutation(3 * n)[:n])
+    uniq = np.unique(keys, axis=0)
+    ref = oc.build(m, k, np.ascontiguousarray(uniq).ravel(), len(uniq), stride=16)
+    kd = seb.dev_keys(to_dev(torch, keys), n=n, stride=16)
+    with seb.option("build_algo", 2), seb.option("scatter_bins", bins):
+        words = seb.new_words(m)
+        for rep in range(2):
+            words.view(torch.uint8).fill_(0xC3 if rep == 0 else 0xFF)
+            seb.dev_build_fresh(kd, words, m, k)
+            torch.cuda.synchronize()
+            raw = words.cpu().numpy().view(np.uint8)
+            assert np.array_equal(raw[: (m + 7) // 8], ref), (case, bins, rep)
+            assert not raw[(m + 7) // 8:].any()
+        # OR-accumulating build: half the keys into a fresh filter, then all of them
+        w2 = seb.new_words(m)
+        seb.dev_build(seb.dev_keys(to_dev(torch, keys[: n // 2]), n=n // 2, stride=16), w2, m, k)
+        seb.dev_build(kd, w2, m, k)
+        torch.cuda.synchronize()
+        assert np.array_equal(seb.words_to_bits(w2, m), ref), (case, bins)
+
+
 @pytest.mark.parametrize("algo", [0, 1, 2, 3, 4])
 def test_fresh_build_overwrites_garbage(seb, golden, torch_cuda, algo):
     """seb_dev_build_fresh: words full of garbage (never cleared) become the filter of the keys, bit
