@@ -229,191 +229,41 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter(Src src, uint64_t n, Mo
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) counts[(uint64_t)b * ntiles + t] = fill[b];
 }
 
-// ---- scatter through fixed bins (k == 7; the default for 512..kBinsMaxBuckets buckets).  The
-// counting sort above costs two LDS atomics per position (histogram, then slot claim), a block
-// scan and nine barriers per round.  Here every bucket owns a fixed bin of kBinSlots u16 in LDS
-// (a round's mean is ~24.5 positions per bucket), so a position is placed with ONE returning LDS
-// atomic (its slot) and a 2-B LDS write, right after hashing; no histogram, no scan.  After one
-// barrier each bucket's run goes out as 16-B chunks (4 lanes per bucket, 16 buckets per wave):
-// the run is padded to a multiple of 8 with copies of the chunk's first index (apply ORs a bit
-// twice, harmlessly), so every region offset stays 16-B aligned and apply needs no per-index
-// bounds.  A claim past the bin (the tail of a Poisson count, ~0.5% of positions) is stored
-// straight to its region slot, which the round's start fixes.  The bucket's fill advances in the
-// same wave that read it (its 4 lanes are one aligned quad), so a round has two barriers.
-// LDS: bins[nb][kBinSlots] u16 | cnt[nb] (this round's claims) | fill[nb] (region fill) | a
-// scratch word; two arrays, not one of pairs: the claim atomics then spread over all the banks.
-constexpr uint32_t kBinSlots = 32;                  // u16 per bucket bin: 4 chunks of 8
+// ---- scatter through fixed bins (k == 7; the default for kBinMinBuckets..kBinMaxBuckets
+// buckets, C2/C4's 1463).  The counting sort above costs two LDS atomics per position (histogram,
+// then slot claim), a block scan and nine barriers per round, and its hashing cannot overlap its
+// LDS work: every wave hashes, then every wave sorts.  Here every bucket owns a fixed bin of S u16
+// in LDS (48 for up to 1575 buckets, else 32; a round's mean is ~24.5 positions per bucket), so a
+// position is placed with ONE returning LDS atomic (its slot) and a 2-B LDS write, and a thread
+// software-pipelines its keys: it hashes key r and issues its 7 claims, then writes key r-1's
+// bins, whose claims returned while key r hashed.  The LDS atomics run under the hashing.
+// After one barrier each bucket's run goes out as 16-B chunks, its S/8 chunks on adjacent lanes
+// of one wave; the run is padded to a multiple of 8 with copies of its last chunk's first index
+// (apply ORs that bit again), so every region offset stays 16-B aligned and apply needs no
+// per-index bounds.  A claim past the bin (a Poisson tail: ~3e-5 of the bucket-
+// rounds with S = 48) is stored straight to its region slot, which the round's start fixes.  The
+// lane that advances a bucket's fill sits in the wave whose lanes read it, so a round has two
+// barriers.  LDS: bins[nb][S] u16 | cnt[nb] (this round's claims) | fill[nb] (region fill) | a
+// scratch word; two arrays, not one of pairs, so the claim atomics spread over all the banks.
 constexpr uint32_t kBinMinBuckets = 512;
-constexpr uint32_t kBinMaxBuckets = (160u * 1024 - 16) / (kBinSlots * 2 + 8);  // 2275 (m <= ~149M bits)
-constexpr uint32_t kBinMeanPos = 25;                // positions per bucket per round, at most
+constexpr uint32_t kBinBig = 48, kBinSmall = 32;  // u16 slots per bin
+constexpr uint32_t bin_lds_bytes(uint32_t nb, uint32_t slots) { return nb * (slots * 2 + 8) + 16; }
+constexpr uint32_t kBinBigMaxBuckets = (160u * 1024 - 16) / (kBinBig * 2 + 8);      // 1575 (m <= ~103M bits)
+constexpr uint32_t kBinMaxBuckets = (160u * 1024 - 16) / (kBinSmall * 2 + 8);       // 2275 (m <= ~149M bits)
+constexpr double kBinMeanPos[2] = {20.0, 25.0};  // positions per bucket per round, at most (32 / 48 slots)
 
 __device__ __forceinline__ void bins_overflow_or(uint32_t *ovw, uint32_t b, uint32_t l) {
     const uint32_t p = (b << kBktShift) | l;
     __hip_atomic_fetch_or(ovw + (p >> 5), 1u << (p & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <typename Src, int THREADS, int KPT, uint32_t PAD>
+template <typename Src, int THREADS, int KPT, uint32_t SB>
 __global__ __launch_bounds__(THREADS) void k_bkt_scatter_bins(Src src, uint64_t n, ModArg md, uint32_t nb,
                                                               uint32_t tile_keys, uint32_t round_keys, uint32_t ntiles,
                                                               uint32_t cap, uint16_t *__restrict__ regions,
                                                               uint32_t *__restrict__ counts, uint32_t *__restrict__ ovw) {
     extern __shared__ uint4 smem4[];
-    constexpr uint32_t S = kBinSlots, CH = S / 8;
-    static_assert(64 % CH == 0, "a bucket's chunks must sit in one wave");
-    uint16_t *bins = (uint16_t *)smem4;                      // 16-B aligned chunks
-    uint32_t *cnt = (uint32_t *)(bins + (size_t)nb * S);
-    uint32_t *fill = cnt + nb;
-    const uint32_t t = blockIdx.x;
-    for (uint32_t b = threadIdx.x; b < nb; b += THREADS) {
-        cnt[b] = 0u;
-        fill[b] = 0u;
-    }
-    __syncthreads();
-    const uint64_t t0 = (uint64_t)t * tile_keys;
-    const uint64_t t1 = t0 + tile_keys < n ? t0 + tile_keys : n;
-    constexpr bool kPre = SplitLoad<Src>::value;
-    uint4 kv[kPre ? KPT : 1];
-    auto prefetch = [&](uint64_t r0) {
-        if constexpr (kPre) {
-            const uint64_t r1 = r0 + round_keys < t1 ? r0 + round_keys : t1;
-#pragma unroll
-            for (int r = 0; r < KPT; ++r) {
-                const uint64_t i = r0 + (uint64_t)r * THREADS + threadIdx.x;
-                if (i < r1) kv[r] = src.load(i);
-            }
-        }
-    };
-    prefetch(t0);
-    for (uint64_t k0 = t0; k0 < t1; k0 += round_keys) {
-        const uint64_t k1 = k0 + round_keys < t1 ? k0 + round_keys : t1;
-        uint32_t pos[KPT][7];
-        bool valid[KPT];
-#pragma unroll
-        for (int r = 0; r < KPT; ++r) {
-            const uint64_t i = k0 + (uint64_t)r * THREADS + threadIdx.x;
-            valid[r] = i < k1;
-            if (valid[r]) {
-                if constexpr (IsPacked<Src>::value) {
-                    packed_positions((uint64_t)kv[r].x | (uint64_t)kv[r].y << 32, (uint32_t)md.m, (uint32_t)md.c,
-                                     pos[r]);
-                } else {
-                    uint64_t h1, h2;
-                    if constexpr (kPre)
-                        Src::hash_raw(kv[r], h1, h2);
-                    else
-                        src.hash(i, h1, h2);
-                    for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
-                }
-            }
-        }
-        // all claims first (the returning atomics pipeline), then the bin writes
-        uint32_t slot[KPT][7];
-#pragma unroll
-        for (int r = 0; r < KPT; ++r)
-            if (valid[r]) {
-#pragma unroll
-                for (int q = 0; q < 7; ++q) slot[r][q] = atomicAdd(&cnt[pos[r][q] >> kBktShift], 1u);
-            }
-        // bin writes; a claim past its bin (rare) is only noted here and stored below, so the
-        // common path has no branch that would drain the pipelined claims
-        uint64_t past = 0;
-#pragma unroll
-        for (int r = 0; r < KPT; ++r)
-            if (valid[r]) {
-#pragma unroll
-                for (int q = 0; q < 7; ++q) {
-                    const uint32_t p = pos[r][q], s = slot[r][q];
-                    // branch-free: a claim past the bin writes a scratch word instead
-                    bins[s < S ? (p >> kBktShift) * S + s : nb * S + 4 * nb] = (uint16_t)p;
-                    past |= (uint64_t)(s >= S) << (r * 7 + q);
-                }
-            }
-        while (past) {  // straight to the region slot (the fill is fixed this round)
-            const int i = __builtin_ctzll(past);
-            past &= past - 1;
-            uint32_t p = 0, s = 0;
-#pragma unroll
-            for (int r = 0; r < KPT; ++r)
-#pragma unroll
-                for (int q = 0; q < 7; ++q)
-                    if (r * 7 + q == i) {
-                        p = pos[r][q];
-                        s = slot[r][q];
-                    }
-            const uint32_t b = p >> kBktShift, e = fill[b] + s;
-            if (e < cap)
-                regions[(uint64_t)(b * ntiles + t) * cap + e] = (uint16_t)p;
-            else
-                bins_overflow_or(ovw, b, p & 0xffffu);
-        }
-        if (k1 < t1) prefetch(k1);  // the next round's keys load during the write-out
-        __syncthreads();
-        // write-out: chunk j of bucket b is lane idx = b * CH + j
-        for (uint32_t idx = threadIdx.x; idx < nb * CH; idx += THREADS) {
-            const uint32_t b = idx / CH, j = idx % CH;
-            const uint32_t c = cnt[b], f = fill[b];  // f: region fill, a multiple of PAD
-            const uint64_t base = (uint64_t)(b * ntiles + t) * cap;
-            if (j * 8 < c) {
-                uint4 w = *(const uint4 *)(bins + b * S + j * 8);
-                const uint32_t live = c - j * 8;  // valid indices in this chunk (>= 1)
-                const uint32_t e0 = w.x & 0xffffu;
-                uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-                if (live < 8) {  // pad with the chunk's first index
-#pragma unroll
-                    for (uint32_t i = 0; i < 4; ++i) {
-                        if (PAD == 8 && 2 * i >= live)
-                            ww[i] = e0 | (e0 << 16);
-                        else if (2 * i + 1 == live || (PAD == 8 && 2 * i + 1 > live))
-                            ww[i] = (ww[i] & 0xffffu) | (e0 << 16);
-                    }
-                }
-                const uint32_t e = f + j * 8;
-                const uint32_t len = PAD == 8 ? 8u : (live < 8 ? (live + 1) & ~1u : 8u);  // u16 stored
-                if (e + len <= cap) {
-                    if (PAD == 8 || len == 8) {
-                        struct __attribute__((aligned(4))) U4 { uint32_t a, b, c, d; };
-                        *(U4 *)(regions + base + e) = U4{ww[0], ww[1], ww[2], ww[3]};  // 16-B (PAD 8) or 4-B aligned
-                    } else {
-                        uint32_t *d = (uint32_t *)(regions + base + e);
-#pragma unroll
-                        for (uint32_t i = 0; i < 3; ++i)
-                            if (2 * i < len) d[i] = ww[i];
-                    }
-                } else {
-#pragma unroll
-                    for (uint32_t i = 0; i < 8; ++i)
-                        if (i < len) {
-                            const uint16_t v = (uint16_t)(ww[i >> 1] >> ((i & 1) * 16));
-                            if (e + i < cap)
-                                regions[base + e + i] = v;
-                            else
-                                bins_overflow_or(ovw, b, v);
-                        }
-                }
-            }
-            if (j == 0) {  // the quad's other lanes read cnt[b] and fill[b] above, in this wave
-                const uint32_t padded = (c + (PAD - 1)) & ~(PAD - 1);
-                if (c > S) {  // a run past its bin: pad its tail in the region
-                    const uint16_t d = bins[b * S];
-                    for (uint32_t e = f + c; e < f + padded; ++e)
-                        if (e < cap) regions[base + e] = d;
-                }
-                cnt[b] = 0u;
-                fill[b] = f + padded;
-            }
-        }
-        __syncthreads();
-    }
-    for (uint32_t b = threadIdx.x; b < nb; b += THREADS) counts[(uint64_t)b * ntiles + t] = fill[b];
-}
-
-template <typename Src, int THREADS, int KPT, uint32_t PAD, uint32_t SB>
-__global__ __launch_bounds__(THREADS) void k_bkt_scatter_pipe(Src src, uint64_t n, ModArg md, uint32_t nb,
-                                                              uint32_t tile_keys, uint32_t round_keys, uint32_t ntiles,
-                                                              uint32_t cap, uint16_t *__restrict__ regions,
-                                                              uint32_t *__restrict__ counts, uint32_t *__restrict__ ovw) {
-    extern __shared__ uint4 smem4[];
-    constexpr uint32_t S = SB;
+    constexpr uint32_t S = SB, PAD = 8;
     static_assert(S % 8 == 0 && S <= 64, "a bucket's chunks must sit in one wave");
     uint16_t *bins = (uint16_t *)smem4;                      // 16-B aligned chunks
     uint32_t *cnt = (uint32_t *)(bins + (size_t)nb * S);
@@ -502,7 +352,7 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter_pipe(Src src, uint64_t 
             for (uint32_t b0 = (threadIdx.x >> 6) * BPW; b0 < nb; b0 += NW * BPW) {
                 const uint32_t b = b0 + g;
                 if (g >= BPW || b >= nb) continue;
-                const uint32_t c = cnt[b], f = fill[b];  // f: region fill, a multiple of PAD
+                const uint32_t c = cnt[b], f = fill[b];  // f: region fill, a multiple of 8
                 const uint32_t rb = (b * ntiles + t) * cap;  // region start (< 2^31, host-checked)
                 if (j * 8 < c) {
                     const uint4 w = *(const uint4 *)(bins + b * S + j * 8);
@@ -510,35 +360,14 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter_pipe(Src src, uint64_t 
                     uint32_t ww[4] = {w.x, w.y, w.z, w.w};
                     const uint32_t e0 = w.x & 0xffffu, hi0 = e0 << 16;
 #pragma unroll
-                    for (uint32_t i = 0; i < 4; ++i) {  // pad with the chunk's first index
-                        const uint32_t half = (ww[i] & 0xffffu) | hi0;
-                        if (PAD == 8)
-                            ww[i] = 2 * i + 1 < live ? ww[i] : 2 * i < live ? half : (e0 | hi0);
-                        else
-                            ww[i] = 2 * i + 1 == live ? half : ww[i];
-                    }
-                    const uint32_t e = f + j * 8;
-                    const uint32_t len = PAD == 8 || live >= 8 ? 8u : (live + 1) & ~1u;  // u16 stored
-                    uint16_t *dst = regions + rb + e;
-                    if (e + len <= cap) {
-                        if (PAD == 8 || len == 8) {
-                            struct __attribute__((aligned(4))) U4 { uint32_t a, b, c, d; };
-                            *(U4 *)dst = U4{ww[0], ww[1], ww[2], ww[3]};  // 16-B (PAD 8) or 4-B aligned
-                        } else {
+                    for (uint32_t i = 0; i < 4; ++i)  // pad with the chunk's first index
+                        ww[i] = 2 * i + 1 < live ? ww[i] : 2 * i < live ? (ww[i] & 0xffffu) | hi0 : e0 | hi0;
+                    const uint32_t e = f + j * 8;  // f and cap are multiples of 8: a chunk fits whole or not at all
+                    if (e < cap) {
+                        *(uint4 *)(regions + rb + e) = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+                    } else {  // the region is full: the run's bits by atomics
 #pragma unroll
-                            for (uint32_t i = 0; i < 3; ++i)
-                                if (2 * i < len) ((uint32_t *)dst)[i] = ww[i];
-                        }
-                    } else {  // the region is full: the rest of its bits by atomics
-#pragma unroll
-                        for (uint32_t i = 0; i < 8; ++i)
-                            if (i < len) {
-                                const uint16_t v = (uint16_t)(ww[i >> 1] >> ((i & 1) * 16));
-                                if (e + i < cap)
-                                    dst[i] = v;
-                                else
-                                    bins_overflow_or(ovw, b, v);
-                            }
+                        for (uint32_t i = 0; i < 8; ++i) bins_overflow_or(ovw, b, (ww[i >> 1] >> ((i & 1) * 16)) & 0xffffu);
                     }
                 }
                 if (j == 0) {
@@ -564,7 +393,8 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter_pipe(Src src, uint64_t 
 // instead, and a bucket whose runs overflowed folds in (and re-zeroes) its words of the overflow
 // bitmap `ovf`, which is all zero between builds.  PADDED: the runs were written by
 // k_bkt_scatter_bins, whole 16-B chunks, so a region's count is a multiple of 8 and every index
-// below it is valid.
+// below it is valid (a chunk's padding repeats its first index; skipping it by a compare measured
+// slower than OR-ing it: apply 43.0 vs 41.7 us, tools/diag/apply_or_padding.patch reversed).
 template <int THREADS, bool FRESH, bool PADDED = false>
 __global__ __launch_bounds__(THREADS) void k_bkt_apply(const uint16_t *__restrict__ regions,
                                                    const uint32_t *__restrict__ counts, uint32_t ntiles, uint32_t cap,
@@ -602,7 +432,7 @@ __global__ __launch_bounds__(THREADS) void k_bkt_apply(const uint16_t *__restric
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (uint32_t e = 0; e < 8; ++e)
-                if (PADDED || c * 8 + e < valid) {
+                if (PADDED || c * 8 + e < valid) {  // PADDED: the padding ORs its chunk's first bit again
                     const uint32_t l = (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
                     atomicOr(&img[l >> 5], 1u << (l & 31));
                 }
@@ -634,19 +464,17 @@ __global__ __launch_bounds__(THREADS) void k_bkt_apply(const uint16_t *__restric
 struct BktPlan {
     uint32_t nb, tile_keys, ntiles, cap;  // a region of cap u16 per (bucket, tile)
     uint32_t round_keys;
-    bool bins;                            // k_bkt_scatter_bins
-    uint32_t pad;                         // its runs' multiple: 8 (padded apply) or 2
-    uint32_t kpt;
-    uint32_t sb;                          // u16 slots per bin
+    uint32_t bins;                        // k_bkt_scatter_bins' slots per bin (48 or 32), 0: the counting sort
     uint64_t off_regions, off_counts, bytes;
 };
 
 // The fixed-bin scatter takes k == 7 filters of kBinMinBuckets..kBinMaxBuckets buckets.
-static bool bins_fit(uint64_t m, uint32_t k) {
+static uint32_t bin_slots(uint64_t m, uint32_t k) {
     const uint64_t nb = ((m + 31) / 32 + kBktWords - 1) / kBktWords;
-    return k == 7 && nb >= kBinMinBuckets && nb <= kBinMaxBuckets;
+    if (k != 7 || nb < kBinMinBuckets || nb > kBinMaxBuckets) return 0;
+    return nb <= kBinBigMaxBuckets ? kBinBig : kBinSmall;
 }
-static bool use_bins(uint64_t m, uint32_t k) { return options().scatter_bins && bins_fit(m, k); }
+static uint32_t use_bins(uint64_t m, uint32_t k) { return options().scatter_bins ? bin_slots(m, k) : 0; }
 
 // One 1024-thread scatter workgroup per CU (two of 512 measured slower).
 constexpr uint32_t kScatterThreads = 1024;
@@ -656,22 +484,18 @@ static uint32_t scatter_kpt(uint32_t nb) {
     return ((uint64_t)kScatterThreads * 5 * 7 + 2 * nb + 17) * 4 <= 160u * 1024 ? 5u : 4u;
 }
 
-static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k, bool bins) {
+static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k, uint32_t bins) {
     BktPlan p{};
     const uint64_t nwords = (m + 31) / 32;
     p.nb = (uint32_t)((nwords + kBktWords - 1) / kBktWords);
     p.bins = bins;
-    const int sbo = options().scatter_bins;
-    p.pad = (sbo == 2 || sbo == 3 || sbo == 5 || sbo == 7) ? 2u : 8u;
-    p.sb = (sbo >= 4 && p.nb <= (160u * 1024 - 16) / (48 * 2 + 8)) ? 48u : 32u;
     const uint32_t thr = kScatterThreads;
-    const uint32_t kpt = bins ? (options().scatter_bins == 3 ? 4u : options().scatter_bins >= 6 ? 6u : 5u) : scatter_kpt(p.nb);
-    p.kpt = kpt;
+    const uint32_t kpt = bins ? 5u : scatter_kpt(p.nb);
     const uint32_t pos = thr * kpt * 7;
     uint32_t round_keys = k == 7 ? kpt * thr : pos / k;
-    if (bins) {  // a round's mean run stays below the bin: <= kBinMeanPos positions per bucket
-        const double mean_cap = options().scatter_bins >= 6 ? 30.0 : (double)kBinMeanPos;
-        const uint64_t most = (uint64_t)(mean_cap * (double)m / (double)(1u << kBktShift) / k);
+    if (bins) {  // a round's mean run stays well below the bin
+        const double mean = kBinMeanPos[bins == kBinBig];
+        const uint64_t most = (uint64_t)(mean * (double)m / (double)(1u << kBktShift) / k);
         if (most < round_keys) round_keys = (uint32_t)(most > 64 ? most : 64);
     }
     p.round_keys = round_keys;
@@ -687,7 +511,7 @@ static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k, bool bins) {
     double c = mu + 8.0 * sqrt(mu > 1 ? mu : 1) + 32.0;
     const double most = rkeys * k;  // never more than every position of the tile
     if (c > most) c = most;
-    if (bins) c += (double)(p.pad - 1) * (double)rounds_per_tile;  // each round's run padded to a multiple of pad
+    if (bins) c += 7.0 * (double)rounds_per_tile;  // each round's run padded to a multiple of 8
     p.cap = ((uint32_t)c + 7) & ~7u;
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
     p.off_regions = 0;
@@ -710,8 +534,9 @@ uint64_t bucketed_workspace_bytes(uint64_t n, uint64_t m, uint32_t k) {
     const uint64_t cap = bucketed_max_keys(k);
     const uint64_t nn = n < cap ? n : cap;
     // either scatter may run (scatter_bins can change between the query and the build)
-    const uint64_t a = plan_bucketed(nn, m, k, false).bytes;
-    const uint64_t b = bins_fit(m, k) ? plan_bucketed(nn, m, k, true).bytes : 0;
+    const uint64_t a = plan_bucketed(nn, m, k, 0).bytes;
+    const uint32_t sl = bin_slots(m, k);
+    const uint64_t b = sl ? plan_bucketed(nn, m, k, sl).bytes : 0;
     return a > b ? a : b;
 }
 
@@ -737,21 +562,19 @@ static hipError_t run_bucketed(uint64_t n, const ModArg &md, uint32_t *words, vo
         hipError_t e = chunk(k0, sn, [&](auto src) -> hipError_t {
             using S = decltype(src);
             if (p.bins) {
-                auto scat = p.sb == 48 && p.kpt == 6 ? (p.pad == 8 ? k_bkt_scatter_pipe<S, kScatterThreads, 6, 8, 48>
-                                                                : k_bkt_scatter_pipe<S, kScatterThreads, 6, 2, 48>)
-                            : p.sb == 48 ? (p.pad == 8 ? k_bkt_scatter_pipe<S, kScatterThreads, 5, 8, 48>
-                                                     : k_bkt_scatter_pipe<S, kScatterThreads, 5, 2, 48>)
-                            : p.pad == 8 ? k_bkt_scatter_bins<S, kScatterThreads, 5, 8>
-                            : p.kpt == 4 ? k_bkt_scatter_bins<S, kScatterThreads, 4, 2> : k_bkt_scatter_bins<S, kScatterThreads, 5, 2>;
-                const size_t blds = (size_t)p.nb * (p.sb * 2 + 8) + 16;  // + the scratch word
+                auto scat = p.bins == kBinBig ? k_bkt_scatter_bins<S, kScatterThreads, 5, kBinBig>
+                                              : k_bkt_scatter_bins<S, kScatterThreads, 5, kBinSmall>;
+                const size_t blds = bin_lds_bytes(p.nb, p.bins);
                 hipError_t a = hipFuncSetAttribute((const void *)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);
                 if (a != hipSuccess) return a;
                 hipLaunchKernelGGL(scat, dim3(p.ntiles), dim3(kScatterThreads), blds, s, src, sn, md, p.nb, p.tile_keys,
                                    p.round_keys, p.ntiles, p.cap, regions, counts, fresh ? ovf : words);
-                auto ap = fresh ? (p.pad == 8 ? k_bkt_apply<1024, true, true> : k_bkt_apply<1024, true, false>)
-                                : (p.pad == 8 ? k_bkt_apply<1024, false, true> : k_bkt_apply<1024, false, false>);
-                hipLaunchKernelGGL(ap, dim3(p.nb), dim3(1024), 0, s, regions, counts, p.ntiles, p.cap, words,
-                                   fresh ? (md.m + 127) / 128 * 4 : nwords, fresh ? ovf : nullptr);
+                if (fresh)
+                    hipLaunchKernelGGL((k_bkt_apply<1024, true, true>), dim3(p.nb), dim3(1024), 0, s, regions, counts,
+                                       p.ntiles, p.cap, words, (md.m + 127) / 128 * 4, ovf);
+                else
+                    hipLaunchKernelGGL((k_bkt_apply<1024, false, true>), dim3(p.nb), dim3(1024), 0, s, regions, counts,
+                                       p.ntiles, p.cap, words, nwords, nullptr);
                 return hipGetLastError();
             }
             constexpr int K0 = IsPacked<S>::value ? 7 : 0;  // packed sources have no generic-k kernel

@@ -1659,7 +1659,7 @@ def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
         seb.set_option("build_algo", 0)
 
 
-@pytest.mark.parametrize("bins", [1, 2, 3, 4, 5, 6, 7, 0], ids=["bins8", "bins2", "bins2k4", "pipe8", "pipe2", "pipe8k6", "pipe2k6", "counting"])
+@pytest.mark.parametrize("bins", [1, 0], ids=["bins", "counting"])
 @pytest.mark.parametrize("case", ["nb513", "c2m", "nb2274", "duplicates", "skewed"])
 def test_bucketed_scatter_bins(seb, torch_cuda, case, bins):
     """The radix-partitioned build's two scatters (scatter_bins 1: fixed LDS bins, runs padded to
