@@ -257,7 +257,7 @@ __device__ __forceinline__ void bins_overflow_or(uint32_t *ovw, uint32_t b, uint
     __hip_atomic_fetch_or(ovw + (p >> 5), 1u << (p & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <typename Src, int THREADS, int KPT, uint32_t SB>
+template <typename Src, int THREADS, int KPT, uint32_t SB, int G = 1>
 __global__ __launch_bounds__(THREADS) void k_bkt_scatter_bins(Src src, uint64_t n, ModArg md, uint32_t nb,
                                                               uint32_t tile_keys, uint32_t round_keys, uint32_t ntiles,
                                                               uint32_t cap, uint16_t *__restrict__ regions,
@@ -291,11 +291,14 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter_bins(Src src, uint64_t 
     prefetch(t0);  // later rounds load key by key, in the pipeline below
     for (uint64_t k0 = t0; k0 < t1; k0 += round_keys) {
         const uint64_t k1 = k0 + round_keys < t1 ? k0 + round_keys : t1;
-        // software pipeline over the thread's keys: hash key r and issue its 7 slot claims, then
-        // write key r-1's bins (its claims returned while key r hashed), so the returning LDS
-        // atomics overlap the hashing instead of following it
-        uint32_t pp[7], ps[7];
-        bool pvalid = false;
+        // software pipeline over the thread's keys, G at a time: hash keys r..r+G-1 and issue
+        // their slot claims, then write the previous G keys' bins (their claims returned while
+        // these hashed), so the returning LDS atomics overlap the hashing instead of following it
+        constexpr int NSTEP = (KPT + G - 1) / G;
+        uint32_t pp[G][7], ps[G][7];
+        bool pv[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) pv[g] = false;
         auto write_bins = [&](const uint32_t (&pw)[7], const uint32_t (&sw)[7]) {
 #pragma unroll
             for (int q = 0; q < 7; ++q) {
@@ -311,37 +314,56 @@ __global__ __launch_bounds__(THREADS) void k_bkt_scatter_bins(Src src, uint64_t 
             }
         };
 #pragma unroll
-        for (int r = 0; r < KPT; ++r) {
-            const uint64_t i = k0 + (uint64_t)r * THREADS + threadIdx.x;
-            const bool valid = i < k1;
-            uint32_t pos[7], sl[7];
-            if (valid) {
-                if constexpr (IsPacked<Src>::value) {
-                    packed_positions((uint64_t)kv[r].x | (uint64_t)kv[r].y << 32, (uint32_t)md.m, (uint32_t)md.c, pos);
-                } else {
-                    uint64_t h1, h2;
-                    if constexpr (kPre)
-                        Src::hash_raw(kv[r], h1, h2);
-                    else
-                        src.hash(i, h1, h2);
-                    for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[q] = (uint32_t)p; });
+        for (int st = 0; st < NSTEP; ++st) {
+            uint32_t pos[G][7], sl[G][7];
+            bool valid[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {  // independent chains, hashed side by side (kv is always loadable)
+                const int r = st * G + g;
+                const uint64_t i = k0 + (uint64_t)r * THREADS + threadIdx.x;
+                valid[g] = r < KPT && i < k1;
+                if (r < KPT && (kPre || valid[g])) {
+                    if constexpr (IsPacked<Src>::value) {
+                        packed_positions((uint64_t)kv[r].x | (uint64_t)kv[r].y << 32, (uint32_t)md.m, (uint32_t)md.c,
+                                         pos[g]);
+                    } else {
+                        uint64_t h1, h2;
+                        if constexpr (kPre)
+                            Src::hash_raw(kv[r], h1, h2);
+                        else
+                            src.hash(i, h1, h2);
+                        for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[g][q] = (uint32_t)p; });
+                    }
                 }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int r = st * G + g;
+                if (r >= KPT) continue;
+                const uint64_t i = k0 + (uint64_t)r * THREADS + threadIdx.x;
                 if constexpr (kPre) {  // this key's register now loads the next round's key r
                     const uint64_t in = i + round_keys;
-                    if (k1 < t1 && in < (k1 + round_keys < t1 ? k1 + round_keys : t1)) kv[r] = src.load(in);
+                    if (valid[g] && k1 < t1 && in < (k1 + round_keys < t1 ? k1 + round_keys : t1)) kv[r] = src.load(in);
                 }
+                if (valid[g]) {
 #pragma unroll
-                for (int q = 0; q < 7; ++q) sl[q] = atomicAdd(&cnt[pos[q] >> kBktShift], 1u);
+                    for (int q = 0; q < 7; ++q) sl[g][q] = atomicAdd(&cnt[pos[g][q] >> kBktShift], 1u);
+                }
             }
-            if (pvalid) write_bins(pp, ps);
 #pragma unroll
-            for (int q = 0; q < 7; ++q) {
-                pp[q] = pos[q];
-                ps[q] = sl[q];
+            for (int g = 0; g < G; ++g) {
+                if (pv[g]) write_bins(pp[g], ps[g]);
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    pp[g][q] = pos[g][q];
+                    ps[g][q] = sl[g][q];
+                }
+                pv[g] = valid[g];
             }
-            pvalid = valid;
         }
-        if (pvalid) write_bins(pp, ps);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+            if (pv[g]) write_bins(pp[g], ps[g]);
         __syncthreads();
         // write-out: a bucket's S/8 chunks on S/8 adjacent lanes of one wave (64/(S/8) buckets per
         // wave; with S = 48, lanes 60-63 idle), so the lane that advances the bucket's fill runs in
@@ -562,6 +584,7 @@ static hipError_t run_bucketed(uint64_t n, const ModArg &md, uint32_t *words, vo
         hipError_t e = chunk(k0, sn, [&](auto src) -> hipError_t {
             using S = decltype(src);
             if (p.bins) {
+                // (two keys per pipeline step, G = 2: scatter 138.6 vs 137.9 us, not kept)
                 auto scat = p.bins == kBinBig ? k_bkt_scatter_bins<S, kScatterThreads, 5, kBinBig>
                                               : k_bkt_scatter_bins<S, kScatterThreads, 5, kBinSmall>;
                 const size_t blds = bin_lds_bytes(p.nb, p.bins);

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 4 (session 2): bin scatter hashing 1 or 2 keys per pipeline step; PMC of the default.
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$ROOT"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py \
+    -k "scatter_bins or fresh_build or c2_c3_10m" > gpurun_out/r4n_tests.log 2>&1 || { tail -30 gpurun_out/r4n_tests.log; exit 1; }
+tail -2 gpurun_out/r4n_tests.log
+bash tools/gpu_ab_env.sh g2 "SEB_SCATTER_BINS=1" "SEB_SCATTER_BINS=2" || exit 1
+bash tools/gpu_pmc_env.sh g2 "SEB_SCATTER_BINS=1" "SEB_SCATTER_BINS=2"
