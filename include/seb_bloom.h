@@ -88,6 +88,9 @@ int seb_abi_version(void);
  *                     (0 = one per 4 MiB of filter; 1 = the single-launch sliced probe)
  *   "probe_compact"   phased probe: later phases read only the live keys' packed words, kept
  *                     compacted per 64-key group (1, default), or every key's (0)
+ *   "scatter_bins"    radix-partitioned build, k == 7, 512-2275 buckets (m ~ 33.5M-149M bits):
+ *                     positions placed through fixed per-bucket LDS bins, the claims pipelined
+ *                     against the hashing (1, default), or by a counting sort (0)
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
  *   "multiget_order"  registry MultiGet walks batches of >= 64K keys in key-range order (1, default)
  *                     or batch order (0)
