@@ -1701,6 +1701,39 @@ def test_bucketed_scatter_bins(seb, torch_cuda, case, bins):
         assert np.array_equal(seb.words_to_bits(w2, m), ref), (case, bins)
 
 
+@pytest.mark.parametrize("bins", [1, 0], ids=["bins", "counting"])
+@pytest.mark.parametrize("src", ["stride20", "stride13", "varlen_direct", "varlen_prehash"])
+def test_bucketed_scatter_key_sources(seb, torch_cuda, src, bins):
+    """Both scatters over every key source the radix-partitioned build reads at a filter size the
+    bins take (95.85M bits, 1463 buckets): 4-B-aligned strided keys, byte-strided keys, and
+    variable-length keys walked per lane or pre-hashed into packed residues; against the oracle."""
+    torch = torch_cuda
+    n, m, k = 300_001, 95_850_584, 7
+    idx = np.random.default_rng(5).permutation(4 * n)[:n]
+    if src.startswith("stride"):
+        stride = int(src[6:])
+        base = kg.key16(idx)
+        host = np.zeros((n, stride), np.uint8)
+        host[:, : min(16, stride)] = base[:, : min(16, stride)]
+        host[:, min(16, stride):] = (idx[:, None] * 7 + np.arange(stride - min(16, stride))) % 251
+        ref = oc.build(m, k, np.ascontiguousarray(host).ravel(), n, stride=stride)
+        kd = seb.dev_keys(to_dev(torch, host.ravel()), n=n, stride=stride)
+    else:
+        data, off = kg.varlen_keys(idx)
+        ref = oc.build(m, k, data, n, offsets=off)
+        kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off.astype(np.int64)))
+    prehash = 0 if src == "varlen_prehash" else 1 << 40
+    with seb.option("build_algo", 2), seb.option("scatter_bins", bins), \
+            seb.option("varlen_prehash_min_keys", prehash):
+        words = seb.new_words(m)
+        words.view(torch.uint8).fill_(0x3C)
+        seb.dev_build_fresh(kd, words, m, k)
+        torch.cuda.synchronize()
+        raw = words.cpu().numpy().view(np.uint8)
+        assert np.array_equal(raw[: (m + 7) // 8], ref), (src, bins)
+        assert not raw[(m + 7) // 8:].any()
+
+
 @pytest.mark.parametrize("algo", [0, 1, 2, 3, 4])
 def test_fresh_build_overwrites_garbage(seb, golden, torch_cuda, algo):
     """seb_dev_build_fresh: words full of garbage (never cleared) become the filter of the keys, bit
