@@ -168,20 +168,10 @@ __global__ __launch_bounds__(256) void k_probe_sliced_emit(Src src, uint64_t n, 
             const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
             uint64_t h1 = 0, h2 = 0;
             if (i < n) src.hash(i, h1, h2);
-            for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
+            const uint64_t pw = pack_residue(h1, h2, md);  // each residue and wrap flag once
+            packed_positions(pw, (uint32_t)md.m, (uint32_t)md.c, pos[r]);
             acc[r] = i < n ? 1u : 0u;
-            if (i < n) {
-                uint64_t f = 0, x = h1;
-#pragma unroll
-                for (uint32_t q = 1; q < 7; ++q) {
-                    const uint64_t xn = x + h2;
-                    f |= (uint64_t)(xn < x) << (q - 1);
-                    x = xn;
-                }
-                const uint64_t b = mod_m31(h2, (uint32_t)md.m, md.mu);
-                __builtin_nontemporal_store((uint64_t)pos[r][0] | (b << kPackBits) | (f << (2 * kPackBits)),
-                                            packed + src.index(i));
-            }
+            if (i < n) __builtin_nontemporal_store(pw, packed + src.index(i));
         }
         for (uint32_t sl = 0; sl < nslices; ++sl) {
 #pragma unroll
@@ -225,20 +215,10 @@ __global__ __launch_bounds__(kPhaseBlock) void k_probe_phase0(Src src, uint64_t 
             const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
             uint64_t h1 = 0, h2 = 0;
             if (i < n) src.hash(i, h1, h2);
-            for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[r][q] = (uint32_t)p; });
+            const uint64_t pw = pack_residue(h1, h2, md);  // each residue and wrap flag once
+            packed_positions(pw, (uint32_t)md.m, (uint32_t)md.c, pos[r]);
             acc[r] = i < n ? 1u : 0u;
-            if (i < n) {
-                uint64_t f = 0, x = h1;
-#pragma unroll
-                for (uint32_t q = 1; q < 7; ++q) {
-                    const uint64_t xn = x + h2;
-                    f |= (uint64_t)(xn < x) << (q - 1);
-                    x = xn;
-                }
-                const uint64_t b = mod_m31(h2, (uint32_t)md.m, md.mu);
-                __builtin_nontemporal_store((uint64_t)pos[r][0] | (b << kPackBits) | (f << (2 * kPackBits)),
-                                            packed + i);
-            }
+            if (i < n) __builtin_nontemporal_store(pw, packed + i);
         }
 #pragma unroll
         for (int r = 0; r < KPT; ++r)
@@ -339,18 +319,11 @@ __global__ __launch_bounds__(kPhaseBlock) void k_probe_c0(Src src, uint64_t n, c
             const uint4 v = i < n ? src.load(i) : make_uint4(0u, 0u, 0u, 0u);
             pw = (uint64_t)v.x | (uint64_t)v.y << 32;
             packed_positions(pw, (uint32_t)md.m, (uint32_t)md.c, pos);
-        } else {
+        } else {  // the packed word first, the positions from it: each residue and wrap flag once
             uint64_t h1 = 0, h2 = 0;
             if (i < n) src.hash(i, h1, h2);
-            for_positions<7, true>(h1, h2, md, 7, [&](uint32_t q, uint64_t p) { pos[q] = (uint32_t)p; });
-            uint64_t f = 0, x = h1;
-#pragma unroll
-            for (uint32_t q = 1; q < 7; ++q) {
-                const uint64_t xn = x + h2;
-                f |= (uint64_t)(xn < x) << (q - 1);
-                x = xn;
-            }
-            pw = (uint64_t)pos[0] | ((uint64_t)mod_m31(h2, (uint32_t)md.m, md.mu) << kPackBits) | (f << (2 * kPackBits));
+            pw = pack_residue(h1, h2, md);
+            packed_positions(pw, (uint32_t)md.m, (uint32_t)md.c, pos);
         }
         uint32_t acc = i < n ? 1u : 0u;
 #pragma unroll
