@@ -449,19 +449,36 @@ __global__ __launch_bounds__(THREADS) void k_bkt_apply(const uint16_t *__restric
     const uint32_t chunks = (longest + 7) / 8;
     const uint32_t pairs = ntiles * chunks;
     const uint4 *reg = (const uint4 *)(regions + (uint64_t)b * ntiles * cap);
-#pragma unroll 4
-    for (uint32_t q = threadIdx.x; q < pairs; q += blockDim.x) {
-        const uint32_t t = q / chunks, c = q - t * chunks;
-        const uint32_t valid = cnt[t];
-        if (c * 8 < valid) {
-            const uint4 v = reg[t * stride + c];
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    // U chunk loads in flight per thread: they are issued before any count is consulted (every
+    // chunk below the longest region lies inside its region's capacity, so a load past a shorter
+    // region's count is in bounds and is simply not used); checking the count first put one load
+    // per wave in flight at a time
+    constexpr uint32_t U = 4;
+    for (uint32_t q0 = threadIdx.x; q0 < pairs; q0 += U * THREADS) {
+        uint4 v[U];
 #pragma unroll
-            for (uint32_t e = 0; e < 8; ++e)
-                if (PADDED || c * 8 + e < valid) {  // PADDED: the padding ORs its chunk's first bit again
-                    const uint32_t l = (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
-                    atomicOr(&img[l >> 5], 1u << (l & 31));
-                }
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t q = q0 + u * THREADS;
+            if (q < pairs) {
+                const uint32_t t = q / chunks, c = q - t * chunks;
+                v[u] = reg[t * stride + c];
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t q = q0 + u * THREADS;
+            if (q >= pairs) break;
+            const uint32_t t = q / chunks, c = q - t * chunks;
+            const uint32_t valid = cnt[t];
+            if (c * 8 < valid) {
+                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (uint32_t e = 0; e < 8; ++e)
+                    if (PADDED || c * 8 + e < valid) {  // PADDED: the padding ORs its chunk's first bit again
+                        const uint32_t l = (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+                        atomicOr(&img[l >> 5], 1u << (l & 31));
+                    }
+            }
         }
     }
     __syncthreads();
