@@ -541,11 +541,15 @@ static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k, uint32_t bins) 
         const uint64_t most = (uint64_t)(mean * (double)m / (double)(1u << kBktShift) / k);
         if (most < round_keys) round_keys = (uint32_t)(most > 64 ? most : 64);
     }
-    p.round_keys = round_keys;
     const uint32_t target = kTargetTiles;
     uint64_t rounds_total = (n + round_keys - 1) / round_keys;
     uint64_t rounds_per_tile = (rounds_total + target - 1) / target;
     if (rounds_per_tile < 1) rounds_per_tile = 1;
+    if (bins && options().scatter_tiles_exact) {  // shrink the rounds so the tiles fill every CU
+        const uint64_t rk = (n + target * rounds_per_tile - 1) / (target * rounds_per_tile);
+        if (rk >= 64 && rk < round_keys) round_keys = (uint32_t)rk;
+    }
+    p.round_keys = round_keys;
     p.tile_keys = (uint32_t)(rounds_per_tile * round_keys);
     p.ntiles = (uint32_t)((n + p.tile_keys - 1) / p.tile_keys);
     // positions of one tile landing in one (full) bucket: mean + 8 sigma + 32, 8-aligned

@@ -138,6 +138,7 @@ static const OptionDesc kOptions[] = {
     SEB_OPT(probe_phases, 0, 64),
     SEB_OPT(probe_compact, 0, 1),
     SEB_OPT(scatter_bins, 0, 1),
+    SEB_OPT(scatter_tiles_exact, 0, 1),
     SEB_OPT(grid_cap, 1, 1 << 30),
     SEB_OPT(workspace_limit_mib, 0, 1 << 30),
     SEB_OPT(varlen_tail, 0, 1),

@@ -115,6 +115,7 @@ struct Options {
     int multiget_order = 1;       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
     int multiget_l0_group = 1;    // MultiGet: L0 files of one (m, k) tested through one interleaved table
     int probe_compact = 1;        // phased probe from keys: later phases read only the live keys' words
+    int scatter_tiles_exact = 0;  // bin scatter: rounds shrunk so the tiles fill all 256 CUs (1) (being measured)
     int scatter_bins = 1;         // bucketed build, k == 7: scatter through fixed LDS bins, pipelined against the
                                   // hashing (1), or the counting sort (0)
     uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys
