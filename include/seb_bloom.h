@@ -17,8 +17,11 @@
  * panics or yields nil); the Go shim turns a negative code into the same panic.  The Go API
  * mirror (seb_filter_*) does not fail for want of a device: a build or batched probe whose device
  * path returns SEB_ERR_DEVICE / SEB_ERR_NOMEM is done on the filter's host copy instead (option
- * "cpu_fallback", default on), counted by seb_fallback_count().  Every other entry point
- * (device-resident, host-buffer, registry) reports the error.
+ * "cpu_fallback", default on), counted by seb_fallback_count(), the first one per process also
+ * logged to stderr.  SEB_ERR_INTERNAL (a failed launch, a kernel fault) is never absorbed.  The
+ * fallback needs the filter's host copy to be current: a filter over 64 MiB of bits whose device
+ * copy is ahead of it (built on the device with the host mirror off) reports the error instead.
+ * Every other entry point (device-resident, host-buffer, registry) reports the error.
  */
 #ifndef SEB_BLOOM_H
 #define SEB_BLOOM_H
@@ -35,10 +38,11 @@ extern "C" {
 enum seb_status {
     SEB_OK = 0,
     SEB_ERR_INVALID = -1, /* bad argument; the reference would panic (e.g. % 0, index out of range) */
-    SEB_ERR_DEVICE = -2,  /* HIP runtime error / no gfx950 device / kernel fault */
-    SEB_ERR_NOMEM = -3,   /* host or device allocation failed */
+    SEB_ERR_DEVICE = -2,  /* no usable gfx950 device: none, no driver, no code object, runtime down */
+    SEB_ERR_NOMEM = -3,   /* host or device allocation failed (or over workspace_limit_mib) */
     SEB_ERR_RANGE = -4,   /* sizing outside the reference's defined float->int range */
     SEB_ERR_SHORT = -5,   /* a decoded filter's bits are shorter than ceil(numBits/8) */
+    SEB_ERR_INTERNAL = -6, /* any other HIP error: a rejected launch, a kernel fault, a library bug */
 };
 
 /* A batch of keys.  Fixed-length keys: offsets == NULL, key i = data[i*stride, (i+1)*stride).
@@ -107,7 +111,8 @@ int seb_abi_version(void);
  *                     falls back to batch order; the Go API mirror's build to its CPU fallback)
  *   "cpu_fallback"    Go API mirror: on a device failure build / probe on the host copy (1, default)
  *                     or return the error (0)
- *   "fault_inject"    test only: the Go API mirror's device path fails with SEB_ERR_DEVICE (0/1)
+ *   "fault_inject"    test only: the Go API mirror's device path fails with SEB_ERR_DEVICE (1) or
+ *                     SEB_ERR_INTERNAL (2), or not (0)
  * Environment variables SEB_<NAME> (upper case) set the initial values. */
 int seb_set_option(const char *name, int64_t value);
 int seb_get_option(const char *name, int64_t *value);

@@ -39,6 +39,27 @@ static int fail(int code, const char *fmt, ...) {
     return code;
 }
 
+// The status a failed HIP call maps to.  Only genuine unavailability is SEB_ERR_DEVICE (no device,
+// no driver, no code object for it, a runtime that is not up) and only an allocation failure is
+// SEB_ERR_NOMEM: those two are what the Go API mirror's CPU fallback absorbs.  Everything else (a
+// rejected launch, parameters the library computed wrong, a kernel fault) is SEB_ERR_INTERNAL,
+// which is reported and never absorbed, so a library bug cannot hide behind the fallback.
+static int hip_status(hipError_t e) {
+    switch (e) {
+    case hipErrorOutOfMemory:
+        return SEB_ERR_NOMEM;
+    case hipErrorNoDevice:
+    case hipErrorInvalidDevice:
+    case hipErrorInsufficientDriver:
+    case hipErrorNoBinaryForGpu:
+    case hipErrorNotInitialized:
+    case hipErrorDeinitialized:
+        return SEB_ERR_DEVICE;
+    default:
+        return SEB_ERR_INTERNAL;
+    }
+}
+
 // A failed HIP call is reported through the return code, and HIP's last-error state is cleared so
 // it does not surface again in the caller's own later checks (torch's hipGetLastError, say).
 #define HIP_OR_FAIL(expr)                                                                              \
@@ -46,7 +67,7 @@ static int fail(int code, const char *fmt, ...) {
         hipError_t e_ = (expr);                                                                        \
         if (e_ != hipSuccess) {                                                                        \
             (void)hipGetLastError();                                                                   \
-            return fail(SEB_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_));                       \
+            return fail(hip_status(e_), "%s: %s", #expr, hipGetErrorString(e_));                       \
         }                                                                                              \
     } while (0)
 
@@ -143,7 +164,7 @@ static const OptionDesc kOptions[] = {
     SEB_OPT(workspace_limit_mib, 0, 1 << 30),
     SEB_OPT(varlen_tail, 0, 1),
     SEB_OPT(cpu_fallback, 0, 1),
-    SEB_OPT(fault_inject, 0, 1),
+    SEB_OPT(fault_inject, 0, 2),
 };
 #undef SEB_OPT
 
@@ -394,7 +415,7 @@ extern "C" int seb_workspace_release(void) {
         for (auto &b : sl->bufs)
             if (e == hipSuccess) e = hipFree(b.p);
         if (e != hipSuccess) {
-            rc = fail(SEB_ERR_DEVICE, "seb_workspace_release: %s", hipGetErrorString(e));
+            rc = fail(hip_status(e), "seb_workspace_release: %s", hipGetErrorString(e));
             break;
         }
         sl->bufs.clear();
@@ -913,7 +934,7 @@ struct PinBuf {
         }
         if ((e = hipHostGetDevicePointer(&dev, p, 0)) != hipSuccess) {
             release();
-            return (void)hipGetLastError(), fail(SEB_ERR_DEVICE, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+            return (void)hipGetLastError(), fail(hip_status(e), "hipHostGetDevicePointer: %s", hipGetErrorString(e));
         }
         cap = want;
         return SEB_OK;
@@ -956,7 +977,7 @@ extern "C" int seb_ctx_create(int device, seb_ctx **out) {
     }
     if (e != hipSuccess) {
         seb_ctx_destroy(c);
-        return fail(SEB_ERR_DEVICE, "seb_ctx_create: %s", hipGetErrorString(e));
+        return fail(hip_status(e), "seb_ctx_create: %s", hipGetErrorString(e));
     }
     *out = c;
     return SEB_OK;
@@ -1412,16 +1433,34 @@ static int usable(seb_filter *f, const char *who) {
 // `fresh`: the filter is a New with nothing built, and its device words are taken without a clear
 // (the build writes them whole or clears them itself); host_zero stays set until the build
 // succeeded (build_into_filter drops such a device copy on failure, so a retry starts clean).
+static int build_into_filter_device_on(seb_ctx *c, seb_filter *f, const seb_keys *kb, bool fresh);
+
+// On failure the context's stream is drained before the lease goes back, so nothing queued by this
+// build can still write the filter's device words when drop_device_copy hands them to the pool;
+// only this stream is waited for (no device-wide synchronisation, which would stall other threads'
+// work and break their stream captures).
 static int build_into_filter_device(seb_filter *f, const seb_keys *kb, bool fresh) {
-    if (options().fault_inject) return fail(SEB_ERR_DEVICE, "BloomFilter build: injected device fault (fault_inject)");
+    if (options().fault_inject)
+        return fail(options().fault_inject == 2 ? SEB_ERR_INTERNAL : SEB_ERR_DEVICE,
+                    "BloomFilter build: injected %s (fault_inject)",
+                    options().fault_inject == 2 ? "internal error" : "device fault");
     CtxLease L(f->device);
     if (L.rc) return L.rc;
     std::lock_guard<std::mutex> g(L.c->mu);
     HIP_OR_FAIL(hipSetDevice(f->device));
+    const int rc = build_into_filter_device_on(L.c, f, kb, fresh);
+    if (rc != SEB_OK) {
+        (void)hipStreamSynchronize(L.c->s_comp);
+        (void)hipGetLastError();
+    }
+    return rc;
+}
+
+static int build_into_filter_device_on(seb_ctx *c, seb_filter *f, const seb_keys *kb, bool fresh) {
     int rc;
     // a new filter's first build writes its words whole (image build) or clears them first: no
     // separate memset of the device copy
-    if ((rc = ensure_device_copy(f, L.c->s_comp, !fresh))) return rc;
+    if ((rc = ensure_device_copy(f, c->s_comp, !fresh))) return rc;
     f->host_ok = false;  // the device copy is about to move ahead of the host copy
     f->readable.store(false, std::memory_order_relaxed);
     // Small builds skip the DMA engine, whose copies started ~8 us (keys in) and ~16 us (bits out)
@@ -1436,7 +1475,6 @@ static int build_into_filter_device(seb_filter *f, const seb_keys *kb, bool fres
                          obytes <= (8ull << 20) && !(kb->offsets && kb->n >= options().varlen_prehash_min_keys);
     const bool zc_bits = f->nbytes <= (16ull << 20);
     const bool mirror = f->nbytes <= (64ull << 20);
-    seb_ctx *c = L.c;
     if (zc_keys) {
         const uint64_t kpad = (kbytes + 15) & ~15ull;
         if ((rc = c->hkeys.reserve(kpad + obytes + 16))) return rc;
@@ -1486,6 +1524,14 @@ extern "C" uint64_t seb_fallback_count(void) { return g_fallbacks.load(std::memo
 
 static bool device_failure(int rc) { return rc == SEB_ERR_DEVICE || rc == SEB_ERR_NOMEM; }
 
+// Counts a fallback; the first one in the process is also written to stderr with its cause (the
+// failing call's seb_last_error), so a deployment sees it without reading the counter.
+static void note_fallback(const char *who) {
+    if (g_fallbacks.fetch_add(1, std::memory_order_relaxed) == 0)
+        fprintf(stderr, "seb_bloom: %s fell back to the host copy (CPU) after a device failure: %s\n", who,
+                t_err.c_str());
+}
+
 // lsm/bloom.go:70-77 for one key on the host copy: positions stepped as in host_may_contain
 // ((h1 + i*h2) mod m with u64 wraparound, :58-67), LSB-first byte ORs (:73-75).
 static void host_add_key(seb_filter *f, const uint8_t *key, uint64_t len) {
@@ -1522,13 +1568,13 @@ static const uint8_t *host_key(const seb_keys *kb, uint64_t i, uint64_t *len) {
     return kb->data + i * (uint64_t)kb->stride;
 }
 
-// Give the device word array back (after its stream work ended): a copy that is garbage (a fresh
-// build that failed) or stale (the host copy moved ahead in a fallback).  The next device use
+// Give the device word array back: a copy that is garbage (a fresh build that failed) or stale
+// (the host copy moved ahead in a fallback).  Its only writer, the failed build's stream, was
+// drained before that build's lease ended (build_into_filter_device).  The next device use
 // uploads the host copy again (ensure_device_copy).
 static void drop_device_copy(seb_filter *f) {
     if (!f->dwords) return;
     (void)hipSetDevice(f->device);
-    (void)hipDeviceSynchronize();  // nothing queued may still write the buffer the pool hands out next
     if (!g_words_pool.give(f->device, f->dwords, f->dbytes)) (void)hipFree(f->dwords);
     (void)hipGetLastError();
     f->dwords = nullptr;
@@ -1559,7 +1605,7 @@ static int build_into_filter(seb_filter *f, const seb_keys *kb) {
     drop_device_copy(f);
     f->host_ok = true;
     f->host_zero = false;
-    g_fallbacks.fetch_add(1, std::memory_order_relaxed);
+    note_fallback("BloomFilter build");
     (void)hipGetLastError();
     return SEB_OK;
 }
@@ -1663,7 +1709,10 @@ extern "C" int seb_filter_add_batch(seb_filter *f, const seb_keys *kb) {
 }
 
 static int probe_filter_device(seb_filter *f, const seb_keys *kb, uint8_t *out) {
-    if (options().fault_inject) return fail(SEB_ERR_DEVICE, "BloomFilter probe: injected device fault (fault_inject)");
+    if (options().fault_inject)
+        return fail(options().fault_inject == 2 ? SEB_ERR_INTERNAL : SEB_ERR_DEVICE,
+                    "BloomFilter probe: injected %s (fault_inject)",
+                    options().fault_inject == 2 ? "internal error" : "device fault");
     CtxLease L(f->device);
     if (L.rc) return L.rc;
     std::lock_guard<std::mutex> g2(L.c->mu);
@@ -1690,7 +1739,7 @@ extern "C" int seb_filter_may_contain_batch(seb_filter *f, const seb_keys *kb, u
         const uint8_t *key = host_key(kb, i, &len);
         out[i] = (uint8_t)host_may_contain(f, key, len);
     }
-    g_fallbacks.fetch_add(1, std::memory_order_relaxed);
+    note_fallback("BloomFilter.MayContain batch");
     (void)hipGetLastError();
     return SEB_OK;
 }

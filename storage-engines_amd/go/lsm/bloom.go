@@ -11,11 +11,16 @@
 // launch).  MayContain crosses once per call and is answered on the library's host copy of the
 // bits, lock-free (seb_filter_may_contain).
 //
-// Errors: the Go API has no error returns.  A device that is busy, out of HBM or absent does not
-// reach the callers: the library builds / probes on its host copy of the filter instead (the
-// "cpu_fallback" option, counted by seb_fallback_count), so a flush or compaction worker keeps
-// running where the reference would.  libPanic is left for what the reference also panics on
-// (a decoded filter too short for its numBits, sizing outside Go's defined range).
+// Errors: the Go API has no error returns.  A device that is out of HBM or absent
+// (SEB_ERR_NOMEM / SEB_ERR_DEVICE) does not reach the callers: the library builds / probes on its
+// host copy of the filter instead (the "cpu_fallback" option, counted by seb_fallback_count, the
+// first one logged to stderr), so a flush or compaction worker keeps running where the reference
+// would.  Two exceptions panic through libPanic: SEB_ERR_INTERNAL (a rejected launch or a kernel
+// fault, i.e. a library bug, which a fallback must not hide), and a filter of more than 64 MiB of
+// bits (about 56M keys at 1% FPR, past any memtable flush or compaction output) whose device copy
+// is ahead of its host copy, so no correct base for the fallback exists.  libPanic is otherwise
+// left for what the reference also panics on (a decoded filter too short for its numBits, sizing
+// outside Go's defined range).
 //
 // Not compiled in this repository's pipeline: no Go toolchain exists in the build image or on
 // the GPU box (see DESIGN.md).  storage-engines_amd/harness/sstable_replay.c exercises the C call

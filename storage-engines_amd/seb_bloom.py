@@ -29,7 +29,8 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "seb_bloom.h")
 
 SEB_OK = 0
 SEB_BUILD_FRESH = 1
-ERRORS = {-1: "SEB_ERR_INVALID", -2: "SEB_ERR_DEVICE", -3: "SEB_ERR_NOMEM", -4: "SEB_ERR_RANGE", -5: "SEB_ERR_SHORT"}
+ERRORS = {-1: "SEB_ERR_INVALID", -2: "SEB_ERR_DEVICE", -3: "SEB_ERR_NOMEM", -4: "SEB_ERR_RANGE", -5: "SEB_ERR_SHORT",
+          -6: "SEB_ERR_INTERNAL"}
 
 
 class SebError(RuntimeError):

@@ -64,6 +64,20 @@ def _child(case, args, q):
             m, k = seb.params(1000, 0.01)
             bits = oc.build(m, k, np.frombuffer(b"key", np.uint8), 1, offsets=np.array([0, 3], np.uint64))
             out["want"] = sha(m.to_bytes(8, "little") + k.to_bytes(4, "little") + bits.tobytes())
+        elif case == "internal":  # an internal error (a library bug) is reported, never absorbed
+            seb.set_option("fault_inject", 2)
+            f = seb.BloomFilter(1000, 0.01)
+            f.add(b"key")
+            try:
+                f.encode()
+                out["raised"] = None
+            except seb.SebError as e:
+                out["raised"] = e.code
+            try:
+                f.may_contain_batch([b"key"])
+                out["raised_probe"] = None
+            except seb.SebError as e:
+                out["raised_probe"] = e.code
         elif case == "varlen":
             seb.set_option("fault_inject", 1)
             rng = np.random.default_rng(7)
@@ -157,6 +171,14 @@ def test_fallback_off_reports_the_error_and_keeps_the_keys():
     out = _run("no_fallback")
     assert out["raised"] == -2  # SEB_ERR_DEVICE
     assert out["after"] == out["want"]  # the failed build kept the Add; the next Encode built it
+
+
+def test_internal_error_is_not_absorbed():
+    """Only unavailability (SEB_ERR_DEVICE) and allocation failures (SEB_ERR_NOMEM) fall back; a
+    rejected launch or kernel fault (SEB_ERR_INTERNAL) reaches the caller with the fallback on."""
+    out = _run("internal")
+    assert out["raised"] == -6 and out["raised_probe"] == -6  # SEB_ERR_INTERNAL
+    assert out["fallbacks"] == 0
 
 
 def test_fallback_variable_length_keys():

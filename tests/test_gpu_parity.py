@@ -1659,7 +1659,7 @@ def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
         seb.set_option("build_algo", 0)
 
 
-@pytest.mark.parametrize("bins", [1, 0], ids=["bins", "counting"])
+@pytest.mark.parametrize("bins", [(1, 0), (1, 1), (0, 0)], ids=["bins", "bins_tiles_exact", "counting"])
 @pytest.mark.parametrize("case", ["nb513", "c2m", "nb2274", "duplicates", "skewed"])
 def test_bucketed_scatter_bins(seb, torch_cuda, case, bins):
     """The radix-partitioned build's two scatters (scatter_bins 1: fixed LDS bins, runs padded to
@@ -1684,7 +1684,8 @@ def test_bucketed_scatter_bins(seb, torch_cuda, case, bins):
     uniq = np.unique(keys, axis=0)
     ref = oc.build(m, k, np.ascontiguousarray(uniq).ravel(), len(uniq), stride=16)
     kd = seb.dev_keys(to_dev(torch, keys), n=n, stride=16)
-    with seb.option("build_algo", 2), seb.option("scatter_bins", bins):
+    bins, exact = bins
+    with seb.option("build_algo", 2), seb.option("scatter_bins", bins), seb.option("scatter_tiles_exact", exact):
         words = seb.new_words(m)
         for rep in range(2):
             words.view(torch.uint8).fill_(0xC3 if rep == 0 else 0xFF)
@@ -1701,7 +1702,7 @@ def test_bucketed_scatter_bins(seb, torch_cuda, case, bins):
         assert np.array_equal(seb.words_to_bits(w2, m), ref), (case, bins)
 
 
-@pytest.mark.parametrize("bins", [1, 0], ids=["bins", "counting"])
+@pytest.mark.parametrize("bins", [(1, 0), (1, 1), (0, 0)], ids=["bins", "bins_tiles_exact", "counting"])
 @pytest.mark.parametrize("src", ["stride20", "stride13", "varlen_direct", "varlen_prehash"])
 def test_bucketed_scatter_key_sources(seb, torch_cuda, src, bins):
     """Both scatters over every key source the radix-partitioned build reads at a filter size the
@@ -1723,7 +1724,8 @@ def test_bucketed_scatter_key_sources(seb, torch_cuda, src, bins):
         ref = oc.build(m, k, data, n, offsets=off)
         kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off.astype(np.int64)))
     prehash = 0 if src == "varlen_prehash" else 1 << 40
-    with seb.option("build_algo", 2), seb.option("scatter_bins", bins), \
+    bins, exact = bins
+    with seb.option("build_algo", 2), seb.option("scatter_bins", bins), seb.option("scatter_tiles_exact", exact), \
             seb.option("varlen_prehash_min_keys", prehash):
         words = seb.new_words(m)
         words.view(torch.uint8).fill_(0x3C)
