@@ -768,13 +768,19 @@ def launch_check(args, world, rank):
     import torch
     import torch.distributed as dist
 
+    import rank_report as rr
+
     dist.init_process_group("gloo")
     assert dist.get_world_size() == world and dist.get_rank() == rank
     t = torch.tensor([rank + 1], dtype=torch.int64)
     dist.all_reduce(t)
+    rec = rr.rank_record(rank, int(os.environ.get("LOCAL_RANK", rank)), dist.get_world_size(), "gloo", None,
+                         rr.allreduce_ones(torch, dist, None))
+    recs = rr.gather_records(dist, rec, world)
     if rank == 0:
         print(json.dumps({"n_gpus": dist.get_world_size(), "rank_sum": int(t.item()),
-                          "master": f"{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}"}), flush=True)
+                          "master": f"{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}",
+                          "per_rank": recs, **rr.summarize(recs, world, "gloo")}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -916,6 +922,16 @@ def main():
     torch.cuda.synchronize()
     parity = st.parity(args.warmup + args.steps - 1)
     elapsed, kern_ms, bcast, overlap = run["elapsed"], run["kern_ms"], run["bcast"], run["overlap"]
+    # Each rank's record (GPU PCI address, communicator size and an all-reduce of ones over it, its
+    # launch and broadcast-wait times), gathered to rank 0: the line proves what it ran on.
+    import rank_report as rr
+
+    backend = args.dist_backend if world > 1 else "none"
+    rec = rr.rank_record(rank, local, world, backend, rr.device_identity(torch, dev),
+                         rr.allreduce_ones(torch, dist, dev) if world > 1 else 1, kern_ms, run["wait_ms"],
+                         run["wait_host_ms"], run["elapsed_own"])
+    records = rr.gather_records(dist, rec, world)
+    report = rr.summarize(records, world, backend)
     value = st.units_per_step * args.steps / elapsed / 1e6
     resident = None
     if world > 1 and args.config in ("c2c3", "c5") and args.batch == "step" and not args.no_secondary:
@@ -950,7 +966,7 @@ def main():
             "metric": METRIC if args.config in ("c2c3", "c4", "c5", "c5_2d", "lsm", "lsm_wide", "c2_sharded",
                                                 "c3_partitioned")
             else f"{args.config} {st.unit}",
-            "value": round(value, 2), "unit": st.unit, "n_gpus": world, "devices": min(world, ndev),
+            "value": round(value, 2), "unit": st.unit, "n_gpus": world, "devices": report["devices"],
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1000.0 / args.steps, 4),
             "higher_is_better": True, "scaling": st.scaling, "vs_baseline": None, "dtype": st.dtype,
             "data": "synthetic (reference key format user%010d+2B, common/benchmark/keygen.go:89-109)",
@@ -973,6 +989,8 @@ def main():
                              "timed step and the last; ms_per_step is the wall clock of all steps",
             "options": {**{o: seb.get_option(o) for o in OPTIONS}, "overlap": int(overlap)},
             "cpu_fallbacks": seb.fallback_count(),
+            "per_rank": records,
+            "rank_check": {x: report[x] for x in report if x != "devices"},
         }
         if args.config == "c2c3":
             # SURVEY.md 8(d)'s secondary sector model: every bit touch one 64-B DRAM transaction (no
@@ -1011,6 +1029,9 @@ def main():
         dist.destroy_process_group()
     if result is not None:
         print(json.dumps(result), flush=True)
+    if report["problems"]:  # e.g. RCCL ranks that did not land on N distinct GPUs: not a valid N-GPU line
+        print(f"bench.py: rank {rank}: " + "; ".join(report["problems"]), file=sys.stderr)
+        sys.exit(4)
 
 
 def timed_run(args, st, seb, torch, dist, world, rank, dev):
@@ -1043,7 +1064,8 @@ def timed_run(args, st, seb, torch, dist, world, rank, dev):
     # probe (no broadcast to wait for, one stream) the build's end is the probe's start.
     shared = not overlap and pipe is None
     prev_end = [None]
-    pool = [seb.Timer() for _ in range(4 * args.steps + 1)]  # created before the timed region
+    pool = [seb.Timer() for _ in range(6 * args.steps + 1)]  # created before the timed region
+    waits, host_waits = [], []  # the compute stream's stall on the batch's transfer (GPU) / the host's wait
 
     def mark(stream):
         t = pool.pop()
@@ -1067,7 +1089,12 @@ def timed_run(args, st, seb, torch, dist, world, rank, dev):
                     built[j % 2].record(sb)
             if overlap:
                 sp.wait_event(built[j % 2])
+        if record and pipe is not None:  # how long this rank's stream waits for the batch (per-rank record)
+            w0, h0 = mark(sp), time.perf_counter()
         buf = pipe.acquire(j) if pipe is not None else None
+        if record and pipe is not None:
+            host_waits.append(time.perf_counter() - h0)
+            waits.append((w0, mark(sp)))
         target = pipe.root_target(j) if pipe is not None and rank == 0 and pipe.lead > 1 else None
         if record:
             p_start = b_end if shared and b_end is not None else \
@@ -1103,7 +1130,7 @@ def timed_run(args, st, seb, torch, dist, world, rank, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = own = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1128,10 +1155,12 @@ def timed_run(args, st, seb, torch, dist, world, rank, dev):
         bcast = {"bytes": int(nbytes), "ms": round(float(t.item()) * 1e3, 4),
                  "GB/s": round(nbytes / float(t.item()) / 1e9, 2), "backend": args.dist_backend,
                  "note": "RCCL broadcast of the probe batch from rank 0, once per batch, outside the timed steps"}
-    return {"elapsed": elapsed, "kern_ms": kern_ms, "bcast": bcast, "overlap": overlap}
+    wait = {"wait_ms": float(np.mean([a.elapsed_ms(b) for a, b in waits])) if waits else None,
+            "wait_host_ms": float(np.mean(host_waits)) * 1e3 if host_waits else None}
+    return {"elapsed": elapsed, "elapsed_own": own, "kern_ms": kern_ms, "bcast": bcast, "overlap": overlap, **wait}
 
 
-SECONDARY = (("c4", ["--steps", "10", "--warmup", "3", "--no-cpu-baseline"]),
+SECONDARY = (("c4", ["--steps", "10", "--warmup", "3"]),
              ("c5", ["--steps", "10", "--warmup", "3"]),
              ("lsm", ["--steps", "10", "--warmup", "3"]), ("lsm_wide", ["--steps", "10", "--warmup", "3"]),
              ("flush", []))
@@ -1168,6 +1197,14 @@ def secondary_lines():
             if gm:
                 item["gather_model"] = {k: gm[k] for k in ("gathers_per_call", "Ggathers_s", "ceiling_Ggathers_s", "frac",
                                                            "count_source")}
+        cb = line.get("cpu_baseline")
+        if cb and cfg != "flush":
+            item["cpu_baseline"] = {x: cb[x] for x in ("value", "unit", "cores", "kind", "sample", "method", "reps",
+                                                       "build_mkeys_s", "probe_mkeys_s") if x in cb}
+            for legname in ("multi_thread", "all_cpus"):
+                if legname in cb:
+                    item["cpu_baseline"][legname] = {x: cb[legname][x] for x in (
+                        "value", "cores", "build_mkeys_s", "probe_mkeys_s", "bit_exact_vs_1_thread") if x in cb[legname]}
         if cfg == "flush":
             item["sizes"] = [{"n": z["n"], "shim_us": z["shim_us"]["total"], "per_key_add_us": z["build_us"]["total"],
                               "may_contain_ns_1t": z["may_contain"]["ns_per_call_1t"],
@@ -1221,64 +1258,103 @@ def host_inclusive(seb, build_host, probe_host, m, k):
     return res
 
 
-def cpu_baseline(args, n, m, k):
-    """The oracle's C restatement of lsm/bloom.go on this host (checker code, timed only here)."""
+def host_cpu_info() -> dict:
+    """The host the CPU baseline ran on: model name, CPUs visible, CPUs this process may run on,
+    and the cgroup CPU quota (a GPU box's share of a many-core host is a quota, not an affinity)."""
     import platform
 
+    info = {"model": platform.processor() or platform.machine(), "host_cpus": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": None}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()
+            if quota != "max":
+                info["cgroup_cpu_quota"] = round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+CPU_REPS = 5  # timed repetitions per leg after one warm-up (SURVEY 8(d), BASELINE.md 3): the median is reported
+
+
+def cpu_baseline(args, n, m, k):
+    """The oracle's C restatement of lsm/bloom.go on this host (checker code, timed only here,
+    after the GPU's timed region).  SURVEY 8(d) / BASELINE.md 3's method: per leg, 1 warm-up and
+    the median of 5 timed build + probe passes over the same sample, bit-exact-checked against the
+    1-thread leg; legs: 1 thread (scalar-faithful: the reference's Add runs in one goroutine per
+    filter, lsm/sstable_builder.go:53), the 16 threads one GPU's share of the box allows, and every
+    CPU this process may run on.  Multi-threaded: the probe is key-sharded; the build gives every
+    thread a private zeroed filter for its key shard, then ORs the private filters together, each
+    thread one byte range of all of them (no shared-line atomics)."""
     from oracle import oracle_c as oc
     import keygen as kg
 
     sample = n if args.config == "c2c3" else min(n, 2_000_000)
     if args.config == "c2c3":
-        bk = kg.key16(np.arange(sample))
-        pkeys = kg.key16(kg.probe_indices(sample))
-        t0 = time.perf_counter()
-        bits = oc.build(m, k, bk, sample, stride=16, threads=args.cpu_threads)
-        t1 = time.perf_counter()
-        ans = oc.probe(bits, m, k, pkeys, sample, stride=16, threads=args.cpu_threads)
-        t2 = time.perf_counter()
-        assert ans[0::2].all()
+        bk, pk = kg.key16(np.arange(sample)), kg.key16(kg.probe_indices(sample))
+        kw_b, kw_p = dict(data=bk, stride=16), dict(data=pk, stride=16)
     else:
         bd, bo = kg.varlen_keys(np.arange(sample))
         pd, po = kg.varlen_keys(kg.probe_indices(sample))
-        t0 = time.perf_counter()
-        bits = oc.build(m, k, bd, sample, offsets=bo, threads=args.cpu_threads)
-        t1 = time.perf_counter()
-        oc.probe(bits, m, k, pd, sample, offsets=po, threads=args.cpu_threads)
-        t2 = time.perf_counter()
-    model = platform.processor() or platform.machine()
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    res = {"value": round(2.0 * sample / (t2 - t0) / 1e6, 3), "unit": "Mkeys/s", "cores": args.cpu_threads,
-           "host_cpus": os.cpu_count(), "kind": "port",
-           "sample": f"{sample} build + {sample} probe keys ({args.config}), oracle/bloom_oracle.c "
-                     f"(C restatement of lsm/bloom.go; Go toolchain absent), {args.cpu_threads} thread(s), {model}",
-           "build_mkeys_s": round(sample / (t1 - t0) / 1e6, 3), "probe_mkeys_s": round(sample / (t2 - t1) / 1e6, 3)}
-    # SURVEY 8(d)(ii): the same restatement over the host cores this GPU's share allows (16 per GPU
-    # on the box): key-sharded probe, build with atomic byte ORs.  Reported beside the 1-thread
-    # value (the reference's Add runs in one goroutine per filter).
-    mt = min(16, os.cpu_count() or 1)
-    if mt > 1 and args.cpu_threads == 1:
-        if args.config == "c2c3":
+        kw_b, kw_p = dict(data=bd, offsets=bo), dict(data=pd, offsets=po)
+    host = host_cpu_info()
+
+    def leg(threads):
+        tb, tp = [], []
+        bits = ans = None
+        for rep in range(1 + CPU_REPS):
             t0 = time.perf_counter()
-            bits = oc.build(m, k, bk, sample, stride=16, threads=mt)
+            bits = oc.build(m, k, n=sample, threads=threads, **kw_b)
             t1 = time.perf_counter()
-            oc.probe(bits, m, k, pkeys, sample, stride=16, threads=mt)
+            ans = oc.probe(bits, m, k, n=sample, threads=threads, **kw_p)
+            t2 = time.perf_counter()
+            if rep:  # rep 0 is the warm-up
+                tb.append(t1 - t0)
+                tp.append(t2 - t1)
+        b, p = float(np.median(tb)), float(np.median(tp))
+        return {"value": round(2.0 * sample / (b + p) / 1e6, 3), "cores": threads,
+                "build_mkeys_s": round(sample / b / 1e6, 3), "probe_mkeys_s": round(sample / p / 1e6, 3),
+                "build_ms": {"median": round(b * 1e3, 2), "min": round(min(tb) * 1e3, 2), "max": round(max(tb) * 1e3, 2)},
+                "probe_ms": {"median": round(p * 1e3, 2), "min": round(min(tp) * 1e3, 2), "max": round(max(tp) * 1e3, 2)},
+                }, bits, ans
+
+    one, bits1, ans1 = leg(1)
+    if args.config == "c2c3":
+        assert ans1[0::2].all()  # no false negatives on the present half
+    res = {"value": one["value"], "unit": "Mkeys/s", "cores": 1, "host_cpus": host["host_cpus"], "kind": "port",
+           "sample": f"{sample} build + {sample} probe keys ({args.config}), oracle/bloom_oracle.c (C restatement of "
+                     f"lsm/bloom.go; Go toolchain absent), {host['model']}",
+           "method": f"per leg 1 warm-up + median of {CPU_REPS} (build then probe each rep); multi-threaded legs: "
+                     "key-sharded probe, build into per-thread private filters OR-merged by byte range; every leg's "
+                     "filter and answers equal the 1-thread leg's",
+           "reps": CPU_REPS, "host": host,
+           **{x: one[x] for x in ("build_mkeys_s", "probe_mkeys_s", "build_ms", "probe_ms")}}
+    share = min(16, host["affinity_cpus"])
+    legs = [("multi_thread", share)]
+    if host["affinity_cpus"] > share:
+        legs.append(("all_cpus", min(256, host["affinity_cpus"])))
+    for name, threads in legs:
+        if threads <= 1 or args.cpu_threads != 1:
+            continue
+        r, bits, ans = leg(threads)
+        r["bit_exact_vs_1_thread"] = bool(np.array_equal(bits, bits1) and np.array_equal(ans, ans1))
+        r["build_speedup_vs_1_thread"] = round(r["build_mkeys_s"] / one["build_mkeys_s"], 2)
+        r["probe_speedup_vs_1_thread"] = round(r["probe_mkeys_s"] / one["probe_mkeys_s"], 2)
+        if name == "multi_thread":
+            r["note"] = "the 16 host threads one GPU's share of the box allows"
         else:
-            t0 = time.perf_counter()
-            bits = oc.build(m, k, bd, sample, offsets=bo, threads=mt)
-            t1 = time.perf_counter()
-            oc.probe(bits, m, k, pd, sample, offsets=po, threads=mt)
-        t2 = time.perf_counter()
-        res["multi_thread"] = {"value": round(2.0 * sample / (t2 - t0) / 1e6, 3), "cores": mt,
-                               "build_mkeys_s": round(sample / (t1 - t0) / 1e6, 3),
-                               "probe_mkeys_s": round(sample / (t2 - t1) / 1e6, 3)}
+            r["note"] = "every CPU this process may run on (sched_getaffinity), capped at 256; a cgroup CPU quota " \
+                        "(host.cgroup_cpu_quota) may throttle it below that"
+        res[name] = r
     return res
 
 

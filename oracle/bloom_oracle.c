@@ -27,6 +27,7 @@
  * (tests/golden/fnv_kats.json), and agreement with the independent numpy restatement
  * (oracle/bloom_np.py) on every committed fixture.  See DESIGN.md "Oracle".
  */
+#define _POSIX_C_SOURCE 200809L
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -264,8 +265,92 @@ int oracle_probe_mt(const uint8_t *bits, uint64_t m, uint32_t k, const uint8_t *
     return run_mt(probe_worker, b, n, threads);
 }
 
-int oracle_build_mt(uint8_t *bits, uint64_t m, uint32_t k, const uint8_t *data, const uint64_t *offsets,
-                    uint32_t stride, uint64_t n, int threads) {
+/* The atomic variant: every thread ORs into the shared bits with relaxed atomic byte ORs.  Kept
+ * for comparison; contended cache lines make it scale poorly. */
+int oracle_build_mt_atomic(uint8_t *bits, uint64_t m, uint32_t k, const uint8_t *data, const uint64_t *offsets,
+                           uint32_t stride, uint64_t n, int threads) {
     mt_job b = {NULL, bits, m, k, data, offsets, stride, 0, 0, NULL};
     return run_mt(build_worker, b, n, threads);
+}
+
+/* SURVEY.md 8(d)(ii)'s multi-threaded build: per-thread private filters OR-merged.  Each thread
+ * allocates a zeroed private filter (NewBloomFilter's make, lsm/bloom.go:34-37, first touched by
+ * its own thread), runs the scalar Add loop (lsm/bloom.go:70-77) over its contiguous key shard,
+ * and after a barrier ORs byte range t of every private filter into `bits` (so the merge reads
+ * T filters once, split over the T threads).  OR is commutative, so the result equals the
+ * sequential build's. */
+typedef struct {
+    mt_job job;
+    uint8_t **priv;
+    int t, threads;
+    uint64_t nbytes;
+    pthread_barrier_t *bar;
+    int err;
+} priv_job;
+
+static void *build_private_worker(void *arg) {
+    priv_job *j = (priv_job *)arg;
+    uint8_t *mine = (uint8_t *)calloc(j->nbytes ? j->nbytes : 1, 1);
+    j->priv[j->t] = mine;
+    if (mine) {
+        for (uint64_t i = j->job.lo; i < j->job.hi; i++) {
+            uint64_t len;
+            const uint8_t *key = key_at(j->job.data, j->job.offsets, j->job.stride, i, &len);
+            oracle_add(mine, j->job.m, j->job.k, key, len);
+        }
+    } else {
+        j->err = 1;
+    }
+    pthread_barrier_wait(j->bar);
+    /* merge: this thread's 8-B aligned slice of the byte array, across every private filter */
+    const uint64_t words = (j->nbytes + 7) / 8;
+    uint64_t lo = words * (uint64_t)j->t / (uint64_t)j->threads * 8;
+    uint64_t hi = words * (uint64_t)(j->t + 1) / (uint64_t)j->threads * 8;
+    if (hi > j->nbytes) hi = j->nbytes;
+    for (int q = 0; q < j->threads; q++) {
+        const uint8_t *src = j->priv[q];
+        if (!src) continue;
+        uint64_t b = lo;
+        for (; b + 8 <= hi; b += 8) {
+            uint64_t x, y;
+            memcpy(&x, j->job.wbits + b, 8);
+            memcpy(&y, src + b, 8);
+            x |= y;
+            memcpy(j->job.wbits + b, &x, 8);
+        }
+        for (; b < hi; b++) j->job.wbits[b] |= src[b];
+    }
+    pthread_barrier_wait(j->bar);
+    free(mine);
+    return NULL;
+}
+
+int oracle_build_mt(uint8_t *bits, uint64_t m, uint32_t k, const uint8_t *data, const uint64_t *offsets,
+                    uint32_t stride, uint64_t n, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    priv_job jobs[256];
+    uint8_t *priv[256];
+    pthread_barrier_t bar;
+    if (pthread_barrier_init(&bar, NULL, (unsigned)threads) != 0) return -1;
+    const uint64_t nbytes = (m + 7) / 8;
+    int started = 0, rc = 0;
+    for (int t = 0; t < threads; t++) {
+        priv[t] = NULL;
+        mt_job b = {NULL, bits, m, k, data, offsets, stride, n * (uint64_t)t / (uint64_t)threads,
+                    n * (uint64_t)(t + 1) / (uint64_t)threads, NULL};
+        jobs[t] = (priv_job){b, priv, t, threads, nbytes, &bar, 0};
+    }
+    for (int t = 0; t < threads; t++) {
+        /* a thread that cannot start leaves the barrier incomplete: abort (checker code only) */
+        if (pthread_create(&tid[t], NULL, build_private_worker, &jobs[t]) != 0) abort();
+        started++;
+    }
+    for (int t = 0; t < started; t++) {
+        pthread_join(tid[t], NULL);
+        if (jobs[t].err) rc = -1;
+    }
+    pthread_barrier_destroy(&bar);
+    return rc;
 }

@@ -2065,25 +2065,38 @@ static RegLayout mg_layout(const seb_registry *r) {
 }
 
 // multiget_order: the batch's key-range order over the registry's partition level, in the
-// stream's scratch (tag 3); null when off, too small a batch or no disjoint level of >= 2 files.
-static int multiget_order(seb_registry *r, KeyBatch &kb, hipStream_t s, uint32_t **order, bool *order_keys) {
-    *order = nullptr;
-    *order_keys = true;
+// stream's scratch (tag 3); mo->active false when off, too small a batch or no disjoint level of
+// >= 2 files.  On success kb reads the moved keys, if they were moved.
+static int multiget_order(seb_registry *r, KeyBatch &kb, uint64_t answer_bytes, hipStream_t s, MgOrder *mo) {
+    *mo = MgOrder{};
     if (!options().multiget_order || r->part_hi <= r->part_lo || kb.n < 65536 || kb.n > 0xffffffffull) return SEB_OK;
     void *ws = nullptr;
-    int rc = cached_workspace(s, multiget_order_bytes(kb), &ws, 3);
+    int rc = cached_workspace(s, multiget_order_bytes(kb, answer_bytes), &ws, 3);
     if (rc == SEB_ERR_NOMEM) {  // the order is only a speed-up: batch order needs no scratch
         t_err.clear();
         return SEB_OK;
     }
     if (rc) return rc;
-    const uint8_t *moved = nullptr;
     HIP_OR_FAIL(launch_multiget_order(kb, (const RegSlot *)r->dslots.p, r->part_lo, r->part_hi,
-                                      (const uint8_t *)r->dranges.p, ws, order, &moved, s));
-    if (moved) {  // the MultiGet streams the moved keys; answers still land at each key's index
-        kb.data = moved;
-        *order_keys = false;
-    }
+                                      (const uint8_t *)r->dranges.p, ws, mo, s));
+    if (mo->keys) kb.data = mo->keys;  // the MultiGet streams the moved keys
+    return SEB_OK;
+}
+
+// One MultiGet launch (mask form: maybe; list form: cand rows of cap u16) over kb, in key-range
+// order when the registry has a partition level (answers in sorted rows, then unpermuted into the
+// output), else in batch order.
+static int multiget_launch(seb_registry *r, KeyBatch kb, uint64_t *maybe, uint16_t *cand, uint32_t cap,
+                           hipStream_t s) {
+    const uint64_t answer_bytes = maybe ? 8 : 2ull * cap;
+    MgOrder mo;
+    int rc;
+    if ((rc = multiget_order(r, kb, answer_bytes, s, &mo))) return rc;
+    HIP_OR_FAIL(launch_multiget(kb, (const RegSlot *)r->dslots.p, r->nslots, mg_layout(r), (const uint8_t *)r->dranges.p,
+                                mo.active ? (maybe ? (uint64_t *)mo.answers : nullptr) : maybe,
+                                mo.active ? (maybe ? nullptr : (uint16_t *)mo.answers) : cand, cap, s, mo.key_order));
+    if (mo.active)
+        HIP_OR_FAIL(launch_multiget_unpermute(mo, maybe ? (void *)maybe : (void *)cand, answer_bytes, s));
     return SEB_OK;
 }
 
@@ -2111,14 +2124,7 @@ static int registry_multiget_dev(seb_registry *r, const seb_keys *keys, uint64_t
     WsCall ws_call;
     std::lock_guard<std::mutex> g(r->mu);
     if ((rc = sync_registry_locked(r)) || (rc = check_multiget_out(r, maybe, cand, cap, keys->n, who))) return rc;
-    KeyBatch kb = key_batch(keys);
-    uint32_t *order = nullptr;
-    bool order_keys = true;
-    if ((rc = multiget_order(r, kb, (hipStream_t)stream, &order, &order_keys))) return rc;
-    HIP_OR_FAIL(launch_multiget(kb, (const RegSlot *)r->dslots.p, r->nslots, mg_layout(r), (const uint8_t *)r->dranges.p,
-                                maybe, cand, cap, (hipStream_t)stream,
-                                order, order_keys));
-    return SEB_OK;
+    return multiget_launch(r, key_batch(keys), maybe, cand, cap, (hipStream_t)stream);
 }
 
 static int registry_multiget_host_locked(seb_registry *r, const seb_keys *kb, uint64_t *maybe, uint16_t *cand,
@@ -2152,12 +2158,9 @@ static int registry_multiget_host_locked(seb_registry *r, const seb_keys *kb, ui
         if ((rc = stage_chunk(c, kb, chunks[j], b, &dk, false))) return rc;
         if ((rc = c->out[b].reserve(dk.n * per_key))) return rc;
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_comp, c->ev_d2h[b], 0));
-        uint32_t *order = nullptr;
-        bool order_keys = true;
-        if ((rc = multiget_order(r, dk, c->s_comp, &order, &order_keys))) return rc;
-        HIP_OR_FAIL(launch_multiget(dk, (const RegSlot *)r->dslots.p, r->nslots, mg_layout(r),
-                                    (const uint8_t *)r->dranges.p, maybe ? (uint64_t *)c->out[b].p : nullptr,
-                                    maybe ? nullptr : (uint16_t *)c->out[b].p, cap, c->s_comp, order, order_keys));
+        if ((rc = multiget_launch(r, dk, maybe ? (uint64_t *)c->out[b].p : nullptr,
+                                  maybe ? nullptr : (uint16_t *)c->out[b].p, cap, c->s_comp)))
+            return rc;
         HIP_OR_FAIL(hipEventRecord(c->ev_comp[b], c->s_comp));
         HIP_OR_FAIL(hipStreamWaitEvent(c->s_d2h, c->ev_comp[b], 0));
         uint8_t *dst = maybe ? (uint8_t *)(maybe + chunks[j].i0) : (uint8_t *)(cand + chunks[j].i0 * cap);

@@ -89,21 +89,30 @@ hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mo
                           hipStream_t s);
 // cand != null: the list form (cap u16 slots per key, any nslots) instead of masks.
 constexpr uint32_t kRegMaxFiles = 4096;  // registry capacity (u16 slot ids, 0xFFFF = none)
-// order != null: key j answers at index order[j]; order_keys: key j is read as key order[j] of kb
-// (else kb already holds the keys in that order).
+// Answer j goes to row j of maybe / cand; key_order != null: key j is read as key key_order[j] of kb.
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
                            const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap, hipStream_t s,
-                           const uint32_t *order, bool order_keys);
+                           const uint32_t *key_order);
 // Key-range order for MultiGet: buckets = files of slots [lo, hi) (a disjoint, MinKey-ordered
-// level) with MinKey <= key.  *order_out stays null when the level does not apply.
+// level) with MinKey <= key.  The MultiGet then answers into mo.answers (sorted rows) and
+// launch_multiget_unpermute writes them to the caller's output in batch order.
 constexpr uint32_t kMgMaxBuckets = 1025;
-// Aligned fixed 16-B batches are moved into that order with their index (16 B more per key).
+struct MgOrder {
+    bool active = false;          // false: the level does not apply; answer in batch order directly
+    uint64_t n = 0;
+    uint32_t nb = 0, bits = 0, tiles = 0, tile_keys = 0;
+    const uint16_t *bucket = nullptr;
+    const uint32_t *hist = nullptr, *totals = nullptr;
+    const uint32_t *key_order = nullptr;  // batches that are not moved: key index of each sorted row
+    const uint8_t *keys = nullptr;        // aligned fixed 16-B batches: the keys moved into that order
+    void *answers = nullptr;              // n * answer_bytes: the MultiGet's answers in sorted rows
+};
+// Aligned fixed 16-B batches are moved into that order (16 B more per key), others get an index.
 bool multiget_order_moves(const KeyBatch &kb);
-uint64_t multiget_order_bytes(const KeyBatch &kb);
-// *keys_out: the 16-B keys moved into that order (multiget_order_moves), else null.
+uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes);
 hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
-                                 const uint8_t *ranges, void *ws, uint32_t **order_out, const uint8_t **keys_out,
-                                 hipStream_t s);
+                                 const uint8_t *ranges, void *ws, MgOrder *mo, hipStream_t s);
+hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answer_bytes, hipStream_t s);
 
 // Process-wide tuning knobs (seb_set_option): the auto-dispatch thresholds, the build algorithm,
 // and the few shape choices tests force to cover both paths.  Variants measured slower were

@@ -92,8 +92,7 @@ template <typename Src, int KFIX, bool M32, int MODE>
 __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const RegSlot *__restrict__ gslots,
                                                   uint32_t nslots, RegLayout lay, const uint8_t *__restrict__ ranges,
                                                   uint64_t *__restrict__ maybe, uint16_t *__restrict__ cand,
-                                                  uint32_t cap, const uint32_t *__restrict__ order,
-                                                  uint32_t order_keys) {
+                                                  uint32_t cap, const uint32_t *__restrict__ key_order) {
     constexpr bool kLds = MODE < 2, kList = MODE > 0;
     __shared__ RegSlot lslots[kLds ? kMaxSlots : 1];
     if constexpr (kLds) {
@@ -108,10 +107,11 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                              : (cap % 2 == 0 && ((uintptr_t)cand & 3) == 0) ? 4u : 2u;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < kb.n; j += stride) {
-        // key-range order (multiget_order): answer index oi = order[j]; the keys are read through the
-        // order too, or (order_keys == 0) were moved into that order by k_mg_scatter
-        const uint64_t oi = order ? (uint64_t)order[j] : j;
-        const uint64_t i = order_keys ? oi : j;
+        // Answer j goes to row j.  In key-range order (multiget_order) that is the sorted position:
+        // the keys were moved into that order by k_mg_scatter or are read through key_order, and
+        // k_mg_unpermute brings the answers back to batch order as whole lines.
+        const uint64_t oi = j;
+        const uint64_t i = key_order ? (uint64_t)key_order[j] : j;
         const uint8_t *key;
         uint32_t klen;
         if (kb.offsets) {
@@ -217,21 +217,26 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
 // sorting it, by one counting pass over the buckets of the partition level (the disjoint level
 // with the most files; a key's bucket = the number of its files whose MinKey <= key, monotone in
 // the key), like one digit of a radix sort:
-//   k_mg_bucket   tile t of the batch: each key's bucket, and the tile's bucket counts at
-//                 hist[b * T + t] (bucket-major, so one exclusive scan of hist yields every
-//                 (bucket, tile) output offset)
-//   k_mg_rows     scans each bucket's row of T tile counts in place, and writes the row total
-//   k_mg_scatter  tile t: scans the row totals into bucket bases, then per chunk of kMgChunk keys
-//                 sorts the key indices by bucket in LDS and writes each bucket's run of indices,
-//                 and of 16-B keys read through them (lines of the chunk just fetched into L2),
-//                 contiguously
-// k_multiget then walks `order` and writes every answer at the key's own index, so the results
-// are those of the batch order.  Round 3 replaced global cursor atomics per tile and per-lane
-// scattered stores with this (1.022 -> 1.010 ms on 28 files, 1.322 -> 1.183 ms on 244; DESIGN.md
-// 5.7 has the variants measured on the way).
-constexpr uint32_t kMgChunk = 2048;  // keys sorted in LDS at a time by k_mg_scatter
+//   k_mg_bucket     tile t of the batch: each key's bucket, and the tile's bucket counts at
+//                   hist[b * T + t] (bucket-major, so one exclusive scan of hist yields every
+//                   (bucket, tile) output offset)
+//   k_mg_rows       scans each bucket's row of T tile counts in place, and writes the row total
+//   k_mg_scatter    tile t: scans the row totals into bucket bases, then per chunk of kMgChunk keys
+//                   ranks the keys by bucket (stable, chunk_positions) and writes each bucket's run
+//                   of 16-B keys (read through the chunk's lines just fetched into L2), or of key
+//                   indices for batches it cannot move, contiguously
+// k_multiget then writes answer j at sorted row j (whole lines, no scattered 8-B stores), and
+//   k_mg_unpermute  tile t, chunk by chunk: the same stable ranks from the bucket array give each
+//                   key its sorted row; the chunk's runs of answers are read into LDS (contiguous
+//                   runs) and written back in batch order as whole lines.
+// Round 3 wrote answers at each key's own index from k_multiget: one 32-B write per 8-B mask (517 MB
+// written per 10M-key call for 80 MB of masks, profiles/r04_lsm_pmc.csv); the order array (40 MB)
+// is no longer needed either for moved keys.
+constexpr uint32_t kMgChunk = 2048;  // keys ranked in LDS at a time by k_mg_scatter / k_mg_unpermute
 constexpr uint32_t kMgTiles = 768;   // most tiles (blocks) of the ordering passes: one round on 256 CUs
 constexpr uint32_t kMgBucketThreads = 1024;
+constexpr uint32_t kMgWaves = 4;                      // 256-thread ordering blocks
+constexpr uint32_t kMgSteps = kMgChunk / kMgWaves / 64;  // 64-key steps of one wave's chunk segment
 
 __device__ __forceinline__ void key_at(const KeyBatch &kb, uint64_t i, const uint8_t *&key, uint32_t &klen) {
     if (kb.offsets) {
@@ -275,6 +280,62 @@ __device__ uint32_t block_scan_lds(uint32_t *a, uint32_t n, uint32_t *wsum) {
 __device__ __forceinline__ uint64_t tile_begin(uint64_t n, uint32_t tl, uint32_t t) {
     const uint64_t b = (uint64_t)tl * t;
     return b < n ? b : n;
+}
+
+// Chunk key q of this thread's step s: wave w owns the chunk's keys [w * 512, (w + 1) * 512), lane
+// l of step s holds key w * 512 + s * 64 + l.
+__device__ __forceinline__ uint32_t chunk_key(uint32_t s) {
+    return (threadIdx.x >> 6) * (kMgChunk / kMgWaves) + s * 64 + (threadIdx.x & 63);
+}
+
+// The chunk's sorted row of each of this thread's keys: bucket-major, keys of one bucket in chunk
+// order (stable, so k_mg_scatter and k_mg_unpermute derive the same rows from the bucket array
+// alone; no atomic decides a row).  Each wave ranks its segment step by step: equal buckets within
+// a step by __ballot peer masks (one ballot per bucket bit), across steps by the wave's running
+// count per bucket (cw[w][b]); then the buckets' chunk offsets (loc) and the waves before it.
+// bk[s]: bucket of key chunk_key(s) (>= nb for keys past cnt).  loc[0..nb] ends as the exclusive
+// scan of the chunk's bucket counts, loc[nb] = cnt.  Every thread calls it; it synchronises.
+__device__ __forceinline__ void chunk_positions(const uint32_t (&bk)[kMgSteps], uint32_t cnt, uint32_t nb,
+                                                uint32_t bits, uint32_t *cw, uint32_t *loc, uint32_t *wsum,
+                                                uint32_t (&pos)[kMgSteps]) {
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (uint32_t u = threadIdx.x; u < kMgWaves * nb; u += blockDim.x) cw[u] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t *mine = cw + w * nb;
+#pragma unroll
+    for (uint32_t s = 0; s < kMgSteps; ++s) {
+        const uint32_t b = bk[s];
+        uint64_t peers = ~0ull;
+        for (uint32_t i = 0; i < bits; ++i) {
+            const uint32_t set = (b >> i) & 1u;
+            const uint64_t bal = __ballot(set);
+            peers &= set ? bal : ~bal;
+        }
+        uint32_t before = 0;
+        if (b < nb) before = mine[b];  // every lane of the peer group reads before its leader writes
+        if (b < nb && (peers & lt) == 0) mine[b] = before + (uint32_t)__popcll(peers);
+        pos[s] = before + (uint32_t)__popcll(peers & lt);
+    }
+    __syncthreads();
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {
+        uint32_t t = 0;
+        for (uint32_t v = 0; v < kMgWaves; ++v) {  // cw[v][u] becomes the waves-before offset
+            const uint32_t c = cw[v * nb + u];
+            cw[v * nb + u] = t;
+            t += c;
+        }
+        loc[u] = t;
+    }
+    __syncthreads();
+    block_scan_lds(loc, nb, wsum);
+    if (threadIdx.x == 0) loc[nb] = cnt;
+#pragma unroll
+    for (uint32_t s = 0; s < kMgSteps; ++s) {
+        const uint32_t b = bk[s];
+        if (b < nb) pos[s] += loc[b] + mine[b];
+    }
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(kMgBucketThreads) void k_mg_bucket(KeyBatch kb, const RegSlot *__restrict__ slots, uint32_t lo,
@@ -335,63 +396,116 @@ __global__ __launch_bounds__(256) void k_mg_rows(uint32_t *__restrict__ hist, ui
     if (threadIdx.x == 0) totals[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *__restrict__ bucket,
-                                                    const uint32_t *__restrict__ hist,
-                                                    const uint32_t *__restrict__ totals, uint32_t nb,
-                                                    uint32_t *__restrict__ order, const uint4 *__restrict__ keys,
-                                                    uint4 *__restrict__ keys_out, uint32_t tl) {
-    __shared__ uint32_t base[kMgMaxBuckets];     // next output position of each bucket for this tile
-    __shared__ uint32_t loc[kMgMaxBuckets + 1];  // chunk counts, then their exclusive scan
-    __shared__ uint32_t sidx[kMgChunk];
-    __shared__ uint16_t sb[kMgChunk];
-    __shared__ uint32_t wsum[4];
-    constexpr uint32_t kPer = kMgChunk / 256;
+// Bucket bases of tile t: the exclusive scan of the row totals plus the tile's row offsets.
+__device__ __forceinline__ void tile_bases(const uint32_t *hist, const uint32_t *totals, uint32_t nb, uint32_t *base,
+                                           uint32_t *wsum) {
     const uint32_t T = gridDim.x, t = blockIdx.x;
     for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] = totals[u];
     __syncthreads();
     block_scan_lds(base, nb, wsum);
     for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] += hist[(uint64_t)u * T + t];
-    const uint64_t end = tile_begin(n, tl, t + 1);
-    uint32_t bk[kPer], rk[kPer];
-    auto load = [&](uint64_t c0) {  // chunk c0's buckets into registers
-        const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, end - c0);
+}
+
+// The buckets of chunk [c0, end) into registers (nb, i.e. "no key", past the end).
+__device__ __forceinline__ void load_chunk_buckets(const uint16_t *bucket, uint64_t c0, uint64_t end, uint32_t nb,
+                                                   uint32_t (&bk)[kMgSteps]) {
+    const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, end - c0);
 #pragma unroll
-        for (uint32_t r = 0; r < kPer; ++r) {
-            const uint32_t q = r * 256 + threadIdx.x;
-            bk[r] = q < cnt ? bucket[c0 + q] : 0u;
-        }
-    };
-    uint64_t c0 = tile_begin(n, tl, t);
-    if (c0 < end) load(c0);
+    for (uint32_t s = 0; s < kMgSteps; ++s) {
+        const uint32_t q = chunk_key(s);
+        bk[s] = q < cnt ? bucket[c0 + q] : nb;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *__restrict__ bucket,
+                                                    const uint32_t *__restrict__ hist,
+                                                    const uint32_t *__restrict__ totals, uint32_t nb, uint32_t bits,
+                                                    uint32_t *__restrict__ order, const uint4 *__restrict__ keys,
+                                                    uint4 *__restrict__ keys_out, uint32_t tl) {
+    __shared__ uint32_t base[kMgMaxBuckets];     // next output row of each bucket for this tile
+    __shared__ uint32_t loc[kMgMaxBuckets + 1];  // the chunk's bucket offsets
+    __shared__ uint32_t cw[kMgWaves * kMgMaxBuckets];
+    __shared__ uint32_t sidx[kMgChunk];
+    __shared__ uint16_t sb[kMgChunk];
+    __shared__ uint32_t wsum[4];
+    tile_bases(hist, totals, nb, base, wsum);
+    const uint64_t end = tile_begin(n, tl, blockIdx.x + 1);
+    uint32_t bk[kMgSteps], pos[kMgSteps];
+    uint64_t c0 = tile_begin(n, tl, blockIdx.x);
+    if (c0 < end) load_chunk_buckets(bucket, c0, end, nb, bk);
     for (; c0 < end; c0 += kMgChunk) {
         const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, end - c0);
-        for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) loc[u] = 0;
-        __syncthreads();
+        chunk_positions(bk, cnt, nb, bits, cw, loc, wsum, pos);
 #pragma unroll
-        for (uint32_t r = 0; r < kPer; ++r)
-            if (r * 256 + threadIdx.x < cnt) rk[r] = atomicAdd(&loc[bk[r]], 1u);
-        __syncthreads();
-        block_scan_lds(loc, nb, wsum);
-        if (threadIdx.x == 0) loc[nb] = cnt;
-#pragma unroll
-        for (uint32_t r = 0; r < kPer; ++r) {
-            const uint32_t q = r * 256 + threadIdx.x;
-            if (q < cnt) {
-                const uint32_t p = loc[bk[r]] + rk[r];
-                sidx[p] = (uint32_t)(c0 + q);
-                sb[p] = (uint16_t)bk[r];
+        for (uint32_t s = 0; s < kMgSteps; ++s)
+            if (bk[s] < nb) {
+                sidx[pos[s]] = (uint32_t)(c0 + chunk_key(s));
+                sb[pos[s]] = (uint16_t)bk[s];
             }
-        }
         __syncthreads();
-        if (c0 + kMgChunk < end) load(c0 + kMgChunk);  // the next chunk's buckets load during the stores
+        if (c0 + kMgChunk < end) load_chunk_buckets(bucket, c0 + kMgChunk, end, nb, bk);  // during the stores
         // each bucket's run of this chunk goes out contiguously
         for (uint32_t q = threadIdx.x; q < cnt; q += blockDim.x) {
             const uint32_t b = sb[q];
             const uint32_t dst = base[b] + (q - loc[b]);
-            order[dst] = sidx[q];
-            if (keys_out) keys_out[dst] = keys[sidx[q]];
+            if (keys_out)
+                keys_out[dst] = keys[sidx[q]];
+            else
+                order[dst] = sidx[q];
         }
         __syncthreads();
+        for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] += loc[u + 1] - loc[u];
+        __syncthreads();
+    }
+}
+
+// out[i] = sorted[row of key i], ge granules of G per answer (masks: two u32; candidate rows: cap u16
+// or cap/2 u32), chunk by chunk in the tiles of k_mg_scatter: the chunk's sorted runs are staged in
+// LDS 8 bytes of each answer at a time and written back in batch order.
+template <typename G>
+__global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const uint16_t *__restrict__ bucket,
+                                                      const uint32_t *__restrict__ hist,
+                                                      const uint32_t *__restrict__ totals, uint32_t nb, uint32_t bits,
+                                                      const G *__restrict__ sorted, G *__restrict__ out, uint32_t ge,
+                                                      uint32_t tl) {
+    __shared__ uint32_t base[kMgMaxBuckets];
+    __shared__ uint32_t loc[kMgMaxBuckets + 1];
+    __shared__ uint32_t cw[kMgWaves * kMgMaxBuckets];
+    __shared__ uint16_t sb[kMgChunk];   // bucket of each chunk row
+    __shared__ uint16_t rowq[kMgChunk]; // chunk row of each chunk key
+    constexpr uint32_t kMgSlice = 8 / sizeof(G);  // granules staged per answer per pass
+    __shared__ G stage[kMgChunk * kMgSlice];
+    __shared__ uint32_t wsum[4];
+    tile_bases(hist, totals, nb, base, wsum);
+    const uint64_t end = tile_begin(n, tl, blockIdx.x + 1);
+    uint32_t bk[kMgSteps], pos[kMgSteps];
+    for (uint64_t c0 = tile_begin(n, tl, blockIdx.x); c0 < end; c0 += kMgChunk) {
+        const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, end - c0);
+        load_chunk_buckets(bucket, c0, end, nb, bk);
+        chunk_positions(bk, cnt, nb, bits, cw, loc, wsum, pos);
+#pragma unroll
+        for (uint32_t s = 0; s < kMgSteps; ++s)
+            if (bk[s] < nb) {
+                sb[pos[s]] = (uint16_t)bk[s];
+                rowq[chunk_key(s)] = (uint16_t)pos[s];
+            }
+        __syncthreads();
+        for (uint32_t g0 = 0; g0 < ge; g0 += kMgSlice) {
+            const uint32_t gs = min(kMgSlice, ge - g0);
+            for (uint32_t u = threadIdx.x; u < cnt * gs; u += blockDim.x) {  // the chunk's runs, contiguous
+                const uint32_t p = u / gs, g = u - p * gs;
+                const uint32_t b = min((uint32_t)sb[p], nb - 1);
+                uint64_t row = base[b] + (p - loc[b]);
+                row = row < n ? row : n - 1;  // always true when the ranks are a permutation; a guard
+                stage[p * kMgSlice + g] = sorted[row * ge + g0 + g];
+            }
+            __syncthreads();
+            for (uint32_t u = threadIdx.x; u < cnt * gs; u += blockDim.x) {  // batch order, whole lines
+                const uint32_t q = u / gs, g = u - q * gs;
+                out[(c0 + q) * ge + g0 + g] = stage[rowq[q] * kMgSlice + g];
+            }
+            __syncthreads();
+        }
         for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] += loc[u + 1] - loc[u];
         __syncthreads();
     }
@@ -442,41 +556,68 @@ static uint32_t order_tiles(uint64_t n) {
 
 static uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
 
-uint64_t multiget_order_bytes(const KeyBatch &kb) {
+uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes) {
     const uint64_t n = kb.n;
-    return al256(n * 2) + al256(n * 4) + al256(4ull * kMgMaxBuckets * order_tiles(n)) + al256(4 * kMgMaxBuckets) +
-           (multiget_order_moves(kb) ? n * 16 : 0);
+    return al256(n * 2) + al256(4ull * kMgMaxBuckets * order_tiles(n)) + al256(4 * kMgMaxBuckets) +
+           al256(multiget_order_moves(kb) ? n * 16 : n * 4) + al256(n * answer_bytes);
 }
 
 hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
-                                 const uint8_t *ranges, void *ws, uint32_t **order_out, const uint8_t **keys_out,
-                                 hipStream_t s) {
-    *order_out = nullptr;
-    *keys_out = nullptr;
+                                 const uint8_t *ranges, void *ws, MgOrder *mo, hipStream_t s) {
+    *mo = MgOrder{};
     const uint32_t nb = hi - lo + 1;
     if (kb.n == 0 || nb > kMgMaxBuckets || nb < 2 || kb.n > 0xffffffffull) return hipSuccess;
     const uint32_t T = order_tiles(kb.n), tl = tile_keys(kb.n);
     uint8_t *p = (uint8_t *)ws;
     uint16_t *bucket = (uint16_t *)p;
-    uint32_t *order = (uint32_t *)(p += al256(kb.n * 2));
-    uint32_t *hist = (uint32_t *)(p += al256(kb.n * 4));
+    uint32_t *hist = (uint32_t *)(p += al256(kb.n * 2));
     uint32_t *totals = (uint32_t *)(p += al256(4ull * kMgMaxBuckets * T));
-    // aligned fixed 16-B keys are moved into bucket order as well (the MultiGet then streams them)
-    uint4 *sorted = multiget_order_moves(kb) ? (uint4 *)(p + al256(4 * kMgMaxBuckets)) : nullptr;
+    uint8_t *moved = p += al256(4 * kMgMaxBuckets);
+    const bool moves = multiget_order_moves(kb);
+    void *answers = p + al256(moves ? kb.n * 16 : kb.n * 4);
+    uint32_t bits = 0;
+    while ((1u << bits) <= nb) ++bits;  // bucket ids and the "no key" value nb
     hipLaunchKernelGGL(k_mg_bucket, dim3(T), dim3(kMgBucketThreads), 0, s, kb, slots, lo, hi, ranges, bucket, hist, tl);
     hipLaunchKernelGGL(k_mg_rows, dim3(nb), dim3(256), 0, s, hist, T, totals);
-    hipLaunchKernelGGL(k_mg_scatter, dim3(T), dim3(256), 0, s, kb.n, bucket, hist, totals, nb, order,
-                       (const uint4 *)kb.data, sorted, tl);
+    // aligned fixed 16-B keys are moved into bucket order (the MultiGet then streams them); other
+    // batches get the key indices in that order
+    hipLaunchKernelGGL(k_mg_scatter, dim3(T), dim3(256), 0, s, kb.n, bucket, hist, totals, nb, bits,
+                       moves ? nullptr : (uint32_t *)moved, (const uint4 *)kb.data, moves ? (uint4 *)moved : nullptr, tl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    *order_out = order;
-    *keys_out = (const uint8_t *)sorted;
+    mo->active = true;
+    mo->n = kb.n;
+    mo->nb = nb;
+    mo->bits = bits;
+    mo->tiles = T;
+    mo->tile_keys = tl;
+    mo->bucket = bucket;
+    mo->hist = hist;
+    mo->totals = totals;
+    mo->key_order = moves ? nullptr : (const uint32_t *)moved;
+    mo->keys = moves ? moved : nullptr;
+    mo->answers = answers;
     return hipSuccess;
+}
+
+hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answer_bytes, hipStream_t s) {
+    if (!mo.active || mo.n == 0) return hipSuccess;
+    if (answer_bytes % 4 == 0)
+        hipLaunchKernelGGL(k_mg_unpermute<uint32_t>, dim3(mo.tiles), dim3(256), 0, s, mo.n, mo.bucket, mo.hist, mo.totals,
+                           mo.nb, mo.bits, (const uint32_t *)mo.answers, (uint32_t *)out, (uint32_t)(answer_bytes / 4),
+                           mo.tile_keys);
+    else if (answer_bytes % 2 == 0)
+        hipLaunchKernelGGL(k_mg_unpermute<uint16_t>, dim3(mo.tiles), dim3(256), 0, s, mo.n, mo.bucket, mo.hist, mo.totals,
+                           mo.nb, mo.bits, (const uint16_t *)mo.answers, (uint16_t *)out, (uint32_t)(answer_bytes / 2),
+                           mo.tile_keys);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
 }
 
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
                            const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap, hipStream_t s,
-                           const uint32_t *order, bool order_keys) {
+                           const uint32_t *key_order) {
     if (kb.n == 0) return hipSuccess;
     if (!cand && nslots > kMaxSlots) return hipErrorInvalidValue;  // the mask form stages slots in LDS
     uint64_t g = (kb.n + 255) / 256;
@@ -486,7 +627,7 @@ hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t ns
         using S = decltype(src);
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe, cand,
-                               cap, order, (uint32_t)(order && order_keys));
+                               cap, key_order);
             return hipGetLastError();
         };
         if (lay.all_k7_m32) {

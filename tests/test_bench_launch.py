@@ -34,6 +34,36 @@ def test_gpus_n_spawns_n_ranks(n):
     assert d["n_gpus"] == n
     assert d["rank_sum"] == n * (n + 1) // 2
     assert d["master"].startswith("127.0.0.1:")
+    # the per-rank records the N-GPU line carries, here on gloo without a GPU
+    recs = d["per_rank"]
+    assert [r["rank"] for r in recs] == list(range(n))
+    for r in recs:
+        assert r["world_size"] == n and r["allreduce_ones"] == n and r["backend"] == "gloo"
+        assert r["device"] is None and r["local_rank"] == r["rank"] and r["host"]
+        assert set(r) >= {"kernel_ms", "wait_ms", "wait_host_ms", "elapsed_s"}
+    assert d["devices"] == 0 and d["problems"] == []
+
+
+def test_rank_report_summary():
+    """rank_report.summarize: distinct GPUs by (host, PCI address); an RCCL run whose ranks share a
+    GPU, disagree on the world size or miss an all-reduce contribution is flagged."""
+    sys.path.insert(0, os.path.join(ROOT, "storage-engines_amd"))
+    import rank_report as rr
+
+    def rec(rank, pci, ones=2, world=2, backend="nccl", elapsed=1.0):
+        dev = {"index": rank, "current_device": rank, "pci": pci, "name": "x", "arch": "gfx950", "uuid": ""}
+        r = rr.rank_record(rank, rank, world, backend, dev, ones, {"build": 0.2, "probe": 0.3}, 0.05, 0.01, elapsed)
+        r["host"] = "h"
+        return r
+
+    ok = rr.summarize([rec(0, "0000:05:00.0"), rec(1, "0000:15:00.0", elapsed=1.5)], 2, "nccl")
+    assert ok["devices"] == 2 and ok["problems"] == [] and ok["slowest_rank"] == 1
+    assert ok["elapsed_s_spread"] == 0.5 and ok["wait_ms_max"] == 0.05
+    same = rr.summarize([rec(0, "0000:05:00.0"), rec(1, "0000:05:00.0")], 2, "nccl")
+    assert same["devices"] == 1 and any("distinct GPU" in p for p in same["problems"])
+    assert rr.summarize([rec(0, "a", backend="gloo"), rec(1, "a", backend="gloo")], 2, "gloo")["problems"] == []
+    bad = rr.summarize([rec(0, "a", ones=1), rec(1, "b", world=3)], 2, "nccl")
+    assert len(bad["problems"]) == 2
 
 
 def test_world_size_must_match_gpus():

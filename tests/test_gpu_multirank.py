@@ -30,7 +30,16 @@ def _bench(*args, timeout=170):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
-    return json.loads(lines[0])
+    d = json.loads(lines[0])
+    # the per-rank records: both ranks on the box's one GPU under gloo
+    recs = d["per_rank"]
+    assert len(recs) == 2 and [r["rank"] for r in recs] == [0, 1]
+    assert d["devices"] == 1 and d["rank_check"]["problems"] == []
+    for r in recs:
+        assert r["backend"] == "gloo" and r["world_size"] == 2 and r["allreduce_ones"] == 2
+        assert r["device"]["arch"].startswith("gfx950") and r["device"]["pci"] == recs[0]["device"]["pci"]
+        assert r["kernel_ms"] and r["elapsed_s"] > 0 and r["wait_ms"] is not None
+    return d
 
 
 def test_c5_filter_split_two_ranks():
