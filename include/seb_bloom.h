@@ -103,6 +103,8 @@ int seb_abi_version(void);
  *   "multiget_l0_group" registry MultiGet tests the L0 files that share (m, k) through one
  *                     bit-interleaved table, one gather per position for all of them (1, default)
  *   "varlen_prehash_min_keys"  variable-length batches of this many keys are pre-hashed in LDS
+ *   "varlen_long"     packed pre-hash (k == 7 filters): keys over 48 B are hashed first by a pass that
+ *                     groups them by length across 8192 keys (1), or all in the LDS pre-hash (0)
  *   "varlen_tail"     pre-hash: the 64 longest keys of a workgroup run on two waves, one per FNV
  *                     chain (1, default), or one key per lane like the others (0)
  *   "grid_cap"        maximum workgroups of the grid-stride kernels
