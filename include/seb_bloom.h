@@ -102,6 +102,9 @@ int seb_abi_version(void);
  *                     or batch order (0)
  *   "multiget_l0_group" registry MultiGet tests the L0 files that share (m, k) through one
  *                     bit-interleaved table, one gather per position for all of them (1, default)
+ *   "multiget_xcd"    registry MultiGet: the workgroups that share an XCD walk one contiguous eighth of
+ *                     the (key-range ordered) batch, so each XCD's L2 holds its own stretch's filters
+ *                     (1, default), or blocks walk the batch in launch order (0)
  *   "varlen_prehash_min_keys"  variable-length batches of this many keys are pre-hashed in LDS
  *   "varlen_long"     packed pre-hash (k == 7 filters): keys over 48 B are hashed first by a pass that
  *                     groups them by length across 8192 keys (1), or all in the LDS pre-hash (0)

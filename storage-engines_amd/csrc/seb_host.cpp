@@ -152,6 +152,7 @@ static const OptionDesc kOptions[] = {
     SEB_OPT(multi_interleave, 0, 1),
     SEB_OPT(multiget_order, 0, 1),
     SEB_OPT(multiget_l0_group, 0, 1),
+    SEB_OPT(multiget_xcd, 0, 1),
     SEB_OPT(varlen_prehash_min_keys, 0, INT64_MAX),
     SEB_OPT(bucket_min_keys, 0, INT64_MAX),
     SEB_OPT(lds_min_keys, 0, INT64_MAX),

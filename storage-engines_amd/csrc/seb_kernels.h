@@ -100,9 +100,7 @@ constexpr uint32_t kMgMaxBuckets = 1025;
 struct MgOrder {
     bool active = false;          // false: the level does not apply; answer in batch order directly
     uint64_t n = 0;
-    uint32_t nb = 0, bits = 0, tiles = 0, tile_keys = 0;
-    const uint16_t *bucket = nullptr;
-    const uint32_t *hist = nullptr, *totals = nullptr;
+    const uint32_t *rowpos = nullptr;     // each key's sorted row, in batch order
     const uint32_t *key_order = nullptr;  // batches that are not moved: key index of each sorted row
     const uint8_t *keys = nullptr;        // aligned fixed 16-B batches: the keys moved into that order
     void *answers = nullptr;              // n * answer_bytes: the MultiGet's answers in sorted rows
@@ -123,6 +121,8 @@ struct Options {
     int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
     int multiget_order = 1;       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
     int multiget_l0_group = 1;    // MultiGet: L0 files of one (m, k) tested through one interleaved table
+    int multiget_xcd = 1;         // MultiGet: the blocks sharing an XCD walk one contiguous eighth of the batch
+                                  // (1, default: 575 vs 596 us per 10M-key k_multiget on 28 files), or not (0)
     int probe_compact = 1;        // phased probe from keys: later phases read only the live keys' words
     int scatter_tiles_exact = 0;  // bin scatter: rounds shrunk so the tiles fill all 256 CUs (1) (being measured)
     int scatter_bins = 1;         // bucketed build, k == 7: scatter through fixed LDS bins, pipelined against the

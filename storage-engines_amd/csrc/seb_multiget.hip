@@ -92,7 +92,8 @@ template <typename Src, int KFIX, bool M32, int MODE>
 __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const RegSlot *__restrict__ gslots,
                                                   uint32_t nslots, RegLayout lay, const uint8_t *__restrict__ ranges,
                                                   uint64_t *__restrict__ maybe, uint16_t *__restrict__ cand,
-                                                  uint32_t cap, const uint32_t *__restrict__ key_order) {
+                                                  uint32_t cap, const uint32_t *__restrict__ key_order,
+                                                  uint32_t xcd) {
     constexpr bool kLds = MODE < 2, kList = MODE > 0;
     __shared__ RegSlot lslots[kLds ? kMaxSlots : 1];
     if constexpr (kLds) {
@@ -106,7 +107,16 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                              : (cap % 4 == 0 && ((uintptr_t)cand & 7) == 0) ? 8u
                              : (cap % 2 == 0 && ((uintptr_t)cand & 3) == 0) ? 4u : 2u;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < kb.n; j += stride) {
+    // xcd: the blocks that share an XCD (blockIdx % 8 under round-robin placement, speed only) take
+    // one contiguous eighth of the batch, so in key-range order each XCD's L2 holds the filters of
+    // its own key stretch instead of every XCD holding the whole chip's window (bijective remap,
+    // cdna_hip_programming.md T1)
+    uint32_t wg = blockIdx.x;
+    if (xcd) {
+        const uint32_t q = gridDim.x / 8, r = gridDim.x % 8, x = blockIdx.x % 8;
+        wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
+    }
+    for (uint64_t j = (uint64_t)wg * blockDim.x + threadIdx.x; j < kb.n; j += stride) {
         // Answer j goes to row j.  In key-range order (multiget_order) that is the sorted position:
         // the keys were moved into that order by k_mg_scatter or are read through key_order, and
         // k_mg_unpermute brings the answers back to batch order as whole lines.
@@ -223,17 +233,18 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
 //   k_mg_rows       scans each bucket's row of T tile counts in place, and writes the row total
 //   k_mg_scatter    tile t: scans the row totals into bucket bases, then per chunk of kMgChunk keys
 //                   ranks the keys by bucket (stable, chunk_positions) and writes each bucket's run
-//                   of 16-B keys (read through the chunk's lines just fetched into L2), or of key
-//                   indices for batches it cannot move, contiguously
+//                   of 16-B keys (read through the chunk's lines), or of key indices for batches it
+//                   cannot move, contiguously, and each key's sorted row (rowpos, in batch order)
 // k_multiget then writes answer j at sorted row j (whole lines, no scattered 8-B stores), and
-//   k_mg_unpermute  tile t, chunk by chunk: the same stable ranks from the bucket array give each
-//                   key its sorted row; the chunk's runs of answers are read into LDS (contiguous
-//                   runs) and written back in batch order as whole lines.
+//   k_mg_unpermute  out[i] = answers[rowpos[i]]: reads from the chunks' contiguous runs, writes
+//                   whole lines in batch order.
 // Round 3 wrote answers at each key's own index from k_multiget: one 32-B write per 8-B mask (517 MB
 // written per 10M-key call for 80 MB of masks, profiles/r04_lsm_pmc.csv); the order array (40 MB)
 // is no longer needed either for moved keys.
 constexpr uint32_t kMgChunk = 2048;  // keys ranked in LDS at a time by k_mg_scatter / k_mg_unpermute
-constexpr uint32_t kMgTiles = 768;   // most tiles (blocks) of the ordering passes: one round on 256 CUs
+// Most tiles (blocks) of the ordering passes: one round on 256 CUs.  2048 and 8192 tiles (one chunk
+// each, no serial chunk loop) measured the same within 1% (profiles/r05e_mg_tiles.txt).
+constexpr uint32_t kMgTiles = 768;
 constexpr uint32_t kMgBucketThreads = 1024;
 constexpr uint32_t kMgWaves = 4;                      // 256-thread ordering blocks
 constexpr uint32_t kMgSteps = kMgChunk / kMgWaves / 64;  // 64-key steps of one wave's chunk segment
@@ -417,17 +428,33 @@ __device__ __forceinline__ void load_chunk_buckets(const uint16_t *bucket, uint6
     }
 }
 
+// LDS (dynamic, sized by nb): base[nb] | loc[nb + 1] | cw[kMgWaves * nb] | wsum[4] (u32), then
+// sb[kMgChunk] (u16), then the chunk's key indices in sorted order (u32).
+static size_t mg_scatter_lds(uint32_t nb) {
+    const size_t words = (size_t)nb + (nb + 1) + (size_t)kMgWaves * nb + 4;
+    return ((words * 4 + 2 * kMgChunk + 15) & ~(size_t)15) + (size_t)kMgChunk * 4;
+}
+
+// MOVE: aligned 16-B keys, read through the chunk's sorted indices (the chunk's 32 KB of lines come
+// into L2 on first touch) and stored as contiguous bucket runs.  Staging them instead in LDS, loaded
+// in batch order a chunk ahead, measured slower (163 vs 115 us, profiles/r05d_mg_stage.txt).
+// Otherwise the key indices are written in that order (key_order) for the MultiGet to read keys
+// through.
+template <bool MOVE>
 __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *__restrict__ bucket,
                                                     const uint32_t *__restrict__ hist,
                                                     const uint32_t *__restrict__ totals, uint32_t nb, uint32_t bits,
                                                     uint32_t *__restrict__ order, const uint4 *__restrict__ keys,
-                                                    uint4 *__restrict__ keys_out, uint32_t tl) {
-    __shared__ uint32_t base[kMgMaxBuckets];     // next output row of each bucket for this tile
-    __shared__ uint32_t loc[kMgMaxBuckets + 1];  // the chunk's bucket offsets
-    __shared__ uint32_t cw[kMgWaves * kMgMaxBuckets];
-    __shared__ uint32_t sidx[kMgChunk];
-    __shared__ uint16_t sb[kMgChunk];
-    __shared__ uint32_t wsum[4];
+                                                    uint4 *__restrict__ keys_out, uint32_t *__restrict__ rowpos,
+                                                    uint32_t tl) {
+    extern __shared__ uint4 mg_lds[];
+    uint32_t *base = (uint32_t *)mg_lds;          // next output row of each bucket for this tile
+    uint32_t *loc = base + nb;                     // the chunk's bucket offsets
+    uint32_t *cw = loc + nb + 1;
+    uint32_t *wsum = cw + kMgWaves * nb;
+    uint16_t *sb = (uint16_t *)(wsum + 4);
+    uint32_t *sidx = (uint32_t *)((uint8_t *)mg_lds +
+                                  ((((size_t)nb + (nb + 1) + (size_t)kMgWaves * nb + 4) * 4 + 2 * kMgChunk + 15) & ~(size_t)15));
     tile_bases(hist, totals, nb, base, wsum);
     const uint64_t end = tile_begin(n, tl, blockIdx.x + 1);
     uint32_t bk[kMgSteps], pos[kMgSteps];
@@ -441,6 +468,8 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *
             if (bk[s] < nb) {
                 sidx[pos[s]] = (uint32_t)(c0 + chunk_key(s));
                 sb[pos[s]] = (uint16_t)bk[s];
+                // the key's sorted row, in batch order (coalesced): k_mg_unpermute gathers through it
+                rowpos[c0 + chunk_key(s)] = base[bk[s]] + (pos[s] - loc[bk[s]]);
             }
         __syncthreads();
         if (c0 + kMgChunk < end) load_chunk_buckets(bucket, c0 + kMgChunk, end, nb, bk);  // during the stores
@@ -448,7 +477,7 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *
         for (uint32_t q = threadIdx.x; q < cnt; q += blockDim.x) {
             const uint32_t b = sb[q];
             const uint32_t dst = base[b] + (q - loc[b]);
-            if (keys_out)
+            if constexpr (MOVE)
                 keys_out[dst] = keys[sidx[q]];
             else
                 order[dst] = sidx[q];
@@ -459,55 +488,18 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *
     }
 }
 
-// out[i] = sorted[row of key i], ge granules of G per answer (masks: two u32; candidate rows: cap u16
-// or cap/2 u32), chunk by chunk in the tiles of k_mg_scatter: the chunk's sorted runs are staged in
-// LDS 8 bytes of each answer at a time and written back in batch order.
-template <typename G>
-__global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const uint16_t *__restrict__ bucket,
-                                                      const uint32_t *__restrict__ hist,
-                                                      const uint32_t *__restrict__ totals, uint32_t nb, uint32_t bits,
-                                                      const G *__restrict__ sorted, G *__restrict__ out, uint32_t ge,
-                                                      uint32_t tl) {
-    __shared__ uint32_t base[kMgMaxBuckets];
-    __shared__ uint32_t loc[kMgMaxBuckets + 1];
-    __shared__ uint32_t cw[kMgWaves * kMgMaxBuckets];
-    __shared__ uint16_t sb[kMgChunk];   // bucket of each chunk row
-    __shared__ uint16_t rowq[kMgChunk]; // chunk row of each chunk key
-    constexpr uint32_t kMgSlice = 8 / sizeof(G);  // granules staged per answer per pass
-    __shared__ G stage[kMgChunk * kMgSlice];
-    __shared__ uint32_t wsum[4];
-    tile_bases(hist, totals, nb, base, wsum);
-    const uint64_t end = tile_begin(n, tl, blockIdx.x + 1);
-    uint32_t bk[kMgSteps], pos[kMgSteps];
-    for (uint64_t c0 = tile_begin(n, tl, blockIdx.x); c0 < end; c0 += kMgChunk) {
-        const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, end - c0);
-        load_chunk_buckets(bucket, c0, end, nb, bk);
-        chunk_positions(bk, cnt, nb, bits, cw, loc, wsum, pos);
-#pragma unroll
-        for (uint32_t s = 0; s < kMgSteps; ++s)
-            if (bk[s] < nb) {
-                sb[pos[s]] = (uint16_t)bk[s];
-                rowq[chunk_key(s)] = (uint16_t)pos[s];
-            }
-        __syncthreads();
-        for (uint32_t g0 = 0; g0 < ge; g0 += kMgSlice) {
-            const uint32_t gs = min(kMgSlice, ge - g0);
-            for (uint32_t u = threadIdx.x; u < cnt * gs; u += blockDim.x) {  // the chunk's runs, contiguous
-                const uint32_t p = u / gs, g = u - p * gs;
-                const uint32_t b = min((uint32_t)sb[p], nb - 1);
-                uint64_t row = base[b] + (p - loc[b]);
-                row = row < n ? row : n - 1;  // always true when the ranks are a permutation; a guard
-                stage[p * kMgSlice + g] = sorted[row * ge + g0 + g];
-            }
-            __syncthreads();
-            for (uint32_t u = threadIdx.x; u < cnt * gs; u += blockDim.x) {  // batch order, whole lines
-                const uint32_t q = u / gs, g = u - q * gs;
-                out[(c0 + q) * ge + g0 + g] = stage[rowq[q] * kMgSlice + g];
-            }
-            __syncthreads();
-        }
-        for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] += loc[u + 1] - loc[u];
-        __syncthreads();
+// out[i] = answers[rowpos[i]]: each key's answer from its sorted row, written in batch order as
+// whole lines.  The reads come from the chunk's bucket runs, each contiguous in the sorted rows, so
+// a wave's 64 keys read a few dozen runs and the lines are shared between neighbouring waves.
+// E: the answer as one unit (uint2 masks, u32/u16 granules of a candidate row, ge per answer).
+template <typename E>
+__global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const uint32_t *__restrict__ rowpos,
+                                                      const E *__restrict__ answers, E *__restrict__ out,
+                                                      uint32_t ge) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t r = rowpos[i];
+        for (uint32_t g = 0; g < ge; ++g) out[i * ge + g] = answers[r * ge + g];
     }
 }
 
@@ -559,7 +551,7 @@ static uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
 uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes) {
     const uint64_t n = kb.n;
     return al256(n * 2) + al256(4ull * kMgMaxBuckets * order_tiles(n)) + al256(4 * kMgMaxBuckets) +
-           al256(multiget_order_moves(kb) ? n * 16 : n * 4) + al256(n * answer_bytes);
+           al256(multiget_order_moves(kb) ? n * 16 : n * 4) + al256(n * 4) + al256(n * answer_bytes);
 }
 
 hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
@@ -574,26 +566,26 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
     uint32_t *totals = (uint32_t *)(p += al256(4ull * kMgMaxBuckets * T));
     uint8_t *moved = p += al256(4 * kMgMaxBuckets);
     const bool moves = multiget_order_moves(kb);
-    void *answers = p + al256(moves ? kb.n * 16 : kb.n * 4);
+    uint32_t *rowpos = (uint32_t *)(p + al256(moves ? kb.n * 16 : kb.n * 4));
+    void *answers = (uint8_t *)rowpos + al256(kb.n * 4);
     uint32_t bits = 0;
     while ((1u << bits) <= nb) ++bits;  // bucket ids and the "no key" value nb
     hipLaunchKernelGGL(k_mg_bucket, dim3(T), dim3(kMgBucketThreads), 0, s, kb, slots, lo, hi, ranges, bucket, hist, tl);
     hipLaunchKernelGGL(k_mg_rows, dim3(nb), dim3(256), 0, s, hist, T, totals);
     // aligned fixed 16-B keys are moved into bucket order (the MultiGet then streams them); other
     // batches get the key indices in that order
-    hipLaunchKernelGGL(k_mg_scatter, dim3(T), dim3(256), 0, s, kb.n, bucket, hist, totals, nb, bits,
-                       moves ? nullptr : (uint32_t *)moved, (const uint4 *)kb.data, moves ? (uint4 *)moved : nullptr, tl);
+    const size_t lds = mg_scatter_lds(nb);
+    auto scat = moves ? k_mg_scatter<true> : k_mg_scatter<false>;
+    hipError_t a = hipFuncSetAttribute((const void *)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (a != hipSuccess) return a;
+    hipLaunchKernelGGL(scat, dim3(T), dim3(256), lds, s, kb.n, bucket, hist, totals, nb, bits,
+                       moves ? nullptr : (uint32_t *)moved, (const uint4 *)kb.data, moves ? (uint4 *)moved : nullptr,
+                       rowpos, tl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     mo->active = true;
     mo->n = kb.n;
-    mo->nb = nb;
-    mo->bits = bits;
-    mo->tiles = T;
-    mo->tile_keys = tl;
-    mo->bucket = bucket;
-    mo->hist = hist;
-    mo->totals = totals;
+    mo->rowpos = rowpos;
     mo->key_order = moves ? nullptr : (const uint32_t *)moved;
     mo->keys = moves ? moved : nullptr;
     mo->answers = answers;
@@ -602,14 +594,25 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
 
 hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answer_bytes, hipStream_t s) {
     if (!mo.active || mo.n == 0) return hipSuccess;
-    if (answer_bytes % 4 == 0)
-        hipLaunchKernelGGL(k_mg_unpermute<uint32_t>, dim3(mo.tiles), dim3(256), 0, s, mo.n, mo.bucket, mo.hist, mo.totals,
-                           mo.nb, mo.bits, (const uint32_t *)mo.answers, (uint32_t *)out, (uint32_t)(answer_bytes / 4),
-                           mo.tile_keys);
+    uint64_t g = (mo.n + 255) / 256;
+    if (g > 65536) g = 65536;
+    const uint32_t *rp = mo.rowpos;
+    const bool a16 = ((uintptr_t)out & 15) == 0, a8 = ((uintptr_t)out & 7) == 0, a4 = ((uintptr_t)out & 3) == 0;
+    if (answer_bytes == 16 && a16)
+        hipLaunchKernelGGL(k_mg_unpermute<uint4>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
+                           (const uint4 *)mo.answers, (uint4 *)out, 1u);
+    else if (answer_bytes == 12 && a4)  // 6-slot candidate rows: one dwordx3 per key
+        hipLaunchKernelGGL(k_mg_unpermute<uint3>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
+                           (const uint3 *)mo.answers, (uint3 *)out, 1u);
+    else if (answer_bytes == 8 && a8)
+        hipLaunchKernelGGL(k_mg_unpermute<uint2>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
+                           (const uint2 *)mo.answers, (uint2 *)out, 1u);
+    else if (answer_bytes % 4 == 0 && a4)
+        hipLaunchKernelGGL(k_mg_unpermute<uint32_t>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
+                           (const uint32_t *)mo.answers, (uint32_t *)out, (uint32_t)(answer_bytes / 4));
     else if (answer_bytes % 2 == 0)
-        hipLaunchKernelGGL(k_mg_unpermute<uint16_t>, dim3(mo.tiles), dim3(256), 0, s, mo.n, mo.bucket, mo.hist, mo.totals,
-                           mo.nb, mo.bits, (const uint16_t *)mo.answers, (uint16_t *)out, (uint32_t)(answer_bytes / 2),
-                           mo.tile_keys);
+        hipLaunchKernelGGL(k_mg_unpermute<uint16_t>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
+                           (const uint16_t *)mo.answers, (uint16_t *)out, (uint32_t)(answer_bytes / 2));
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -627,7 +630,7 @@ hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t ns
         using S = decltype(src);
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe, cand,
-                               cap, key_order);
+                               cap, key_order, (uint32_t)options().multiget_xcd);
             return hipGetLastError();
         };
         if (lay.all_k7_m32) {

@@ -1305,13 +1305,14 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
         want_mask = reg.multiget(probes)
         want_list = reg.multiget_list(probes)
         want_odd = reg.multiget_list(probes, cap=5)  # odd rows: the unpermute moves u16 granules
-    with seb.option("multiget_order", 1):
-        got_mask = reg.multiget(probes)
-        got_list = reg.multiget_list(probes)
-        got_odd = reg.multiget_list(probes, cap=5)
-    assert np.array_equal(got_mask, want_mask)
-    assert np.array_equal(got_list, want_list)
-    assert np.array_equal(got_odd, want_odd) and np.array_equal(got_odd[:, :4], want_list)
+    for xcd in (0, 1):  # multiget_xcd: the XCD-contiguous block remap walks the same rows
+        with seb.option("multiget_order", 1), seb.option("multiget_xcd", xcd):
+            got_mask = reg.multiget(probes)
+            got_list = reg.multiget_list(probes)
+            got_odd = reg.multiget_list(probes, cap=5)
+        assert np.array_equal(got_mask, want_mask), xcd
+        assert np.array_equal(got_list, want_list), xcd
+        assert np.array_equal(got_odd, want_odd) and np.array_equal(got_odd[:, :4], want_list), xcd
     sample = list(range(0, n, 97)) + [0, 1, 2, 3]
     assert np.array_equal(got_list[sample], _walk_rows(files, [probes[i] for i in sample], got_list.shape[1]))
     fixed = np.frombuffer(b"".join(p for p in probes if len(p) == 16), np.uint8)
