@@ -95,8 +95,6 @@ int seb_abi_version(void);
  *   "scatter_bins"    radix-partitioned build, k == 7, 512-2275 buckets (m ~ 33.5M-149M bits):
  *                     positions placed through fixed per-bucket LDS bins, the claims pipelined
  *                     against the hashing (1, default), or by a counting sort (0)
- *   "scatter_tiles_exact" fixed-bin scatter: shrink the rounds so the key tiles fill every CU (1),
- *                     or fill the last rounds (0, default; 1 is unmeasured)
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
  *   "multiget_order"  registry MultiGet walks batches of >= 64K keys in key-range order (1, default)
  *                     or batch order (0)

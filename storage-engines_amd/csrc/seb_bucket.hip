@@ -527,7 +527,7 @@ static uint32_t scatter_kpt(uint32_t nb) {
     return ((uint64_t)kScatterThreads * 5 * 7 + 2 * nb + 17) * 4 <= 160u * 1024 ? 5u : 4u;
 }
 
-static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k, uint32_t bins, bool tiles_exact) {
+static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k, uint32_t bins) {
     BktPlan p{};
     const uint64_t nwords = (m + 31) / 32;
     p.nb = (uint32_t)((nwords + kBktWords - 1) / kBktWords);
@@ -545,10 +545,8 @@ static BktPlan plan_bucketed(uint64_t n, uint64_t m, uint32_t k, uint32_t bins, 
     uint64_t rounds_total = (n + round_keys - 1) / round_keys;
     uint64_t rounds_per_tile = (rounds_total + target - 1) / target;
     if (rounds_per_tile < 1) rounds_per_tile = 1;
-    if (bins && tiles_exact) {  // shrink the rounds so the tiles fill every CU
-        const uint64_t rk = (n + target * rounds_per_tile - 1) / (target * rounds_per_tile);
-        if (rk >= 64 && rk < round_keys) round_keys = (uint32_t)rk;
-    }
+    // (shrinking the rounds so C2's tiles are exactly 256 rather than 245 measured the same:
+    // scatter 137.4 vs 137.3 us, profiles/r05c_tiles_exact_ab.txt)
     p.round_keys = round_keys;
     p.tile_keys = (uint32_t)(rounds_per_tile * round_keys);
     p.ntiles = (uint32_t)((n + p.tile_keys - 1) / p.tile_keys);
@@ -580,14 +578,11 @@ uint64_t bucketed_workspace_bytes(uint64_t n, uint64_t m, uint32_t k) {
     if (!bucketed_supported(m, k) || n == 0) return 0;
     const uint64_t cap = bucketed_max_keys(k);
     const uint64_t nn = n < cap ? n : cap;
-    // any plan may run (scatter_bins / scatter_tiles_exact can change between the query and the build)
-    uint64_t a = plan_bucketed(nn, m, k, 0, false).bytes;
+    // either scatter may run (scatter_bins can change between the query and the build)
+    const uint64_t a = plan_bucketed(nn, m, k, 0).bytes;
     const uint32_t sl = bin_slots(m, k);
-    for (int te = 0; sl && te < 2; ++te) {
-        const uint64_t b = plan_bucketed(nn, m, k, sl, te != 0).bytes;
-        if (b > a) a = b;
-    }
-    return a;
+    const uint64_t b = sl ? plan_bucketed(nn, m, k, sl).bytes : 0;
+    return a > b ? a : b;
 }
 
 // One launch pair (scatter + apply) per chunk of at most bucketed_max_keys keys; `chunk(k0, n)`
@@ -600,7 +595,7 @@ static hipError_t run_bucketed(uint64_t n, const ModArg &md, uint32_t *words, vo
     for (uint64_t k0 = 0; k0 < n; k0 += maxk) {  // OR-accumulative: split large batches
         const bool fresh = ovf && k0 == 0;
         const uint64_t sn = n - k0 < maxk ? n - k0 : maxk;
-        const BktPlan p = plan_bucketed(sn, md.m, md.k, use_bins(md.m, md.k), options().scatter_tiles_exact != 0);
+        const BktPlan p = plan_bucketed(sn, md.m, md.k, use_bins(md.m, md.k));
         if (p.bytes > ws_bytes || p.ntiles > kMaxTiles) return hipErrorInvalidValue;
         if ((uint64_t)p.nb * p.ntiles * p.cap >= (1ull << 31)) return hipErrorInvalidValue;  // u32 region index
         uint8_t *w = (uint8_t *)ws;

@@ -160,11 +160,10 @@ static const OptionDesc kOptions[] = {
     SEB_OPT(probe_phases, 0, 64),
     SEB_OPT(probe_compact, 0, 1),
     SEB_OPT(scatter_bins, 0, 1),
-    SEB_OPT(scatter_tiles_exact, 0, 1),
     SEB_OPT(grid_cap, 1, 1 << 30),
     SEB_OPT(workspace_limit_mib, 0, 1 << 30),
     SEB_OPT(varlen_tail, 0, 1),
-    SEB_OPT(varlen_long, 0, 1),
+    SEB_OPT(varlen_long, 0, 2),
     SEB_OPT(cpu_fallback, 0, 1),
     SEB_OPT(fault_inject, 0, 2),
 };
@@ -543,7 +542,7 @@ static int probe_dispatch(KeyBatch kb, const uint32_t *words, const ModArg &md, 
         // varlen_long, the long keys' packed words in tag 1's scratch)
         void *rows, *lp = nullptr;
         if ((rc = cached_workspace(s, probe_compact_bytes(kb.n), &rows, 2))) return rc;
-        if (options().varlen_long && (rc = cached_workspace(s, kb.n * 8, &lp, 1))) return rc;
+        if (options().varlen_long > 1 && (rc = cached_workspace(s, kb.n * 8, &lp, 1))) return rc;
         HIP_OR_FAIL(launch_probe_compact_varlen(kb, words, md, out, rows, (uint64_t *)lp, s));
         return SEB_OK;
     }

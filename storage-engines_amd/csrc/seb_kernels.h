@@ -124,7 +124,6 @@ struct Options {
     int multiget_xcd = 1;         // MultiGet: the blocks sharing an XCD walk one contiguous eighth of the batch
                                   // (1, default: 575 vs 596 us per 10M-key k_multiget on 28 files), or not (0)
     int probe_compact = 1;        // phased probe from keys: later phases read only the live keys' words
-    int scatter_tiles_exact = 0;  // bin scatter: rounds shrunk so the tiles fill all 256 CUs (1) (being measured)
     int scatter_bins = 1;         // bucketed build, k == 7: scatter through fixed LDS bins, pipelined against the
                                   // hashing (1), or the counting sort (0)
     uint64_t varlen_prehash_min_keys = 1u << 16;  // LDS-staged pre-hash from this many var-length keys

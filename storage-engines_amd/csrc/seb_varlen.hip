@@ -337,23 +337,34 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
 // ahead, nothing read past the key's last dword).  Output: packed residues at each key's index.
 constexpr uint32_t kLongThreads = 512, kLongPer = 16, kLongTile = kLongThreads * kLongPer;
 
+// The key's dwords are loaded kLongBatch at a time, all issued before any is used (a dword loop that
+// consumes each load an iteration later waits a memory round trip per dword: 943 us per C4 batch).
+constexpr uint32_t kLongBatch = 8;
+
 __device__ __forceinline__ void fnv_global(const uint8_t *p, uint32_t len, uint64_t &h1, uint64_t &h2) {
     const uint32_t *w = (const uint32_t *)((uintptr_t)p & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
-    const uint32_t nd = (sh + len + 3) >> 2;  // dwords holding key bytes
-    auto ld = [&](uint32_t j) { return j < nd ? w[j] : 0u; };
-    uint32_t cur = ld(0), nxt = ld(1);
-    FnvSplit f;
+    const uint32_t nd = (sh + len + 3) >> 2;  // dwords holding key bytes (nothing past them is read)
     const uint32_t nw = len >> 2;
-    for (uint32_t j = 0; j < nw; ++j) {
-        const uint32_t ahead = ld(j + 2);
-        f.word(__builtin_amdgcn_alignbyte(nxt, cur, sh));
-        cur = nxt;
-        nxt = ahead;
+    FnvSplit f;
+    uint32_t cur = nd ? w[0] : 0u;
+    uint32_t j = 0;
+    for (; j < nw; j += kLongBatch) {  // words j .. j + kLongBatch - 1 need dwords j .. j + kLongBatch
+        uint32_t v[kLongBatch + 1];
+        v[0] = cur;
+#pragma unroll
+        for (uint32_t i = 1; i <= kLongBatch; ++i) v[i] = j + i < nd ? w[j + i] : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < kLongBatch; ++i)
+            if (j + i < nw) f.word(__builtin_amdgcn_alignbyte(v[i + 1], v[i], sh));
+        cur = v[kLongBatch];
     }
     f.get(h1, h2);
     const uint32_t r = len & 3u;
-    if (r) fnv_word_part(__builtin_amdgcn_alignbyte(nxt, cur, sh), 0u, r, h1, h2);
+    if (r) {  // dwords nw and nw + 1 (the latter only when the last bytes cross into it)
+        const uint32_t a = w[nw], b = nw + 1 < nd ? w[nw + 1] : 0u;
+        fnv_word_part(__builtin_amdgcn_alignbyte(b, a, sh), 0u, r, h1, h2);
+    }
 }
 
 __global__ __launch_bounds__(kLongThreads) void k_hash_long(const uint8_t *__restrict__ data,
@@ -435,7 +446,7 @@ static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const Mo
     if (!kb.offsets || kb.n == 0) return hipSuccess;
     const uint64_t ntiles = (kb.n + kVarKeys - 1) / kVarKeys;
     if constexpr (PACK) {
-        if (options().varlen_long && (!P0 || p0.long_packed)) {  // long keys first, then the rest
+        if (options().varlen_long && (!P0 || (options().varlen_long > 1 && p0.long_packed))) {  // long keys first
             hipError_t e = launch_hash_long(kb, md, P0 ? (uint64_t *)p0.long_packed : (uint64_t *)out, s);
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, 0, P0, kLongDw>), dim3((unsigned)ntiles),

@@ -474,7 +474,7 @@ def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
     assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
-@pytest.mark.parametrize("tail", [(0, 0), (1, 0), (1, 1)], ids=["no_tail", "tail", "long_pass"])
+@pytest.mark.parametrize("tail", [(0, 0), (1, 0), (1, 2)], ids=["no_tail", "tail", "long_pass"])
 @pytest.mark.parametrize("algo", [0, 2])
 def test_c4_prehash_golden(seb, golden, torch_cuda, algo, tail):
     """C4's zipf lengths (the spans fit the LDS window, so the sorted and split-chain hashing
@@ -527,7 +527,7 @@ def test_varlen_processing_order_invisible(seb, torch_cuda, prehash_min, build_a
         assert np.array_equal(out.cpu().numpy(), oc.probe(ref, m, k, pd, n, offsets=off))
 
 
-@pytest.mark.parametrize("tail", [(0, 0), (1, 0), (1, 1)], ids=["no_tail", "tail", "long_pass"])
+@pytest.mark.parametrize("tail", [(0, 0), (1, 0), (1, 2)], ids=["no_tail", "tail", "long_pass"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed, tail):
     """The pre-hash (448-key workgroups, 64-B window per key, with and without the split-chain tail
@@ -571,7 +571,7 @@ def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed, tail):
         assert np.array_equal(out.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("long_pass", [0, 1])
+@pytest.mark.parametrize("long_pass", [0, 2])
 @pytest.mark.parametrize("k", [7, 8])
 @pytest.mark.parametrize("algo", [1, 2])
 def test_varlen_prehash_packed_paths(seb, torch_cuda, k, algo, probe_compact, long_pass):
@@ -638,7 +638,7 @@ def test_varlen_bucketed_build_chunks(seb, torch_cuda, k):
         assert np.array_equal(bits, ref)
 
 
-@pytest.mark.parametrize("long_pass", [0, 1])
+@pytest.mark.parametrize("long_pass", [0, 2])
 def test_c4_varlen_10m_properties(seb, golden, torch_cuda, long_pass):
     """Full C4 size: the filter and the 10M answers match the golden digests (tests/golden varlen
     n = 10M, the oracle's), and every built key answers true; with and without the long-key pass."""
@@ -1673,7 +1673,7 @@ def test_bucketed_build_overflow_and_lds_limits(seb, torch_cuda, case):
         seb.set_option("build_algo", 0)
 
 
-@pytest.mark.parametrize("bins", [(1, 0), (1, 1), (0, 0)], ids=["bins", "bins_tiles_exact", "counting"])
+@pytest.mark.parametrize("bins", [1, 0], ids=["bins", "counting"])
 @pytest.mark.parametrize("case", ["nb513", "c2m", "nb2274", "duplicates", "skewed"])
 def test_bucketed_scatter_bins(seb, torch_cuda, case, bins):
     """The radix-partitioned build's two scatters (scatter_bins 1: fixed LDS bins, runs padded to
@@ -1698,8 +1698,7 @@ def test_bucketed_scatter_bins(seb, torch_cuda, case, bins):
     uniq = np.unique(keys, axis=0)
     ref = oc.build(m, k, np.ascontiguousarray(uniq).ravel(), len(uniq), stride=16)
     kd = seb.dev_keys(to_dev(torch, keys), n=n, stride=16)
-    bins, exact = bins
-    with seb.option("build_algo", 2), seb.option("scatter_bins", bins), seb.option("scatter_tiles_exact", exact):
+    with seb.option("build_algo", 2), seb.option("scatter_bins", bins):
         words = seb.new_words(m)
         for rep in range(2):
             words.view(torch.uint8).fill_(0xC3 if rep == 0 else 0xFF)
@@ -1716,7 +1715,7 @@ def test_bucketed_scatter_bins(seb, torch_cuda, case, bins):
         assert np.array_equal(seb.words_to_bits(w2, m), ref), (case, bins)
 
 
-@pytest.mark.parametrize("bins", [(1, 0), (1, 1), (0, 0)], ids=["bins", "bins_tiles_exact", "counting"])
+@pytest.mark.parametrize("bins", [1, 0], ids=["bins", "counting"])
 @pytest.mark.parametrize("src", ["stride20", "stride13", "varlen_direct", "varlen_prehash"])
 def test_bucketed_scatter_key_sources(seb, torch_cuda, src, bins):
     """Both scatters over every key source the radix-partitioned build reads at a filter size the
@@ -1738,8 +1737,7 @@ def test_bucketed_scatter_key_sources(seb, torch_cuda, src, bins):
         ref = oc.build(m, k, data, n, offsets=off)
         kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off.astype(np.int64)))
     prehash = 0 if src == "varlen_prehash" else 1 << 40
-    bins, exact = bins
-    with seb.option("build_algo", 2), seb.option("scatter_bins", bins), seb.option("scatter_tiles_exact", exact), \
+    with seb.option("build_algo", 2), seb.option("scatter_bins", bins), \
             seb.option("varlen_prehash_min_keys", prehash):
         words = seb.new_words(m)
         words.view(torch.uint8).fill_(0x3C)
