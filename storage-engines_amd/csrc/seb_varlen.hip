@@ -341,28 +341,33 @@ constexpr uint32_t kLongThreads = 512, kLongPer = 16, kLongTile = kLongThreads *
 // consumes each load an iteration later waits a memory round trip per dword: 943 us per C4 batch).
 constexpr uint32_t kLongBatch = 8;
 
-__device__ __forceinline__ void fnv_global(const uint8_t *p, uint32_t len, uint64_t &h1, uint64_t &h2) {
-    const uint32_t *w = (const uint32_t *)((uintptr_t)p & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
-    const uint32_t nd = (sh + len + 3) >> 2;  // dwords holding key bytes (nothing past them is read)
+// A key of len >= 1 bytes at data + ks (the long pass's keys have len > 4 * long_dw): its dwords are
+// read with plain global loads at clamped indices (every load stays inside the key's dwords, no
+// branch around it), kLongBatch issued before any is used.
+__device__ __forceinline__ void fnv_global(const uint8_t *__restrict__ data, uint64_t ks, uint32_t len,
+                                           uint64_t &h1, uint64_t &h2) {
+    const uint32_t sh = (uint32_t)(((uintptr_t)data + ks) & 3u);
+    const uint32_t *w = (const uint32_t *)(data + (ks - sh));  // keeps the kernel argument's address space
+    const uint32_t last = (sh + len - 1) >> 2;                 // the last dword holding key bytes
     const uint32_t nw = len >> 2;
     FnvSplit f;
-    uint32_t cur = nd ? w[0] : 0u;
-    uint32_t j = 0;
-    for (; j < nw; j += kLongBatch) {  // words j .. j + kLongBatch - 1 need dwords j .. j + kLongBatch
+    uint32_t cur = w[0];
+    for (uint32_t j = 0; j < nw; j += kLongBatch) {  // words j .. j + kLongBatch - 1 need dwords j .. j + kLongBatch
         uint32_t v[kLongBatch + 1];
         v[0] = cur;
 #pragma unroll
-        for (uint32_t i = 1; i <= kLongBatch; ++i) v[i] = j + i < nd ? w[j + i] : 0u;
+        for (uint32_t i = 1; i <= kLongBatch; ++i) v[i] = w[min(j + i, last)];
 #pragma unroll
-        for (uint32_t i = 0; i < kLongBatch; ++i)
-            if (j + i < nw) f.word(__builtin_amdgcn_alignbyte(v[i + 1], v[i], sh));
+        for (uint32_t i = 0; i < kLongBatch; ++i) {
+            const uint32_t hi = j + i + 1 <= last ? v[i + 1] : 0u;
+            if (j + i < nw) f.word(__builtin_amdgcn_alignbyte(hi, v[i], sh));
+        }
         cur = v[kLongBatch];
     }
     f.get(h1, h2);
     const uint32_t r = len & 3u;
     if (r) {  // dwords nw and nw + 1 (the latter only when the last bytes cross into it)
-        const uint32_t a = w[nw], b = nw + 1 < nd ? w[nw + 1] : 0u;
+        const uint32_t a = w[nw], b = nw + 1 <= last ? w[nw + 1] : 0u;
         fnv_word_part(__builtin_amdgcn_alignbyte(b, a, sh), 0u, r, h1, h2);
     }
 }
@@ -379,18 +384,19 @@ __global__ __launch_bounds__(kLongThreads) void k_hash_long(const uint8_t *__res
     if (t <= nc) cls_n[t] = 0u;
     __syncthreads();
     uint32_t cls[kLongPer];
+    uint64_t lo[kLongPer], hi[kLongPer];
+#pragma unroll
+    for (uint32_t r = 0; r < kLongPer; ++r) {  // every offset load issued before any is used
+        const uint64_t i = min(k0 + r * kLongThreads + t, k1 - 1);
+        lo[r] = off[i];
+        hi[r] = off[i + 1];
+    }
 #pragma unroll
     for (uint32_t r = 0; r < kLongPer; ++r) {
-        const uint64_t i = k0 + r * kLongThreads + t;
-        cls[r] = 0xffu;
-        if (i < k1) {
-            const uint64_t len = off[i + 1] - off[i];
-            const uint64_t dw = (len + 3) >> 2;
-            if (dw > long_dw) {
-                cls[r] = (uint32_t)((dw > 64 ? 65 : dw) - long_dw - 1);
-                atomicAdd(&cls_n[cls[r]], 1u);
-            }
-        }
+        const uint64_t dw = (hi[r] - lo[r] + 3) >> 2;
+        const bool in = k0 + r * kLongThreads + t < k1 && dw > long_dw;
+        cls[r] = in ? (uint32_t)((dw > 64 ? 65 : dw) - long_dw - 1) : 0xffu;
+        if (in) atomicAdd(&cls_n[cls[r]], 1u);
     }
     __syncthreads();
     if (t < 64) {  // exclusive scan of the nc <= 65 class counts by one wave (two entries per lane)
@@ -418,7 +424,7 @@ __global__ __launch_bounds__(kLongThreads) void k_hash_long(const uint8_t *__res
             const uint64_t i = k0 + list[q];
             const uint64_t ks = off[i];
             uint64_t h1, h2;
-            fnv_global(data + ks, (uint32_t)(off[i + 1] - ks), h1, h2);
+            fnv_global(data, ks, (uint32_t)(off[i + 1] - ks), h1, h2);
             packed[i] = pack_residue(h1, h2, md);
         }
     }
