@@ -59,7 +59,7 @@ GOLDEN_MANY = "18f390ebd4082f2282f8f6352c2e02f946e855b57078fcd4f21e81956050baa7"
 GOLDEN_WAL = "7d661e321c2804cebf541abd9c1a34463b70fe27fce3c5459a71408ac91b3e01"  # sha256(u32 CRCs), 2M records
 OPTIONS = ("build_algo", "multi_interleave", "multiget_order", "multiget_l0_group", "multiget_xcd", "varlen_prehash_min_keys", "bucket_min_keys",
            "lds_min_keys", "many_splits", "probe_phases", "probe_compact", "grid_cap", "workspace_limit_mib",
-           "varlen_tail", "varlen_long", "scatter_bins", "cpu_fallback")
+           "varlen_tail", "scatter_bins", "cpu_fallback")
 
 
 def option_value(seb, name):

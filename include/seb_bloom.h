@@ -104,8 +104,6 @@ int seb_abi_version(void);
  *                     the (key-range ordered) batch, so each XCD's L2 holds its own stretch's filters
  *                     (1, default), or blocks walk the batch in launch order (0)
  *   "varlen_prehash_min_keys"  variable-length batches of this many keys are pre-hashed in LDS
- *   "varlen_long"     packed pre-hash (k == 7 filters): keys over 48 B are hashed first by a pass that
- *                     groups them by length across 8192 keys (1), or all in the LDS pre-hash (0)
  *   "varlen_tail"     pre-hash: the 64 longest keys of a workgroup run on two waves, one per FNV
  *                     chain (1, default), or one key per lane like the others (0)
  *   "grid_cap"        maximum workgroups of the grid-stride kernels

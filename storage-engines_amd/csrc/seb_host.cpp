@@ -163,7 +163,6 @@ static const OptionDesc kOptions[] = {
     SEB_OPT(grid_cap, 1, 1 << 30),
     SEB_OPT(workspace_limit_mib, 0, 1 << 30),
     SEB_OPT(varlen_tail, 0, 1),
-    SEB_OPT(varlen_long, 0, 2),
     SEB_OPT(cpu_fallback, 0, 1),
     SEB_OPT(fault_inject, 0, 2),
 };
@@ -538,12 +537,10 @@ static int probe_dispatch(KeyBatch kb, const uint32_t *words, const ModArg &md, 
     void *ws;
     int rc;
     if (want_phased(kb.n, md, out) && want_prehash_packed(kb, md) && options().probe_compact) {
-        // the pre-hash with phase 0 fused in: compacted rows (tag 2) only, no dense packed batch (with
-        // varlen_long, the long keys' packed words in tag 1's scratch)
-        void *rows, *lp = nullptr;
+        // the pre-hash with phase 0 fused in: compacted rows (tag 2) only, no dense packed batch
+        void *rows;
         if ((rc = cached_workspace(s, probe_compact_bytes(kb.n), &rows, 2))) return rc;
-        if (options().varlen_long > 1 && (rc = cached_workspace(s, kb.n * 8, &lp, 1))) return rc;
-        HIP_OR_FAIL(launch_probe_compact_varlen(kb, words, md, out, rows, (uint64_t *)lp, s));
+        HIP_OR_FAIL(launch_probe_compact_varlen(kb, words, md, out, rows, s));
         return SEB_OK;
     }
     if (want_phased(kb.n, md, out) && want_prehash_packed(kb, md)) {  // pre-hash to packed, all phases from it

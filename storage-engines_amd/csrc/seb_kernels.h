@@ -133,8 +133,6 @@ struct Options {
     int probe_phases = 0;         // phased probe: number of filter ranges (0 = one per 4 MiB of filter)
     unsigned grid_cap = 1u << 20; // grid-stride kernels: most workgroups per launch
     uint64_t workspace_limit_mib = 0;  // library scratch cap (0 = none); a larger request fails SEB_ERR_NOMEM
-    int varlen_long = 0;          // packed pre-hash: keys over 48 B hashed first by the long-key pass, grouped by
-                                  // length across the workgroup's 8192 keys (1), or in the LDS pre-hash (0)
     int varlen_tail = 1;          // pre-hash: the 64 longest keys of a workgroup on two chain waves (1), or
                                   // one key per lane throughout (0, measured slower: DESIGN.md 5.5)
     int cpu_fallback = 1;         // Go API mirror: a build/probe whose device path fails (SEB_ERR_DEVICE/NOMEM)
@@ -204,10 +202,9 @@ hipError_t launch_probe_compact(const KeyBatch &kb, const uint32_t *words, const
                                 hipStream_t s);
 // The same from a variable-length batch, phase 0 fused into the LDS-staged pre-hash.
 hipError_t launch_probe_compact_varlen(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out,
-                                       void *ws, uint64_t *long_packed, hipStream_t s);
-// long_packed (n * 8 B of scratch, varlen_long on): the long-key pass's packed words.
+                                       void *ws, hipStream_t s);
 hipError_t launch_hash_varlen_phase0(const KeyBatch &kb, const ModArg &md, const uint32_t *words, uint64_t *rows,
-                                     ulonglong2 *recs, uint32_t hi, uint64_t *long_packed, hipStream_t s);
+                                     ulonglong2 *recs, uint32_t hi, hipStream_t s);
 // The same from a batch of packed residues (the pre-hashed variable-length batch, a broadcast batch).
 hipError_t launch_probe_compact_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,
                                        uint8_t *out, void *ws, hipStream_t s);

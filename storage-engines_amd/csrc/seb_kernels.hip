@@ -1141,9 +1141,9 @@ hipError_t launch_probe_compact_packed(const uint64_t *packed, uint64_t n, const
 }
 
 hipError_t launch_probe_compact_varlen(const KeyBatch &kb, const uint32_t *words, const ModArg &md, uint8_t *out,
-                                       void *ws, uint64_t *long_packed, hipStream_t s) {
+                                       void *ws, hipStream_t s) {
     return run_probe_compact(kb.n, words, md, out, ws, s, [&](auto &&, uint64_t *rows, ulonglong2 *recs, uint32_t hi) {
-        return launch_hash_varlen_phase0(kb, md, words, rows, recs, hi, long_packed, s);
+        return launch_hash_varlen_phase0(kb, md, words, rows, recs, hi, s);
     });
 }
 

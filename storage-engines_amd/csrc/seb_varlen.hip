@@ -152,21 +152,16 @@ struct Phase0Arg {
     uint64_t *rows;
     ulonglong2 *recs;
     uint32_t hi;
-    const uint64_t *long_packed;  // LONG: the long keys' packed words (k_hash_long), at their key index
 };
 
 // Every thread of the workgroup arrives here (has: it hashed key k0 + my_j); the packed words go to
 // xpk (the staging window), then waves 0 .. KEYS/64 - 1 each take the group of keys
 // k0 + 64 * wave + lane (k0 is a multiple of 64).
-// long_pw (the long-key pass ran, varlen_long_dw): key k0 + threadIdx.x is a long key whose word the
-// pass left in long_packed.
 template <uint32_t KEYS>
 __device__ __forceinline__ void varlen_phase0(uint64_t *xpk, bool has, uint32_t my_j, uint64_t my_pw, uint64_t k0,
-                                              uint32_t cnt, const ModArg &md, const Phase0Arg &p0,
-                                              bool long_pw = false) {
+                                              uint32_t cnt, const ModArg &md, const Phase0Arg &p0) {
     __syncthreads();  // every key is hashed: the staging window is free
     if (has) xpk[my_j] = my_pw;
-    if (long_pw) xpk[threadIdx.x] = p0.long_packed[k0 + threadIdx.x];
     __syncthreads();  // every key's packed word is in xpk, in key order
     const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     if (wid >= KEYS / 64 || 64 * wid >= cnt) return;  // wave-uniform; no barrier follows
@@ -187,14 +182,10 @@ __device__ __forceinline__ void varlen_phase0(uint64_t *xpk, bool has, uint32_t 
     if (lane == 0) p0.recs[g] = make_ulonglong2(alive, alive);
 }
 
-// LONG > 0 (with PACK): keys of more than LONG dwords were hashed by k_hash_long, which wrote their
-// packed words; this workgroup sorts and hashes only the others (at most LONG dwords, so no chain
-// waves), and with P0 reads the long keys' words back for phase 0.
-template <uint32_t KEYS, uint32_t WIN, bool PACK, uint32_t NS = 0, bool P0 = false, uint32_t LONG = 0>
+template <uint32_t KEYS, uint32_t WIN, bool PACK, uint32_t NS = 0, bool P0 = false>
 __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *__restrict__ data,
                                                       const uint64_t *__restrict__ off, uint64_t n,
                                                       void *__restrict__ hashes, ModArg md, Phase0Arg p0) {
-    static_assert(LONG == 0 || (PACK && NS == 0 && LONG < 64), "the long-key pass writes packed words");
     constexpr uint32_t kHashLds = KEYS * WIN;
     static_assert(kHashLds % 16 == 0 && kHashLds + 16 < 65536, "window offsets are 16-bit");
     static_assert(!P0 || (PACK && KEYS % 64 == 0 && KEYS * 8 <= kHashLds), "phase 0: whole groups of 64 keys, words in the window");
@@ -208,10 +199,7 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
     const uint64_t k0 = (uint64_t)blockIdx.x * KEYS;
     const uint64_t k1 = k0 + KEYS < n ? k0 + KEYS : n;
     const uint32_t cnt = (uint32_t)(k1 - k0);
-    const bool inb = t < cnt;
-    const uint64_t ks = inb ? off[k0 + t] : 0, ke = inb ? off[k0 + t + 1] : 0;
-    const bool is_long = LONG > 0 && inb && ke - ks > 4ull * LONG;
-    const bool mine = inb && !is_long;  // the keys this workgroup hashes
+    const bool mine = t < cnt;
     // P0: a thread keeps its key's packed word until every key is hashed, then the words go to the
     // (by then unused) staging window in key order: no LDS of its own, so 5 workgroups still fit a CU
     uint32_t my_j = 0;
@@ -226,6 +214,7 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
             put_hash<PACK>(hashes, k0 + j, h1, h2, md);
         }
     };
+    const uint64_t ks = mine ? off[k0 + t] : 0, ke = mine ? off[k0 + t + 1] : 0;
     const uintptr_t s0 = (uintptr_t)(data + off[k0]);
     const uintptr_t s1 = (uintptr_t)(data + off[k1]);
     const uintptr_t base = s0 & ~(uintptr_t)15;
@@ -237,11 +226,9 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
             emit(t, h1, h2);
         }
         if constexpr (P0)
-            varlen_phase0<KEYS>((uint64_t *)stage, has, my_j, my_pw, k0, cnt, md, p0, is_long);
+            varlen_phase0<KEYS>((uint64_t *)stage, has, my_j, my_pw, k0, cnt, md, p0);
         return;
     }
-    __shared__ uint32_t nmine;
-    if (LONG > 0 && t == 0) nmine = 0u;
     if (t < kLenBuckets) cur[t] = 0u;
     if (t < NS) xflag[t] = 0u;
     for (uint32_t c = t; c < (uint32_t)chunks; c += blockDim.x) stage[c] = ((const uint4 *)base)[c];
@@ -256,10 +243,8 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
     const uint64_t peers = same == live ? live : 1ull << (t & 63);
     const uint32_t below = lanes_below(peers);
     const bool leader = mine && below == 0;
-    const uint32_t wave_mine = LONG > 0 ? (uint32_t)__popcll(__ballot(mine)) : 0u;
     __syncthreads();
     if (leader) atomicAdd(&cur[bk], (uint32_t)__popcll(peers));
-    if (LONG > 0 && (t & 63) == 0 && wave_mine) atomicAdd(&nmine, wave_mine);
     __syncthreads();
     if (t < 64) {  // exclusive scan of the 65 bucket counts by one wave
         uint32_t c = cur[t] + (t == 63 ? cur[64] : 0u);
@@ -314,8 +299,7 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
             if constexpr (!P0) return;
         }
     }
-    const uint32_t nhash = LONG > 0 ? nmine : cnt;
-    if (t < nhash && !tail) {  // nhash lanes hash the nhash sorted slots
+    if (mine && !tail) {  // cnt lanes hash the cnt sorted slots
         const uint32_t sk = slot_key[t];
         Funnel f;
         f.init(lds, sk >> 16, sk & 0xffffu);
@@ -324,110 +308,7 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
         f.finish(lds, h1, h2);
         emit(slot_idx[t], h1, h2);
     }
-    if constexpr (P0) varlen_phase0<KEYS>((uint64_t *)stage, has, my_j, my_pw, k0, cnt, md, p0, is_long);
-}
-
-// ---- the long-key pass (varlen_long_dw = L > 0): every key of more than L dwords is hashed here,
-// so the LDS pre-hash's waves only see keys of at most L dwords.  Inside one workgroup a wave pays
-// its longest key (57% of C4's pre-hash VALU was the two chain waves of each
-// workgroup's 64 longest keys); here a workgroup takes kLongTile keys, lists its long ones by dword
-// length in LDS (a counting sort over the classes L+1 .. 64, longer keys in one more class), and each
-// wave hashes 64 consecutive list entries, whose lengths are about equal whatever their positions,
-// straight from HBM: each lane walks its key's aligned dwords (v_alignbyte funnel, one dword read
-// ahead, nothing read past the key's last dword).  Output: packed residues at each key's index.
-constexpr uint32_t kLongThreads = 512, kLongPer = 16, kLongTile = kLongThreads * kLongPer;
-
-// The key's dwords are loaded kLongBatch at a time, all issued before any is used (a dword loop that
-// consumes each load an iteration later waits a memory round trip per dword: 943 us per C4 batch).
-constexpr uint32_t kLongBatch = 8;
-
-// A key of len >= 1 bytes at data + ks (the long pass's keys have len > 4 * long_dw): its dwords are
-// read with plain global loads at clamped indices (every load stays inside the key's dwords, no
-// branch around it), kLongBatch issued before any is used.
-__device__ __forceinline__ void fnv_global(const uint8_t *__restrict__ data, uint64_t ks, uint32_t len,
-                                           uint64_t &h1, uint64_t &h2) {
-    const uint32_t sh = (uint32_t)(((uintptr_t)data + ks) & 3u);
-    const uint32_t *w = (const uint32_t *)(data + (ks - sh));  // keeps the kernel argument's address space
-    const uint32_t last = (sh + len - 1) >> 2;                 // the last dword holding key bytes
-    const uint32_t nw = len >> 2;
-    FnvSplit f;
-    uint32_t cur = w[0];
-    for (uint32_t j = 0; j < nw; j += kLongBatch) {  // words j .. j + kLongBatch - 1 need dwords j .. j + kLongBatch
-        uint32_t v[kLongBatch + 1];
-        v[0] = cur;
-#pragma unroll
-        for (uint32_t i = 1; i <= kLongBatch; ++i) v[i] = w[min(j + i, last)];
-#pragma unroll
-        for (uint32_t i = 0; i < kLongBatch; ++i) {
-            const uint32_t hi = j + i + 1 <= last ? v[i + 1] : 0u;
-            if (j + i < nw) f.word(__builtin_amdgcn_alignbyte(hi, v[i], sh));
-        }
-        cur = v[kLongBatch];
-    }
-    f.get(h1, h2);
-    const uint32_t r = len & 3u;
-    if (r) {  // dwords nw and nw + 1 (the latter only when the last bytes cross into it)
-        const uint32_t a = w[nw], b = nw + 1 <= last ? w[nw + 1] : 0u;
-        fnv_word_part(__builtin_amdgcn_alignbyte(b, a, sh), 0u, r, h1, h2);
-    }
-}
-
-__global__ __launch_bounds__(kLongThreads) void k_hash_long(const uint8_t *__restrict__ data,
-                                                           const uint64_t *__restrict__ off, uint64_t n, ModArg md,
-                                                           uint64_t *__restrict__ packed, uint32_t long_dw) {
-    __shared__ uint32_t cls_n[66];
-    __shared__ uint16_t list[kLongTile];
-    __shared__ uint32_t total;
-    const uint32_t t = threadIdx.x, nc = 65 - long_dw;  // classes: dw = long_dw + 1 .. 64, then > 64
-    const uint64_t k0 = (uint64_t)blockIdx.x * kLongTile;
-    const uint64_t k1 = k0 + kLongTile < n ? k0 + kLongTile : n;
-    if (t <= nc) cls_n[t] = 0u;
-    __syncthreads();
-    uint32_t cls[kLongPer];
-    uint64_t lo[kLongPer], hi[kLongPer];
-#pragma unroll
-    for (uint32_t r = 0; r < kLongPer; ++r) {  // every offset load issued before any is used
-        const uint64_t i = min(k0 + r * kLongThreads + t, k1 - 1);
-        lo[r] = off[i];
-        hi[r] = off[i + 1];
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < kLongPer; ++r) {
-        const uint64_t dw = (hi[r] - lo[r] + 3) >> 2;
-        const bool in = k0 + r * kLongThreads + t < k1 && dw > long_dw;
-        cls[r] = in ? (uint32_t)((dw > 64 ? 65 : dw) - long_dw - 1) : 0xffu;
-        if (in) atomicAdd(&cls_n[cls[r]], 1u);
-    }
-    __syncthreads();
-    if (t < 64) {  // exclusive scan of the nc <= 65 class counts by one wave (two entries per lane)
-        const uint32_t a = 2 * t < nc ? cls_n[2 * t] : 0u, b = 2 * t + 1 < nc ? cls_n[2 * t + 1] : 0u;
-        uint32_t v = a + b;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(v, d, 64);
-            if (t >= (uint32_t)d) v += y;
-        }
-        const uint32_t ex = v - a - b;
-        if (2 * t < nc) cls_n[2 * t] = ex;
-        if (2 * t + 1 < nc) cls_n[2 * t + 1] = ex + a;
-        if (t == 63) total = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t r = 0; r < kLongPer; ++r)
-        if (cls[r] != 0xffu) list[atomicAdd(&cls_n[cls[r]], 1u)] = (uint16_t)(r * kLongThreads + t);
-    __syncthreads();
-    const uint32_t L = total, wave = t >> 6, lane = t & 63;
-    for (uint32_t g = wave; 64 * g < L; g += kLongThreads / 64) {
-        const uint32_t q = 64 * g + lane;
-        if (q < L) {
-            const uint64_t i = k0 + list[q];
-            const uint64_t ks = off[i];
-            uint64_t h1, h2;
-            fnv_global(data, ks, (uint32_t)(off[i + 1] - ks), h1, h2);
-            packed[i] = pack_residue(h1, h2, md);
-        }
-    }
+    if constexpr (P0) varlen_phase0<KEYS>((uint64_t *)stage, has, my_j, my_pw, k0, cnt, md, p0);
 }
 
 // 448 keys per workgroup, a 64-B window per key, the top 64 split over two chain waves
@@ -436,30 +317,11 @@ __global__ __launch_bounds__(kLongThreads) void k_hash_long(const uint8_t *__res
 // ways of giving the chain waves' lanes more keys measured slower.
 constexpr uint32_t kVarKeys = 448, kVarWin = 64;
 
-// The long-key pass's threshold: keys of more than this many dwords (0: no pass).
-constexpr uint32_t kLongDw = 12;
-
-static hipError_t launch_hash_long(const KeyBatch &kb, const ModArg &md, uint64_t *packed, hipStream_t s) {
-    const uint64_t tiles = (kb.n + kLongTile - 1) / kLongTile;
-    hipLaunchKernelGGL(k_hash_long, dim3((unsigned)tiles), dim3(kLongThreads), 0, s, kb.data, kb.offsets, kb.n, md,
-                       packed, kLongDw);
-    return hipGetLastError();
-}
-
 template <bool PACK, bool P0 = false>
 static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const ModArg &md, hipStream_t s,
                                         Phase0Arg p0 = {}) {
     if (!kb.offsets || kb.n == 0) return hipSuccess;
     const uint64_t ntiles = (kb.n + kVarKeys - 1) / kVarKeys;
-    if constexpr (PACK) {
-        if (options().varlen_long && (!P0 || (options().varlen_long > 1 && p0.long_packed))) {  // long keys first
-            hipError_t e = launch_hash_long(kb, md, P0 ? (uint64_t *)p0.long_packed : (uint64_t *)out, s);
-            if (e != hipSuccess) return e;
-            hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, 0, P0, kLongDw>), dim3((unsigned)ntiles),
-                               dim3(kVarKeys), 0, s, kb.data, kb.offsets, kb.n, out, md, p0);
-            return hipGetLastError();
-        }
-    }
     if (options().varlen_tail == 0)
         hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, 0, P0>), dim3((unsigned)ntiles), dim3(kVarKeys), 0,
                            s, kb.data, kb.offsets, kb.n, out, md, p0);
@@ -470,9 +332,9 @@ static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const Mo
 }
 
 hipError_t launch_hash_varlen_phase0(const KeyBatch &kb, const ModArg &md, const uint32_t *words, uint64_t *rows,
-                                     ulonglong2 *recs, uint32_t hi, uint64_t *long_packed, hipStream_t s) {
+                                     ulonglong2 *recs, uint32_t hi, hipStream_t s) {
     if (md.k != 7 || md.m >= (1ull << kPackBits)) return hipErrorInvalidValue;
-    return launch_hash_varlen_any<true, true>(kb, nullptr, md, s, Phase0Arg{words, rows, recs, hi, long_packed});
+    return launch_hash_varlen_any<true, true>(kb, nullptr, md, s, Phase0Arg{words, rows, recs, hi});
 }
 
 hipError_t launch_hash_varlen(const KeyBatch &kb, uint4 *hashes, hipStream_t s) {

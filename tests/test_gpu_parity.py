@@ -474,23 +474,20 @@ def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
     assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
-@pytest.mark.parametrize("tail", [(0, 0), (1, 0), (1, 2)], ids=["no_tail", "tail", "long_pass"])
+@pytest.mark.parametrize("tail", [0, 1])
 @pytest.mark.parametrize("algo", [0, 2])
 def test_c4_prehash_golden(seb, golden, torch_cuda, algo, tail):
     """C4's zipf lengths (the spans fit the LDS window, so the sorted and split-chain hashing
     paths run rather than the overflow fallback), pre-hashed to 16-B hashes (LDS-resident build,
     unphased probe) and to packed residues (bucketed build), reproduce the C4 golden digests;
-    with the 64 longest keys of a workgroup on two chain waves (varlen_tail 1) and without (0), and
-    with the keys over 48 B hashed first by the long-key pass (varlen_long 1, packed paths)."""
+    with the 64 longest keys of a workgroup on two chain waves (varlen_tail 1) and without (0)."""
     torch = torch_cuda
     n = 100000
     row = next(r for r in golden["varlen"] if r["n"] == n)
     m, k = row["m"], row["k"]
     data, off = kg.varlen_keys(np.arange(n))
     pdata, poff = kg.varlen_keys(kg.probe_indices(n))
-    tail, long_pass = tail
-    with seb.option("varlen_prehash_min_keys", 0), seb.option("build_algo", algo), seb.option("varlen_tail", tail), \
-            seb.option("varlen_long", long_pass):
+    with seb.option("varlen_prehash_min_keys", 0), seb.option("build_algo", algo), seb.option("varlen_tail", tail):
         kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
         words, bits = dev_build_bits(seb, torch, kd, m, k)
         assert sha(bn.encode(bits, m, k)) == row["encode_sha256"]
@@ -527,16 +524,15 @@ def test_varlen_processing_order_invisible(seb, torch_cuda, prehash_min, build_a
         assert np.array_equal(out.cpu().numpy(), oc.probe(ref, m, k, pd, n, offsets=off))
 
 
-@pytest.mark.parametrize("tail", [(0, 0), (1, 0), (1, 2)], ids=["no_tail", "tail", "long_pass"])
+@pytest.mark.parametrize("packed", [0, 1], ids=["small_filter", "packed_paths"])
+@pytest.mark.parametrize("tail", [0, 1])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed, tail):
+def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed, tail, packed):
     """The pre-hash (448-key workgroups, 64-B window per key, with and without the split-chain tail
-    waves, and with the long-key pass: keys over 48 B hashed first, by length class, straight from
-    HBM) hashes like the oracle over lengths that mix empty, sub-word, bucket-edge, threshold-edge
-    (48/49 B) and window-overflowing keys, and a ragged last workgroup; the answers of a
-    half-present batch equal the oracle's key by key.  The long-pass case uses a two-range filter
-    and the bucketed build, so its packed paths (build, fused phase 0) run."""
-    tail, long_pass = tail
+    waves) hashes like the oracle over lengths that mix empty, sub-word, bucket-edge, 48/49-B and
+    window-overflowing keys, and a ragged last workgroup; the answers of a half-present batch
+    equal the oracle's key by key; with a two-range filter and the bucketed build as well, so the
+    packed paths (build from packed residues, phase 0 fused into the pre-hash) run."""
     torch = torch_cuda
     rng = np.random.default_rng(seed)
     n = 40000 + 77
@@ -546,13 +542,13 @@ def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed, tail):
     off = np.zeros(n + 1, np.uint64)
     np.cumsum(lens, out=off[1:])
     data = rng.integers(0, 256, int(off[-1]) + 1, dtype=np.uint8)[1:]  # odd base offset in the host copy
-    m, k = (40_000_003, 7) if long_pass else oc.params(n, 0.01)
+    m, k = (40_000_003, 7) if packed else oc.params(n, 0.01)
     ref = oc.build(m, k, data, n, offsets=off)
     pd = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
     pd[: int(off[n // 2])] = data[: int(off[n // 2])]  # first half present
     want = oc.probe(ref, m, k, pd, n, offsets=off)
     with seb.option("varlen_prehash_min_keys", 0), seb.option("varlen_tail", tail), \
-            seb.option("varlen_long", long_pass), seb.option("build_algo", 2 if long_pass else 0):
+            seb.option("build_algo", 2 if packed else 0):
         pkd = seb.dev_keys(to_dev(torch, pd), to_dev(torch, off))
         dd = torch.zeros(int(off[-1]) + 64, dtype=torch.uint8, device="cuda")
         offd = to_dev(torch, off)
@@ -571,10 +567,9 @@ def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed, tail):
         assert np.array_equal(out.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("long_pass", [0, 2])
 @pytest.mark.parametrize("k", [7, 8])
 @pytest.mark.parametrize("algo", [1, 2])
-def test_varlen_prehash_packed_paths(seb, torch_cuda, k, algo, probe_compact, long_pass):
+def test_varlen_prehash_packed_paths(seb, torch_cuda, k, algo, probe_compact):
     """Pre-hash to packed residues (k = 7: bucketed build from KeysPacked; the phased probe with
     phase 0 fused into the pre-hash (compacted) or from the dense packed words; pack_residues /
     emit_packed over variable-length keys) against the oracle, and the 16-B hash path (k = 8); a
@@ -594,7 +589,7 @@ def test_varlen_prehash_packed_paths(seb, torch_cuda, k, algo, probe_compact, lo
     pd = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
     pd[: int(off[n // 2])] = data[: int(off[n // 2])]  # first half present
     want = oc.probe(ref, m, k, pd, n, offsets=off)
-    with seb.option("build_algo", algo), seb.option("varlen_long", long_pass):
+    with seb.option("build_algo", algo):
         kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
         words, bits = dev_build_bits(seb, torch, kd, m, k)
         assert np.array_equal(bits, ref)
@@ -638,10 +633,9 @@ def test_varlen_bucketed_build_chunks(seb, torch_cuda, k):
         assert np.array_equal(bits, ref)
 
 
-@pytest.mark.parametrize("long_pass", [0, 2])
-def test_c4_varlen_10m_properties(seb, golden, torch_cuda, long_pass):
+def test_c4_varlen_10m_properties(seb, golden, torch_cuda):
     """Full C4 size: the filter and the 10M answers match the golden digests (tests/golden varlen
-    n = 10M, the oracle's), and every built key answers true; with and without the long-key pass."""
+    n = 10M, the oracle's), and every built key answers true."""
     torch = torch_cuda
     n = 10_000_000
     row = next(r for r in golden["varlen"] if r["n"] == n)
@@ -649,17 +643,16 @@ def test_c4_varlen_10m_properties(seb, golden, torch_cuda, long_pass):
     assert (m, k) == (row["m"], row["k"])
     data, off = kg.varlen_keys(np.arange(n))
     pdata, poff = kg.varlen_keys(kg.probe_indices(n))
-    with seb.option("varlen_long", long_pass):
-        kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
-        words, bits = dev_build_bits(seb, torch, kd, m, k)
-        assert sha(bn.encode(bits, m, k)) == row["encode_sha256"]
-        out = torch.empty(n, dtype=torch.uint8, device="cuda")
-        seb.dev_probe(kd, words, m, k, out)  # every built key must answer true
-        torch.cuda.synchronize()
-        assert bool(out.all())
-        seb.dev_probe(seb.dev_keys(to_dev(torch, pdata), to_dev(torch, poff)), words, m, k, out)
-        torch.cuda.synchronize()
-        assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
+    kd = seb.dev_keys(to_dev(torch, data), to_dev(torch, off))
+    words, bits = dev_build_bits(seb, torch, kd, m, k)
+    assert sha(bn.encode(bits, m, k)) == row["encode_sha256"]
+    out = torch.empty(n, dtype=torch.uint8, device="cuda")
+    seb.dev_probe(kd, words, m, k, out)  # every built key must answer true
+    torch.cuda.synchronize()
+    assert bool(out.all())
+    seb.dev_probe(seb.dev_keys(to_dev(torch, pdata), to_dev(torch, poff)), words, m, k, out)
+    torch.cuda.synchronize()
+    assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
 @pytest.mark.parametrize("stride", [0, 1, 3, 13, 16, 24, 33, 64])

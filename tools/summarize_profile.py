@@ -34,8 +34,8 @@ STEP_KERNELS = {  # per config: timed step name -> kernels launched by that step
     "c2c3": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "k_clear_words"),
              "probe": ("k_probe",)},
     # the pre-hash is k_hash_varlen<..., false> for the build and <..., true> (phase 0 fused) for the probe
-    "c4": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "1u, false>", "2u, false>"),
-           "probe": ("k_probe", "1u, true>", "2u, true>")},
+    "c4": {"build": ("k_bkt_scatter", "k_bkt_apply", "k_build<", "1u, false>", "2u, false>", "true, 1u, false"),
+           "probe": ("k_probe", "1u, true>", "2u, true>", "true, 1u, true")},
     "c5": {"probe": ("k_probe_interleaved", "k_interleave", "k_probe_multi")},
     "lsm": {"probe": ("k_multiget", "k_mg_")},
     "lsm_wide": {"probe": ("k_multiget", "k_mg_")},
