@@ -28,11 +28,13 @@
  * (oracle/bloom_np.py) on every committed fixture.  See DESIGN.md "Oracle".
  */
 #define _POSIX_C_SOURCE 200809L
+#define _DEFAULT_SOURCE  /* MADV_HUGEPAGE */
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
+#include <sys/mman.h>
 
 #define FNV_OFFSET 0xcbf29ce484222325ULL
 #define FNV_PRIME 0x100000001b3ULL
@@ -288,9 +290,24 @@ typedef struct {
     int err;
 } priv_job;
 
+/* A zeroed private filter on 2 MiB pages where the kernel allows them (madvise; 6 TLB entries for
+ * a 12 MB filter instead of ~3000, which the random byte ORs would otherwise miss in), first
+ * touched by its own thread. */
+static uint8_t *private_filter(uint64_t nbytes) {
+    const size_t huge = (size_t)2 << 20;
+    const size_t size = ((nbytes ? nbytes : 1) + huge - 1) / huge * huge;
+    void *p = NULL;
+    if (posix_memalign(&p, huge, size) != 0) return NULL;
+#ifdef MADV_HUGEPAGE
+    (void)madvise(p, size, MADV_HUGEPAGE);
+#endif
+    memset(p, 0, size);
+    return (uint8_t *)p;
+}
+
 static void *build_private_worker(void *arg) {
     priv_job *j = (priv_job *)arg;
-    uint8_t *mine = (uint8_t *)calloc(j->nbytes ? j->nbytes : 1, 1);
+    uint8_t *mine = private_filter(j->nbytes);
     j->priv[j->t] = mine;
     if (mine) {
         for (uint64_t i = j->job.lo; i < j->job.hi; i++) {
