@@ -236,8 +236,8 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
 //                   of 16-B keys (read through the chunk's lines), or of key indices for batches it
 //                   cannot move, contiguously, and each key's sorted row (rowpos, in batch order)
 // k_multiget then writes answer j at sorted row j (whole lines, no scattered 8-B stores), and
-//   k_mg_unpermute  out[i] = answers[rowpos[i]]: reads from the chunks' contiguous runs, writes
-//                   whole lines in batch order.
+//   k_mg_unpermute  out[i] = answers[rowpos[i]], written as whole lines in batch order (a gather per
+//                   key, or per chunk through LDS, reading the chunk's runs in row order).
 // Round 3 wrote answers at each key's own index from k_multiget: one 32-B write per 8-B mask (517 MB
 // written per 10M-key call for 80 MB of masks, profiles/r04_lsm_pmc.csv); the order array (40 MB)
 // is no longer needed either for moved keys.
@@ -246,6 +246,7 @@ constexpr uint32_t kMgChunk = 2048;  // keys ranked in LDS at a time by k_mg_sca
 // each, no serial chunk loop) measured the same within 1% (profiles/r05e_mg_tiles.txt).
 constexpr uint32_t kMgTiles = 768;
 constexpr uint32_t kMgBucketThreads = 1024;
+
 constexpr uint32_t kMgWaves = 4;                      // 256-thread ordering blocks
 constexpr uint32_t kMgSteps = kMgChunk / kMgWaves / 64;  // 64-key steps of one wave's chunk segment
 
@@ -489,18 +490,83 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *
 }
 
 // out[i] = answers[rowpos[i]]: each key's answer from its sorted row, written in batch order as
-// whole lines.  The reads come from the chunk's bucket runs, each contiguous in the sorted rows, so
-// a wave's 64 keys read a few dozen runs and the lines are shared between neighbouring waves.
-// E: the answer as one unit (uint2 masks, u32/u16 granules of a candidate row, ge per answer).
+// whole lines.  E: the answer as one unit (uint2 masks, uint3 six-slot rows, uint4), ge = 1.
+//   k_mg_unpermute         one workgroup per chunk of kMgChunk keys: the chunk's keys of one bucket
+//                          hold a contiguous run of rows (the scatter placed them so), which starts at
+//                          their smallest rowpos; the runs are read in row order into LDS (contiguous
+//                          loads) and each key takes its answer from its slot there;
+//   k_mg_unpermute_gather  (other row widths) one key per thread, its answer read at its row: a
+//                          wave's 64 keys read one line per bucket run they touch, so many buckets
+//                          (short runs) cost a line per key.
 template <typename E>
-__global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const uint32_t *__restrict__ rowpos,
-                                                      const E *__restrict__ answers, E *__restrict__ out,
-                                                      uint32_t ge) {
+__global__ __launch_bounds__(256) void k_mg_unpermute_gather(uint64_t n, const uint32_t *__restrict__ rowpos,
+                                                             const E *__restrict__ answers, E *__restrict__ out,
+                                                             uint32_t ge) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint64_t r = rowpos[i];
         for (uint32_t g = 0; g < ge; ++g) out[i * ge + g] = answers[r * ge + g];
     }
+}
+
+// LDS (dynamic): cnt/loc[nb + 1] | rmin[nb] | wsum[4] (u32) | sb[kMgChunk] (u16) | stage[kMgChunk] (E)
+template <typename E>
+static size_t mg_unpermute_lds(uint32_t nb) {
+    return ((((size_t)nb + 1 + nb + 4) * 4 + 2 * kMgChunk + 15) & ~(size_t)15) + (size_t)kMgChunk * sizeof(E);
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const uint16_t *__restrict__ bucket,
+                                                      const uint32_t *__restrict__ rowpos, uint32_t nb,
+                                                      const E *__restrict__ answers, E *__restrict__ out) {
+    extern __shared__ uint4 mgu_lds[];
+    uint32_t *loc = (uint32_t *)mgu_lds;
+    uint32_t *rmin = loc + nb + 1;
+    uint32_t *wsum = rmin + nb;
+    uint16_t *sb = (uint16_t *)(wsum + 4);
+    E *stage = (E *)((uint8_t *)mgu_lds + ((((size_t)nb + 1 + nb + 4) * 4 + 2 * kMgChunk + 15) & ~(size_t)15));
+    constexpr uint32_t kPer = kMgChunk / 256;
+    const uint64_t c0 = (uint64_t)blockIdx.x * kMgChunk;
+    const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, n - c0);
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {
+        loc[u] = 0u;
+        rmin[u] = 0xffffffffu;
+    }
+    uint32_t bk[kPer], rp[kPer];
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; ++r) {  // every load issued before any is used
+        const uint32_t q = r * 256 + threadIdx.x;
+        bk[r] = q < cnt ? bucket[c0 + q] : nb;
+        rp[r] = q < cnt ? rowpos[c0 + q] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; ++r)
+        if (bk[r] < nb) {
+            atomicAdd(&loc[bk[r]], 1u);
+            atomicMin(&rmin[bk[r]], rp[r]);
+        }
+    __syncthreads();
+    block_scan_lds(loc, nb, wsum);
+    if (threadIdx.x == 0) loc[nb] = cnt;
+    uint32_t slot[kPer];
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; ++r)
+        if (bk[r] < nb) {
+            slot[r] = loc[bk[r]] + (rp[r] - rmin[bk[r]]);
+            sb[slot[r]] = (uint16_t)bk[r];
+        }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < cnt; p += blockDim.x) {  // the chunk's runs, in row order
+        const uint32_t b = min((uint32_t)sb[p], nb - 1);
+        uint64_t row = (uint64_t)rmin[b] + (p - loc[b]);
+        row = row < n ? row : n - 1;  // always true when the rows are the scatter's; a guard
+        stage[p] = answers[row];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; ++r)
+        if (bk[r] < nb) out[c0 + r * 256 + threadIdx.x] = stage[slot[r]];
 }
 
 // L0 group table: one thread per output word (32 / bits entries; every member's bits of those
@@ -585,6 +651,8 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
     if (e != hipSuccess) return e;
     mo->active = true;
     mo->n = kb.n;
+    mo->nb = nb;
+    mo->bucket = bucket;
     mo->rowpos = rowpos;
     mo->key_order = moves ? nullptr : (const uint32_t *)moved;
     mo->keys = moves ? moved : nullptr;
@@ -598,20 +666,28 @@ hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answ
     if (g > 65536) g = 65536;
     const uint32_t *rp = mo.rowpos;
     const bool a16 = ((uintptr_t)out & 15) == 0, a8 = ((uintptr_t)out & 7) == 0, a4 = ((uintptr_t)out & 3) == 0;
-    if (answer_bytes == 16 && a16)
-        hipLaunchKernelGGL(k_mg_unpermute<uint4>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
-                           (const uint4 *)mo.answers, (uint4 *)out, 1u);
-    else if (answer_bytes == 12 && a4)  // 6-slot candidate rows: one dwordx3 per key
-        hipLaunchKernelGGL(k_mg_unpermute<uint3>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
-                           (const uint3 *)mo.answers, (uint3 *)out, 1u);
-    else if (answer_bytes == 8 && a8)
-        hipLaunchKernelGGL(k_mg_unpermute<uint2>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
-                           (const uint2 *)mo.answers, (uint2 *)out, 1u);
-    else if (answer_bytes % 4 == 0 && a4)
-        hipLaunchKernelGGL(k_mg_unpermute<uint32_t>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
+    // answers of 8, 12 or 16 B: one unit per key, per chunk through LDS (28 files, 17 buckets: 40.5 vs
+    // 44.9 us for the per-key gather; 244 files, 161 buckets: 63.9 vs 122.0 us,
+    // profiles/r05i_mg_unpermute.txt); other row widths take the gather in granules
+    auto unit = [&](auto e) -> hipError_t {
+        using E = decltype(e);
+        const uint64_t chunks = (mo.n + kMgChunk - 1) / kMgChunk;
+        const size_t lds = mg_unpermute_lds<E>(mo.nb);
+        hipError_t a = hipFuncSetAttribute((const void *)k_mg_unpermute<E>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+        if (a != hipSuccess) return a;
+        hipLaunchKernelGGL(k_mg_unpermute<E>, dim3((unsigned)chunks), dim3(256), lds, s, mo.n, mo.bucket, rp, mo.nb,
+                           (const E *)mo.answers, (E *)out);
+        return hipGetLastError();
+    };
+    if (answer_bytes == 16 && a16) return unit(uint4{});
+    if (answer_bytes == 12 && a4) return unit(uint3{});
+    if (answer_bytes == 8 && a8) return unit(uint2{});
+    if (answer_bytes % 4 == 0 && a4)
+        hipLaunchKernelGGL(k_mg_unpermute_gather<uint32_t>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
                            (const uint32_t *)mo.answers, (uint32_t *)out, (uint32_t)(answer_bytes / 4));
     else if (answer_bytes % 2 == 0)
-        hipLaunchKernelGGL(k_mg_unpermute<uint16_t>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
+        hipLaunchKernelGGL(k_mg_unpermute_gather<uint16_t>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
                            (const uint16_t *)mo.answers, (uint16_t *)out, (uint32_t)(answer_bytes / 2));
     else
         return hipErrorInvalidValue;
