@@ -15,6 +15,13 @@ for cfg in "c2c3 --bcast packed" "c2c3 --bcast keys" "c5" "c5_2d" "c5_2d --c5-gr
     timeout -k 10 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" --master-addr 127.0.0.1 \
         --master-port $port "$ROOT/bench.py" --gpus "$N" --steps 4 --warmup 2 --dist-backend gloo \
         --no-cpu-baseline --no-host-inclusive --config $cfg > "$OUT/rehearse_${N}_${tag}.json" 2> "$OUT/rehearse_${N}_${tag}.err"
-    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['n_gpus'], d['parity'], d.get('resident_batch', {}).get('parity', ''))" \
-        "$OUT/rehearse_${N}_${tag}.json" "$cfg"
+    python3 -c "
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(sys.argv[2], d['n_gpus'], d['parity'], d.get('resident_batch', {}).get('parity', ''))
+print('   devices', d['devices'], 'rank_check', d['rank_check'])
+for r in d['per_rank']:
+    print('   rank', r['rank'], r['device']['pci'], r['backend'], 'world', r['world_size'], 'ones', r['allreduce_ones'],
+          'kernel_ms', r['kernel_ms'], 'wait_ms', r['wait_ms'], 'elapsed_s', r['elapsed_s'])
+" "$OUT/rehearse_${N}_${tag}.json" "$cfg"
 done
