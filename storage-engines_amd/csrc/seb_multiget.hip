@@ -364,24 +364,12 @@ __global__ __launch_bounds__(kMgBucketThreads) void k_mg_bucket(KeyBatch kb, con
     }
     __syncthreads();
     const uint64_t end = tile_begin(kb.n, tl, t + 1);
-    // aligned 16-B keys (block-uniform): the next key's load is issued before this one's bisection
-    const bool k16 = !kb.offsets && kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0;
-    uint4 nxt = make_uint4(0, 0, 0, 0);
-    const uint64_t i0 = tile_begin(kb.n, tl, t) + threadIdx.x;
-    if (k16 && i0 < end) nxt = ((const uint4 *)kb.data)[i0];
-    for (uint64_t i = i0; i < end; i += blockDim.x) {
+    for (uint64_t i = tile_begin(kb.n, tl, t) + threadIdx.x; i < end; i += blockDim.x) {
         const uint8_t *key;
         uint32_t klen;
         key_at(kb, i, key, klen);
         uint64_t k0, k1;
-        if (k16) {
-            const uint4 v = nxt;
-            if (i + blockDim.x < end) nxt = ((const uint4 *)kb.data)[i + blockDim.x];
-            k0 = __builtin_bswap64((uint64_t)v.x | ((uint64_t)v.y << 32));
-            k1 = __builtin_bswap64((uint64_t)v.z | ((uint64_t)v.w << 32));
-        } else {
-            key_prefix(kb, key, klen, k0, k1);
-        }
+        key_prefix(kb, key, klen, k0, k1);
         uint32_t a = lo, b = hi;
         while (a < b) {
             const uint32_t mid = (a + b) >> 1;
