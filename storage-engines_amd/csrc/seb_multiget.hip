@@ -350,6 +350,34 @@ __device__ __forceinline__ void chunk_positions(const uint32_t (&bk)[kMgSteps], 
     __syncthreads();
 }
 
+constexpr uint32_t kMgBucketBatch = 4;
+
+// The partition level's bucket of a key: the number of its files whose MinKey <= key (bisection over
+// the 16-B MinKey prefixes in LDS; equal prefixes fall back to the full compare).
+__device__ __forceinline__ uint32_t mg_bisect(const uint8_t *key, uint32_t klen, uint64_t k0, uint64_t k1,
+                                              const RegSlot *__restrict__ slots, uint32_t lo, uint32_t hi,
+                                              const uint8_t *__restrict__ ranges, const uint64_t *pmin) {
+    uint32_t a = lo, b = hi;
+    while (a < b) {
+        const uint32_t mid = (a + b) >> 1;
+        const uint64_t p0 = pmin[2 * (mid - lo)], p1 = pmin[2 * (mid - lo) + 1];
+        int c;
+        if (k0 != p0) {
+            c = k0 < p0 ? -1 : 1;
+        } else if (k1 != p1) {
+            c = k1 < p1 ? -1 : 1;
+        } else {
+            const RegSlot &sl = slots[mid];
+            c = cmp_key(key, klen, k0, k1, sl.min_be, ranges + sl.min_off, sl.min_len);
+        }
+        if (c >= 0)
+            a = mid + 1;
+        else
+            b = mid;
+    }
+    return a;
+}
+
 __global__ __launch_bounds__(kMgBucketThreads) void k_mg_bucket(KeyBatch kb, const RegSlot *__restrict__ slots, uint32_t lo,
                                                    uint32_t hi, const uint8_t *__restrict__ ranges,
                                                    uint16_t *__restrict__ bucket, uint32_t *__restrict__ hist,
@@ -364,7 +392,31 @@ __global__ __launch_bounds__(kMgBucketThreads) void k_mg_bucket(KeyBatch kb, con
     }
     __syncthreads();
     const uint64_t end = tile_begin(kb.n, tl, t + 1);
-    for (uint64_t i = tile_begin(kb.n, tl, t) + threadIdx.x; i < end; i += blockDim.x) {
+    const uint64_t beg = tile_begin(kb.n, tl, t);
+    // aligned 16-B keys: kMgBucketBatch keys per thread loaded at once (clamped indices, no branch
+    // to sink a load into), then bisected; other batches one key at a time
+    if (!kb.offsets && kb.stride == 16 && ((uintptr_t)kb.data & 15) == 0 && end > beg) {
+        const uint4 *kp = (const uint4 *)kb.data;
+        for (uint64_t i0 = beg + threadIdx.x; i0 < end; i0 += (uint64_t)kMgBucketBatch * blockDim.x) {
+            uint4 v[kMgBucketBatch];
+#pragma unroll
+            for (uint32_t r = 0; r < kMgBucketBatch; ++r) v[r] = kp[min(i0 + (uint64_t)r * blockDim.x, end - 1)];
+#pragma unroll
+            for (uint32_t r = 0; r < kMgBucketBatch; ++r) {
+                const uint64_t i = i0 + (uint64_t)r * blockDim.x;
+                if (i >= end) break;
+                const uint64_t k0 = __builtin_bswap64((uint64_t)v[r].x | ((uint64_t)v[r].y << 32));
+                const uint64_t k1 = __builtin_bswap64((uint64_t)v[r].z | ((uint64_t)v[r].w << 32));
+                const uint32_t a = mg_bisect(kb.data + i * 16, 16, k0, k1, slots, lo, hi, ranges, pmin);
+                bucket[i] = (uint16_t)(a - lo);
+                atomicAdd(&h[a - lo], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) hist[(uint64_t)u * T + t] = h[u];
+        return;
+    }
+    for (uint64_t i = beg + threadIdx.x; i < end; i += blockDim.x) {
         const uint8_t *key;
         uint32_t klen;
         key_at(kb, i, key, klen);
@@ -474,14 +526,27 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *
             }
         __syncthreads();
         if (c0 + kMgChunk < end) load_chunk_buckets(bucket, c0 + kMgChunk, end, nb, bk);  // during the stores
-        // each bucket's run of this chunk goes out contiguously
-        for (uint32_t q = threadIdx.x; q < cnt; q += blockDim.x) {
+        // each bucket's run of this chunk goes out contiguously: a thread's 8 rows are looked up, then
+        // their 8 key loads issued, then the 8 stores (a load-store pair per row waited for every load:
+        // one memory round trip per row).  Rows past cnt repeat row cnt - 1 (the same bytes to the same
+        // place), so no branch lets the compiler sink a load down to its store.
+        uint32_t dst[kMgSteps], src[kMgSteps];
+#pragma unroll
+        for (uint32_t r = 0; r < kMgSteps; ++r) {
+            const uint32_t q = min(r * 256 + threadIdx.x, cnt - 1);
             const uint32_t b = sb[q];
-            const uint32_t dst = base[b] + (q - loc[b]);
-            if constexpr (MOVE)
-                keys_out[dst] = keys[sidx[q]];
-            else
-                order[dst] = sidx[q];
+            dst[r] = base[b] + (q - loc[b]);
+            src[r] = sidx[q];
+        }
+        if constexpr (MOVE) {
+            uint4 v[kMgSteps];
+#pragma unroll
+            for (uint32_t r = 0; r < kMgSteps; ++r) v[r] = keys[src[r]];
+#pragma unroll
+            for (uint32_t r = 0; r < kMgSteps; ++r) keys_out[dst[r]] = v[r];
+        } else {
+#pragma unroll
+            for (uint32_t r = 0; r < kMgSteps; ++r) order[dst[r]] = src[r];
         }
         __syncthreads();
         for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] += loc[u + 1] - loc[u];
@@ -557,12 +622,17 @@ __global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const uint16_t
             sb[slot[r]] = (uint16_t)bk[r];
         }
     __syncthreads();
-    for (uint32_t p = threadIdx.x; p < cnt; p += blockDim.x) {  // the chunk's runs, in row order
+    E v[kPer];  // the chunk's runs, in row order: every load issued before any is stored
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; ++r) {
+        const uint32_t p = min(r * 256 + threadIdx.x, cnt - 1);
         const uint32_t b = min((uint32_t)sb[p], nb - 1);
         uint64_t row = (uint64_t)rmin[b] + (p - loc[b]);
         row = row < n ? row : n - 1;  // always true when the rows are the scatter's; a guard
-        stage[p] = answers[row];
+        v[r] = answers[row];
     }
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; ++r) stage[min(r * 256 + threadIdx.x, cnt - 1)] = v[r];
     __syncthreads();
 #pragma unroll
     for (uint32_t r = 0; r < kPer; ++r)
