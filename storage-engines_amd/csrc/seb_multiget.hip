@@ -56,6 +56,13 @@ __device__ __forceinline__ int cmp_key(const uint8_t *key, uint32_t klen, uint64
     return (int)klen - (int)blen;
 }
 
+// A filter word from global memory.  The words pointers come out of RegSlot / RegLayout structs, so
+// the compiler cannot tell their address space and would issue flat loads (which also count against
+// the LDS wait counter the slot table's reads use); the cast makes them global loads.
+__device__ __forceinline__ uint32_t gword(const uint32_t *w, uint64_t i) {
+    return ((const __attribute__((address_space(1))) uint32_t *)w)[i];
+}
+
 // MayContain of one filter, with the reference's early exit (lsm/bloom.go:86-89): a position is
 // gathered only while every bit so far is set.  Gathering all k unconditionally cost 42 L2
 // requests per key over a MultiGet's 6 filter tests (profiles/r01y_lsm_pmc.csv); the early exit
@@ -64,7 +71,7 @@ template <int KFIX, bool M32>
 __device__ __forceinline__ uint32_t test_filter(const RegSlot &sl, uint64_t h1, uint64_t h2) {
     uint32_t acc = 1u;
     for_positions<KFIX, M32>(h1, h2, sl.md, sl.md.k, [&](uint32_t, uint64_t p) {
-        if (acc & 1u) acc &= sl.words[p >> 5] >> (uint32_t)(p & 31);
+        if (acc & 1u) acc &= gword(sl.words, p >> 5) >> (uint32_t)(p & 31);
     });
     return acc & 1u;
 }
@@ -78,7 +85,7 @@ __device__ __forceinline__ uint32_t test_l0_group(const RegLayout &lay, uint64_t
     for_positions<KFIX, M32>(h1, h2, lay.l0md, lay.l0md.k, [&](uint32_t, uint64_t p) {
         if (alive) {
             const uint64_t bit = p * lay.l0b;
-            alive &= lay.l0tab[bit >> 5] >> (uint32_t)(bit & 31);
+            alive &= gword(lay.l0tab, bit >> 5) >> (uint32_t)(bit & 31);
         }
     });
     return alive;

@@ -231,7 +231,20 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
     }
     if (t < kLenBuckets) cur[t] = 0u;
     if (t < NS) xflag[t] = 0u;
-    for (uint32_t c = t; c < (uint32_t)chunks; c += blockDim.x) stage[c] = ((const uint4 *)base)[c];
+    {  // the span, 4 chunks per thread per batch: every load issued before any LDS store (a load-store
+       // pair per chunk waited for every load), through a pointer that keeps the kernel argument's
+       // global address space (a uintptr_t round trip made these flat loads); clamped chunk indices
+       // repeat the last chunk (the same bytes to the same place), so no branch sinks a load
+        const uint4 *src = (const uint4 *)(data + (off[k0] - (s0 & 15)));
+        const uint32_t nc = (uint32_t)chunks;
+        for (uint32_t c0 = t; c0 < nc; c0 += 4 * blockDim.x) {
+            uint4 v[4];
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) v[r] = src[min(c0 + r * blockDim.x, nc - 1)];
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) stage[min(c0 + r * blockDim.x, nc - 1)] = v[r];
+        }
+    }
     const uint32_t len = (uint32_t)(ke - ks);
     const uint32_t dw = (len + 3) >> 2;
     const uint32_t bk = dw > 64 ? 64u : dw;
