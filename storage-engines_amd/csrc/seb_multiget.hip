@@ -241,10 +241,10 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
 //   k_mg_scatter    tile t: scans the row totals into bucket bases, then per chunk of kMgChunk keys
 //                   ranks the keys by bucket (stable, chunk_positions) and writes each bucket's run
 //                   of 16-B keys (read through the chunk's lines), or of key indices for batches it
-//                   cannot move, contiguously, and each key's sorted row (rowpos, in batch order)
+//                   cannot move, contiguously, and where each bucket's run of the chunk starts (runs)
 // k_multiget then writes answer j at sorted row j (whole lines, no scattered 8-B stores), and
-//   k_mg_unpermute  out[i] = answers[rowpos[i]], written as whole lines in batch order (a gather per
-//                   key, or per chunk through LDS, reading the chunk's runs in row order).
+//   k_mg_unpermute  per chunk: the same stable ranks again, the chunk's runs read in row order into
+//                   LDS, every key's answer written back in batch order as whole lines.
 // Round 3 wrote answers at each key's own index from k_multiget: one 32-B write per 8-B mask (517 MB
 // written per 10M-key call for 80 MB of masks, profiles/r04_lsm_pmc.csv); the order array (40 MB)
 // is no longer needed either for moved keys.
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *
                                                     const uint32_t *__restrict__ hist,
                                                     const uint32_t *__restrict__ totals, uint32_t nb, uint32_t bits,
                                                     uint32_t *__restrict__ order, const uint4 *__restrict__ keys,
-                                                    uint4 *__restrict__ keys_out, uint32_t *__restrict__ rowpos,
+                                                    uint4 *__restrict__ keys_out, uint32_t *__restrict__ runs,
                                                     uint32_t tl) {
     extern __shared__ uint4 mg_lds[];
     uint32_t *base = (uint32_t *)mg_lds;          // next output row of each bucket for this tile
@@ -528,9 +528,10 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *
             if (bk[s] < nb) {
                 sidx[pos[s]] = (uint32_t)(c0 + chunk_key(s));
                 sb[pos[s]] = (uint16_t)bk[s];
-                // the key's sorted row, in batch order (coalesced): k_mg_unpermute gathers through it
-                rowpos[c0 + chunk_key(s)] = base[bk[s]] + (pos[s] - loc[bk[s]]);
             }
+        // where each bucket's run of this chunk starts in the sorted rows: with the stable ranks,
+        // which k_mg_unpermute re-derives from the bucket ids, it gives every key's row
+        for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) runs[(c0 / kMgChunk) * nb + u] = base[u];
         __syncthreads();
         if (c0 + kMgChunk < end) load_chunk_buckets(bucket, c0 + kMgChunk, end, nb, bk);  // during the stores
         // each bucket's run of this chunk goes out contiguously: a thread's 8 rows are looked up, then
@@ -561,89 +562,74 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *
     }
 }
 
-// out[i] = answers[rowpos[i]]: each key's answer from its sorted row, written in batch order as
-// whole lines.  E: the answer as one unit (uint2 masks, uint3 six-slot rows, uint4), ge = 1.
-//   k_mg_unpermute         one workgroup per chunk of kMgChunk keys: the chunk's keys of one bucket
-//                          hold a contiguous run of rows (the scatter placed them so), which starts at
-//                          their smallest rowpos; the runs are read in row order into LDS (contiguous
-//                          loads) and each key takes its answer from its slot there;
-//   k_mg_unpermute_gather  (other row widths) one key per thread, its answer read at its row: a
-//                          wave's 64 keys read one line per bucket run they touch, so many buckets
-//                          (short runs) cost a line per key.
-template <typename E>
-__global__ __launch_bounds__(256) void k_mg_unpermute_gather(uint64_t n, const uint32_t *__restrict__ rowpos,
-                                                             const E *__restrict__ answers, E *__restrict__ out,
-                                                             uint32_t ge) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t r = rowpos[i];
-        for (uint32_t g = 0; g < ge; ++g) out[i * ge + g] = answers[r * ge + g];
-    }
-}
+// Each key's answer back from its sorted row to batch order, one workgroup per chunk of kMgChunk
+// keys: the chunk's stable ranks are derived again from its bucket ids (chunk_positions, as the
+// scatter ranked them), so key q of bucket b sits at row runs[chunk][b] + its rank; the chunk's runs
+// are read in row order into LDS (contiguous loads, all issued before any is stored) and each key
+// stores its answer from its slot there, as whole lines.  G: the unit read and written (uint2 masks,
+// uint3 six-slot rows, uint4, or u32 / u16 granules of other row widths, ge per answer, staged
+// kMgStage bytes per key per pass).  A per-key gather through a stored row index instead took 44.9 /
+// 122.0 us (masks of 28 files / 6-slot rows of 244: short runs cost it a line per key) and its
+// index 80 MB of traffic (profiles/r05i_mg_unpermute.txt).
+constexpr uint32_t kMgStage = 16;
 
-// LDS (dynamic): cnt/loc[nb + 1] | rmin[nb] | wsum[4] (u32) | sb[kMgChunk] (u16) | stage[kMgChunk] (E)
-template <typename E>
+template <typename G>
 static size_t mg_unpermute_lds(uint32_t nb) {
-    return ((((size_t)nb + 1 + nb + 4) * 4 + 2 * kMgChunk + 15) & ~(size_t)15) + (size_t)kMgChunk * sizeof(E);
+    const size_t head = ((size_t)nb + 1 + (size_t)kMgWaves * nb + 4 + nb) * 4 + 2 * kMgChunk;
+    const size_t slice = sizeof(G) >= kMgStage ? 1 : kMgStage / sizeof(G);
+    return ((head + 15) & ~(size_t)15) + (size_t)kMgChunk * slice * sizeof(G);
 }
 
-template <typename E>
+template <typename G>
 __global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const uint16_t *__restrict__ bucket,
-                                                      const uint32_t *__restrict__ rowpos, uint32_t nb,
-                                                      const E *__restrict__ answers, E *__restrict__ out) {
+                                                      const uint32_t *__restrict__ runs, uint32_t nb, uint32_t bits,
+                                                      const G *__restrict__ answers, G *__restrict__ out,
+                                                      uint32_t ge) {
     extern __shared__ uint4 mgu_lds[];
+    constexpr uint32_t kSlice = sizeof(G) >= kMgStage ? 1 : kMgStage / sizeof(G);  // granules per key per pass
     uint32_t *loc = (uint32_t *)mgu_lds;
-    uint32_t *rmin = loc + nb + 1;
-    uint32_t *wsum = rmin + nb;
-    uint16_t *sb = (uint16_t *)(wsum + 4);
-    E *stage = (E *)((uint8_t *)mgu_lds + ((((size_t)nb + 1 + nb + 4) * 4 + 2 * kMgChunk + 15) & ~(size_t)15));
-    constexpr uint32_t kPer = kMgChunk / 256;
+    uint32_t *cw = loc + nb + 1;
+    uint32_t *wsum = cw + kMgWaves * nb;
+    uint32_t *rbase = wsum + 4;
+    uint16_t *sb = (uint16_t *)(rbase + nb);
+    G *stage = (G *)((uint8_t *)mgu_lds +
+                     ((((size_t)nb + 1 + (size_t)kMgWaves * nb + 4 + nb) * 4 + 2 * kMgChunk + 15) & ~(size_t)15));
     const uint64_t c0 = (uint64_t)blockIdx.x * kMgChunk;
     const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, n - c0);
-    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {
-        loc[u] = 0u;
-        rmin[u] = 0xffffffffu;
-    }
-    uint32_t bk[kPer], rp[kPer];
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) rbase[u] = runs[(uint64_t)blockIdx.x * nb + u];
+    uint32_t bk[kMgSteps], pos[kMgSteps];
+    load_chunk_buckets(bucket, c0, c0 + cnt, nb, bk);
+    chunk_positions(bk, cnt, nb, bits, cw, loc, wsum, pos);  // synchronises (rbase is visible after it)
 #pragma unroll
-    for (uint32_t r = 0; r < kPer; ++r) {  // every load issued before any is used
-        const uint32_t q = r * 256 + threadIdx.x;
-        bk[r] = q < cnt ? bucket[c0 + q] : nb;
-        rp[r] = q < cnt ? rowpos[c0 + q] : 0u;
-    }
+    for (uint32_t s = 0; s < kMgSteps; ++s)
+        if (bk[s] < nb) sb[pos[s]] = (uint16_t)bk[s];
     __syncthreads();
+    for (uint32_t g0 = 0; g0 < ge; g0 += kSlice) {
+        const uint32_t gs = min(kSlice, ge - g0), units = cnt * gs;
+        for (uint32_t u0 = threadIdx.x; u0 < units; u0 += 8 * 256) {
+            G v[8];
 #pragma unroll
-    for (uint32_t r = 0; r < kPer; ++r)
-        if (bk[r] < nb) {
-            atomicAdd(&loc[bk[r]], 1u);
-            atomicMin(&rmin[bk[r]], rp[r]);
+            for (uint32_t r = 0; r < 8; ++r) {  // clamped: a unit past the end repeats the last one
+                const uint32_t u = min(u0 + r * 256, units - 1), p = u / gs, g = u - p * gs;
+                const uint32_t b = min((uint32_t)sb[p], nb - 1);
+                uint64_t row = (uint64_t)rbase[b] + (p - loc[b]);
+                row = row < n ? row : n - 1;  // always true when the runs are the scatter's; a guard
+                v[r] = answers[row * ge + g0 + g];
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < 8; ++r) {
+                const uint32_t u = min(u0 + r * 256, units - 1), p = u / gs, g = u - p * gs;
+                stage[p * kSlice + g] = v[r];
+            }
         }
-    __syncthreads();
-    block_scan_lds(loc, nb, wsum);
-    if (threadIdx.x == 0) loc[nb] = cnt;
-    uint32_t slot[kPer];
+        __syncthreads();
 #pragma unroll
-    for (uint32_t r = 0; r < kPer; ++r)
-        if (bk[r] < nb) {
-            slot[r] = loc[bk[r]] + (rp[r] - rmin[bk[r]]);
-            sb[slot[r]] = (uint16_t)bk[r];
-        }
-    __syncthreads();
-    E v[kPer];  // the chunk's runs, in row order: every load issued before any is stored
-#pragma unroll
-    for (uint32_t r = 0; r < kPer; ++r) {
-        const uint32_t p = min(r * 256 + threadIdx.x, cnt - 1);
-        const uint32_t b = min((uint32_t)sb[p], nb - 1);
-        uint64_t row = (uint64_t)rmin[b] + (p - loc[b]);
-        row = row < n ? row : n - 1;  // always true when the rows are the scatter's; a guard
-        v[r] = answers[row];
+        for (uint32_t s = 0; s < kMgSteps; ++s)
+            if (bk[s] < nb)
+                for (uint32_t g = 0; g < gs; ++g)
+                    out[(c0 + chunk_key(s)) * ge + g0 + g] = stage[pos[s] * kSlice + g];
+        __syncthreads();
     }
-#pragma unroll
-    for (uint32_t r = 0; r < kPer; ++r) stage[min(r * 256 + threadIdx.x, cnt - 1)] = v[r];
-    __syncthreads();
-#pragma unroll
-    for (uint32_t r = 0; r < kPer; ++r)
-        if (bk[r] < nb) out[c0 + r * 256 + threadIdx.x] = stage[slot[r]];
 }
 
 // L0 group table: one thread per output word (32 / bits entries; every member's bits of those
@@ -691,10 +677,12 @@ static uint32_t order_tiles(uint64_t n) {
 
 static uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
 
+static uint64_t run_bytes(uint64_t n) { return al256(4ull * kMgMaxBuckets * ((n + kMgChunk - 1) / kMgChunk)); }
+
 uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes) {
     const uint64_t n = kb.n;
     return al256(n * 2) + al256(4ull * kMgMaxBuckets * order_tiles(n)) + al256(4 * kMgMaxBuckets) +
-           al256(multiget_order_moves(kb) ? n * 16 : n * 4) + al256(n * 4) + al256(n * answer_bytes);
+           al256(multiget_order_moves(kb) ? n * 16 : n * 4) + run_bytes(n) + al256(n * answer_bytes);
 }
 
 hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
@@ -709,8 +697,8 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
     uint32_t *totals = (uint32_t *)(p += al256(4ull * kMgMaxBuckets * T));
     uint8_t *moved = p += al256(4 * kMgMaxBuckets);
     const bool moves = multiget_order_moves(kb);
-    uint32_t *rowpos = (uint32_t *)(p + al256(moves ? kb.n * 16 : kb.n * 4));
-    void *answers = (uint8_t *)rowpos + al256(kb.n * 4);
+    uint32_t *runs = (uint32_t *)(p + al256(moves ? kb.n * 16 : kb.n * 4));
+    void *answers = (uint8_t *)runs + run_bytes(kb.n);
     uint32_t bits = 0;
     while ((1u << bits) <= nb) ++bits;  // bucket ids and the "no key" value nb
     hipLaunchKernelGGL(k_mg_bucket, dim3(T), dim3(kMgBucketThreads), 0, s, kb, slots, lo, hi, ranges, bucket, hist, tl);
@@ -723,14 +711,15 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
     if (a != hipSuccess) return a;
     hipLaunchKernelGGL(scat, dim3(T), dim3(256), lds, s, kb.n, bucket, hist, totals, nb, bits,
                        moves ? nullptr : (uint32_t *)moved, (const uint4 *)kb.data, moves ? (uint4 *)moved : nullptr,
-                       rowpos, tl);
+                       runs, tl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     mo->active = true;
     mo->n = kb.n;
     mo->nb = nb;
+    mo->bits = bits;
     mo->bucket = bucket;
-    mo->rowpos = rowpos;
+    mo->runs = runs;
     mo->key_order = moves ? nullptr : (const uint32_t *)moved;
     mo->keys = moves ? moved : nullptr;
     mo->answers = answers;
@@ -739,36 +728,24 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
 
 hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answer_bytes, hipStream_t s) {
     if (!mo.active || mo.n == 0) return hipSuccess;
-    uint64_t g = (mo.n + 255) / 256;
-    if (g > 65536) g = 65536;
-    const uint32_t *rp = mo.rowpos;
-    const bool a16 = ((uintptr_t)out & 15) == 0, a8 = ((uintptr_t)out & 7) == 0, a4 = ((uintptr_t)out & 3) == 0;
-    // answers of 8, 12 or 16 B: one unit per key, per chunk through LDS (28 files, 17 buckets: 40.5 vs
-    // 44.9 us for the per-key gather; 244 files, 161 buckets: 63.9 vs 122.0 us,
-    // profiles/r05i_mg_unpermute.txt); other row widths take the gather in granules
-    auto unit = [&](auto e) -> hipError_t {
-        using E = decltype(e);
-        const uint64_t chunks = (mo.n + kMgChunk - 1) / kMgChunk;
-        const size_t lds = mg_unpermute_lds<E>(mo.nb);
-        hipError_t a = hipFuncSetAttribute((const void *)k_mg_unpermute<E>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    const uint64_t chunks = (mo.n + kMgChunk - 1) / kMgChunk;
+    auto go = [&](auto g, uint32_t ge) -> hipError_t {
+        using G = decltype(g);
+        const size_t lds = mg_unpermute_lds<G>(mo.nb);
+        hipError_t a = hipFuncSetAttribute((const void *)k_mg_unpermute<G>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds);
         if (a != hipSuccess) return a;
-        hipLaunchKernelGGL(k_mg_unpermute<E>, dim3((unsigned)chunks), dim3(256), lds, s, mo.n, mo.bucket, rp, mo.nb,
-                           (const E *)mo.answers, (E *)out);
+        hipLaunchKernelGGL(k_mg_unpermute<G>, dim3((unsigned)chunks), dim3(256), lds, s, mo.n, mo.bucket, mo.runs, mo.nb,
+                           mo.bits, (const G *)mo.answers, (G *)out, ge);
         return hipGetLastError();
     };
-    if (answer_bytes == 16 && a16) return unit(uint4{});
-    if (answer_bytes == 12 && a4) return unit(uint3{});
-    if (answer_bytes == 8 && a8) return unit(uint2{});
-    if (answer_bytes % 4 == 0 && a4)
-        hipLaunchKernelGGL(k_mg_unpermute_gather<uint32_t>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
-                           (const uint32_t *)mo.answers, (uint32_t *)out, (uint32_t)(answer_bytes / 4));
-    else if (answer_bytes % 2 == 0)
-        hipLaunchKernelGGL(k_mg_unpermute_gather<uint16_t>, dim3((unsigned)g), dim3(256), 0, s, mo.n, rp,
-                           (const uint16_t *)mo.answers, (uint16_t *)out, (uint32_t)(answer_bytes / 2));
-    else
-        return hipErrorInvalidValue;
-    return hipGetLastError();
+    const bool a16 = ((uintptr_t)out & 15) == 0, a8 = ((uintptr_t)out & 7) == 0, a4 = ((uintptr_t)out & 3) == 0;
+    if (answer_bytes == 16 && a16) return go(uint4{}, 1u);
+    if (answer_bytes == 12 && a4) return go(uint3{}, 1u);  // 6-slot candidate rows
+    if (answer_bytes == 8 && a8) return go(uint2{}, 1u);   // masks
+    if (answer_bytes % 4 == 0 && a4) return go(uint32_t{}, (uint32_t)(answer_bytes / 4));
+    if (answer_bytes % 2 == 0) return go(uint16_t{}, (uint32_t)(answer_bytes / 2));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
