@@ -1298,11 +1298,14 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
         want_mask = reg.multiget(probes)
         want_list = reg.multiget_list(probes)
         want_odd = reg.multiget_list(probes, cap=5)  # odd rows: the unpermute moves u16 granules
+        want_wide = reg.multiget_list(probes, cap=20)  # 40-B rows: u32 granules staged in 3 passes
     for xcd in (0, 1):  # multiget_xcd: the XCD-contiguous block remap walks the same rows
         with seb.option("multiget_order", 1), seb.option("multiget_xcd", xcd):
             got_mask = reg.multiget(probes)
             got_list = reg.multiget_list(probes)
             got_odd = reg.multiget_list(probes, cap=5)
+            got_wide = reg.multiget_list(probes, cap=20)
+        assert np.array_equal(got_wide, want_wide) and np.array_equal(got_wide[:, :4], want_list), xcd
         assert np.array_equal(got_mask, want_mask), xcd
         assert np.array_equal(got_list, want_list), xcd
         assert np.array_equal(got_odd, want_odd) and np.array_equal(got_odd[:, :4], want_list), xcd
