@@ -101,7 +101,8 @@ struct MgOrder {
     bool active = false;          // false: the level does not apply; answer in batch order directly
     uint64_t n = 0;
     uint32_t nb = 0, bits = 0;            // buckets of the partition level, bits of a bucket id
-    const uint16_t *bucket = nullptr;     // each key's bucket, in batch order
+    const void *bucket = nullptr;         // each key's bucket, in batch order (u8 when bucket8, else u16)
+    bool bucket8 = false;
     const uint32_t *runs = nullptr;       // per chunk and bucket: the first sorted row of its run
     const uint32_t *key_order = nullptr;  // batches that are not moved: key index of each sorted row
     const uint8_t *keys = nullptr;        // aligned fixed 16-B batches: the keys moved into that order

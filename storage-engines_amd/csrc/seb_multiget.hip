@@ -385,9 +385,11 @@ __device__ __forceinline__ uint32_t mg_bisect(const uint8_t *key, uint32_t klen,
     return a;
 }
 
+// B: the bucket id type, u8 while the partition level has at most 255 files (nb <= 256), else u16.
+template <typename B>
 __global__ __launch_bounds__(kMgBucketThreads) void k_mg_bucket(KeyBatch kb, const RegSlot *__restrict__ slots, uint32_t lo,
                                                    uint32_t hi, const uint8_t *__restrict__ ranges,
-                                                   uint16_t *__restrict__ bucket, uint32_t *__restrict__ hist,
+                                                   B *__restrict__ bucket, uint32_t *__restrict__ hist,
                                                    uint32_t tl) {
     __shared__ uint32_t h[kMgMaxBuckets];
     __shared__ uint64_t pmin[2 * (kMgMaxBuckets - 1)];  // the level's MinKey prefixes (16 B per file)
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(kMgBucketThreads) void k_mg_bucket(KeyBatch kb, con
                 const uint64_t k0 = __builtin_bswap64((uint64_t)v[r].x | ((uint64_t)v[r].y << 32));
                 const uint64_t k1 = __builtin_bswap64((uint64_t)v[r].z | ((uint64_t)v[r].w << 32));
                 const uint32_t a = mg_bisect(kb.data + i * 16, 16, k0, k1, slots, lo, hi, ranges, pmin);
-                bucket[i] = (uint16_t)(a - lo);
+                bucket[i] = (B)(a - lo);
                 atomicAdd(&h[a - lo], 1u);
             }
         }
@@ -447,7 +449,7 @@ __global__ __launch_bounds__(kMgBucketThreads) void k_mg_bucket(KeyBatch kb, con
             else
                 b = mid;
         }
-        bucket[i] = (uint16_t)(a - lo);
+        bucket[i] = (B)(a - lo);
         atomicAdd(&h[a - lo], 1u);
     }
     __syncthreads();
@@ -478,7 +480,8 @@ __device__ __forceinline__ void tile_bases(const uint32_t *hist, const uint32_t 
 }
 
 // The buckets of chunk [c0, end) into registers (nb, i.e. "no key", past the end).
-__device__ __forceinline__ void load_chunk_buckets(const uint16_t *bucket, uint64_t c0, uint64_t end, uint32_t nb,
+template <typename B>
+__device__ __forceinline__ void load_chunk_buckets(const B *bucket, uint64_t c0, uint64_t end, uint32_t nb,
                                                    uint32_t (&bk)[kMgSteps]) {
     const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, end - c0);
 #pragma unroll
@@ -500,8 +503,8 @@ static size_t mg_scatter_lds(uint32_t nb) {
 // in batch order a chunk ahead, measured slower (163 vs 115 us, profiles/r05d_mg_stage.txt).
 // Otherwise the key indices are written in that order (key_order) for the MultiGet to read keys
 // through.
-template <bool MOVE>
-__global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const uint16_t *__restrict__ bucket,
+template <bool MOVE, typename B>
+__global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const B *__restrict__ bucket,
                                                     const uint32_t *__restrict__ hist,
                                                     const uint32_t *__restrict__ totals, uint32_t nb, uint32_t bits,
                                                     uint32_t *__restrict__ order, const uint4 *__restrict__ keys,
@@ -580,8 +583,8 @@ static size_t mg_unpermute_lds(uint32_t nb) {
     return ((head + 15) & ~(size_t)15) + (size_t)kMgChunk * slice * sizeof(G);
 }
 
-template <typename G>
-__global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const uint16_t *__restrict__ bucket,
+template <typename G, typename B>
+__global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const B *__restrict__ bucket,
                                                       const uint32_t *__restrict__ runs, uint32_t nb, uint32_t bits,
                                                       const G *__restrict__ answers, G *__restrict__ out,
                                                       uint32_t ge) {
@@ -692,7 +695,8 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
     if (kb.n == 0 || nb > kMgMaxBuckets || nb < 2 || kb.n > 0xffffffffull) return hipSuccess;
     const uint32_t T = order_tiles(kb.n), tl = tile_keys(kb.n);
     uint8_t *p = (uint8_t *)ws;
-    uint16_t *bucket = (uint16_t *)p;
+    void *bucket = p;
+    const bool b8 = nb <= 256;  // u8 bucket ids: 10 MB less written and 20 MB less read per 10M keys
     uint32_t *hist = (uint32_t *)(p += al256(kb.n * 2));
     uint32_t *totals = (uint32_t *)(p += al256(4ull * kMgMaxBuckets * T));
     uint8_t *moved = p += al256(4 * kMgMaxBuckets);
@@ -701,17 +705,28 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
     void *answers = (uint8_t *)runs + run_bytes(kb.n);
     uint32_t bits = 0;
     while ((1u << bits) <= nb) ++bits;  // bucket ids and the "no key" value nb
-    hipLaunchKernelGGL(k_mg_bucket, dim3(T), dim3(kMgBucketThreads), 0, s, kb, slots, lo, hi, ranges, bucket, hist, tl);
+    if (b8)
+        hipLaunchKernelGGL(k_mg_bucket<uint8_t>, dim3(T), dim3(kMgBucketThreads), 0, s, kb, slots, lo, hi, ranges,
+                           (uint8_t *)bucket, hist, tl);
+    else
+        hipLaunchKernelGGL(k_mg_bucket<uint16_t>, dim3(T), dim3(kMgBucketThreads), 0, s, kb, slots, lo, hi, ranges,
+                           (uint16_t *)bucket, hist, tl);
     hipLaunchKernelGGL(k_mg_rows, dim3(nb), dim3(256), 0, s, hist, T, totals);
     // aligned fixed 16-B keys are moved into bucket order (the MultiGet then streams them); other
     // batches get the key indices in that order
     const size_t lds = mg_scatter_lds(nb);
-    auto scat = moves ? k_mg_scatter<true> : k_mg_scatter<false>;
-    hipError_t a = hipFuncSetAttribute((const void *)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    auto scatter = [&](auto bt) -> hipError_t {
+        using B = decltype(bt);
+        auto scat = moves ? k_mg_scatter<true, B> : k_mg_scatter<false, B>;
+        hipError_t a = hipFuncSetAttribute((const void *)scat, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (a != hipSuccess) return a;
+        hipLaunchKernelGGL(scat, dim3(T), dim3(256), lds, s, kb.n, (const B *)bucket, hist, totals, nb, bits,
+                           moves ? nullptr : (uint32_t *)moved, (const uint4 *)kb.data, moves ? (uint4 *)moved : nullptr,
+                           runs, tl);
+        return hipSuccess;
+    };
+    hipError_t a = b8 ? scatter(uint8_t{}) : scatter(uint16_t{});
     if (a != hipSuccess) return a;
-    hipLaunchKernelGGL(scat, dim3(T), dim3(256), lds, s, kb.n, bucket, hist, totals, nb, bits,
-                       moves ? nullptr : (uint32_t *)moved, (const uint4 *)kb.data, moves ? (uint4 *)moved : nullptr,
-                       runs, tl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     mo->active = true;
@@ -719,6 +734,7 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
     mo->nb = nb;
     mo->bits = bits;
     mo->bucket = bucket;
+    mo->bucket8 = b8;
     mo->runs = runs;
     mo->key_order = moves ? nullptr : (const uint32_t *)moved;
     mo->keys = moves ? moved : nullptr;
@@ -729,16 +745,18 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
 hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answer_bytes, hipStream_t s) {
     if (!mo.active || mo.n == 0) return hipSuccess;
     const uint64_t chunks = (mo.n + kMgChunk - 1) / kMgChunk;
-    auto go = [&](auto g, uint32_t ge) -> hipError_t {
+    auto go_b = [&](auto g, auto bt, uint32_t ge) -> hipError_t {
         using G = decltype(g);
+        using B = decltype(bt);
         const size_t lds = mg_unpermute_lds<G>(mo.nb);
-        hipError_t a = hipFuncSetAttribute((const void *)k_mg_unpermute<G>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipError_t a = hipFuncSetAttribute((const void *)k_mg_unpermute<G, B>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds);
         if (a != hipSuccess) return a;
-        hipLaunchKernelGGL(k_mg_unpermute<G>, dim3((unsigned)chunks), dim3(256), lds, s, mo.n, mo.bucket, mo.runs, mo.nb,
-                           mo.bits, (const G *)mo.answers, (G *)out, ge);
+        hipLaunchKernelGGL((k_mg_unpermute<G, B>), dim3((unsigned)chunks), dim3(256), lds, s, mo.n, (const B *)mo.bucket,
+                           mo.runs, mo.nb, mo.bits, (const G *)mo.answers, (G *)out, ge);
         return hipGetLastError();
     };
+    auto go = [&](auto g, uint32_t ge) { return mo.bucket8 ? go_b(g, uint8_t{}, ge) : go_b(g, uint16_t{}, ge); };
     const bool a16 = ((uintptr_t)out & 15) == 0, a8 = ((uintptr_t)out & 7) == 0, a4 = ((uintptr_t)out & 3) == 0;
     if (answer_bytes == 16 && a16) return go(uint4{}, 1u);
     if (answer_bytes == 12 && a4) return go(uint3{}, 1u);  // 6-slot candidate rows
