@@ -199,10 +199,11 @@ int seb_timer_destroy(void *event);
  * so calls from several threads on one stream are safe (their launches do not interleave).
  * seb_workspace_bytes: bytes currently held; seb_workspace_release: synchronise the streams that
  * own scratch and free all of it (the next call re-allocates).  A phased probe holds ≈8.3 bytes per
- * key (its compacted packed words and group records); a key-range ordered registry MultiGet ≈34 bytes
- * per key of aligned 16-B keys (bucket ids, the moved keys, its answers in sorted rows, plus 4 KiB of
- * run starts per 1K keys), or ≈22 for keys it reads through an index; the scratch of a context's (or
- * a registry's) own streams is freed by seb_ctx_destroy (seb_registry_free). */
+ * key (its compacted packed words and group records); a key-range ordered registry MultiGet
+ * 20 bytes per key of aligned 16-B keys (bucket ids, run starts, the moved keys) or 8 for keys it
+ * reads through an index, plus its answers in sorted rows (8 bytes per key for masks, 2 per slot for
+ * candidate rows); the scratch of a context's (or a registry's) own streams is freed by
+ * seb_ctx_destroy (seb_registry_free). */
 uint64_t seb_workspace_bytes(void);
 int seb_workspace_release(void);
 
