@@ -10,10 +10,13 @@ c2c3 (default, the metric's config): one step on every GPU = build a new SSTable
 words written whole by seb_dev_build_fresh, no separate clear; --fresh-build 0: clear + build)
 from 10M x 16-B keys @1% FPR (BASELINE C2; m = 95,850,584, k = 7) and probe a 10M-key batch
 against it (C3, 50% present).  Rank g builds the filter of its own SSTable (keys key16(g*n + i));
-the probe batch arrives on rank 0 and is RCCL-broadcast to every GPU ahead of the step that
-probes it, so the transfer overlaps compute.  Since every rank's filter has the same (m, k), the
-batch travels as 8-byte packed residues that rank 0's own probe emits (--bcast packed, default;
---bcast keys sends the 16-B keys).  Per-GPU work is fixed as N grows (weak scaling); value =
+every rank probes every key of a new batch in every step.  Since every rank's filter has the same
+(m, k), the batch travels as 8-byte packed residues.  By default (--batch-origin spread) each batch
+arrives spread over the ranks, 1/N per GPU, each rank packs its part and an RCCL all-gather
+replicates the whole batch ahead of the step that probes it, so the transfer overlaps compute
+and every xGMI link carries 1/N of the batch; --batch-origin root: the batch arrives on rank 0
+and is RCCL-broadcast (its packed words emitted by rank 0's own probe; --bcast keys sends the
+16-B keys), also measured on the default line as its root_broadcast secondary.  Per-GPU work is fixed as N grows (weak scaling); value =
 (build + probe keys over all ranks) / max-over-ranks wall time, inputs already resident in HBM.
 c4: the same with variable-length keys (8-256 B, zipf); no broadcast.
 c2_sharded / c3_partitioned: ONE filter over the ranks: its 10M keys built from key
@@ -97,6 +100,9 @@ def parse():
     ap.add_argument("--time-every", type=int, default=4,
                     help="record the build/probe launch timers on every Nth timed step (and the last)")
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--kernel-reps", type=int, default=20,
+                    help="after the timed steps (outside their wall clock), this many more steps with every launch "
+                         "timed by HIP events: the kernel_timing median / min (SURVEY 8(d)); 0 skips; one GPU only")
     ap.add_argument("--config", default="c2c3", choices=["c2c3", "c4", "c5", "c5_2d", "lsm", "lsm_wide", "route",
                                                            "wal", "many", "c2_sharded", "c3_partitioned", "flush"])
     ap.add_argument("--keys", type=int, default=10_000_000)
@@ -118,6 +124,12 @@ def parse():
                     help="c2c3/c5, N > 1: 'step' (default, the headline) broadcasts a new probe batch from rank 0 "
                          "in every timed step (pipelined two steps ahead); 'resident' broadcasts it once before "
                          "the timed steps (measured as the line's resident_batch secondary as well)")
+    ap.add_argument("--batch-origin", default="spread", choices=["spread", "root"],
+                    help="c2c3, N > 1, --batch step: 'spread' (default) - each new batch arrives spread over the "
+                         "ranks (rank r holds 1/N of its keys, as when each GPU ingests its share over its own "
+                         "PCIe link) and is replicated by an RCCL all-gather of the ranks' packed residues; 'root' "
+                         "- it arrives on rank 0 and is RCCL-broadcast (measured as the line's root_broadcast "
+                         "secondary as well)")
     ap.add_argument("--c5-groups", type=int, default=None,
                     help="c5_2d: key groups R (default: the world size, i.e. every GPU holds all 64 filters)")
     ap.add_argument("--overlap", type=int, default=0,
@@ -141,6 +153,7 @@ class Setup:
     build = None
     build_host = probe_host = None
     broadcast_bufs = None
+    gather_bufs = None    # batches replicated by an all-gather (dist_probe.AllGatherPipeline)
     bcast_lead = 1        # batch j + lead is broadcast during step j (dist_probe.BroadcastPipeline)
     bcast_prologue = None # rank 0, before the loop: produce(b, buf) fills the buffer of batch b < lead
     pmc_key = None        # profiles/pmc_r01.json entry whose per-launch traffic applies (None: config name)
@@ -177,22 +190,44 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
     # packed words.  Every rank tests all 10M keys against its own filter in every step.
     packed = world > 1 and args.bcast == "packed" and k == 7 and m < (1 << 29)
     per_step = world > 1 and args.batch == "step"
+    spread = per_step and packed and args.batch_origin == "spread"
     st.workload = ("C2+C3: per GPU build one filter from 10M x 16B keys @1% FPR (m=95,850,584, k=7) "
                    + ("(a new filter: every word written by the build, no separate clear) " if args.fresh_build
                       else "(clear + build) ")
                    + "+ probe a 10M-key batch (50% present)")
     if world == 1:
         st.workload += ", resident in HBM (one GPU: no broadcast)"
+    elif spread:
+        st.workload += (", a new batch in every step, arriving spread over the ranks (1/N each) and "
+                        "replicated by an RCCL all-gather")
     elif per_step:
         st.workload += ", a new batch RCCL-broadcast from rank 0 in every step"
     else:
         st.workload += (", RCCL-broadcast from rank 0 once and resident in HBM on every GPU during the timed steps "
                         "(as at N = 1); the broadcast timed on its own")
-    if packed:
+    if spread:
+        # Rank r holds keys [lo, hi) of the batch; in step j it packs its part of batch j + 2
+        # (seb_dev_pack_residues) into its slice of that batch's buffer, the all-gather at the end
+        # of the step fills the other slices while steps j + 1 and j + 2 compute, and every rank
+        # probes the whole batch's packed words (seb_dev_probe_packed).
+        import dist_probe as dp
+
+        lo, hi, width = dp.spread_bounds(n, world, rank)
+        st.spread_keys = torch.from_numpy(kg.key16(kg.probe_indices(n)[lo:hi])).to(dev)
+        st.spread_kb = seb.dev_keys(st.spread_keys, n=hi - lo, stride=16)
+        st.workload += " as 8-B packed residues (each rank hashes its own 1/N)"
+        st.kernel_bytes["probe"] = 24.0 * (hi - lo) + 8.0 * n + nb + n
+        st.bcast_lead = 2
+        st.packed = [torch.zeros(width * world, dtype=torch.int64, device=dev) for _ in range(st.bcast_lead + 1)]
+        st.gather_bufs = st.packed
+        st.bcast_prologue = lambda b, part: seb.dev_pack_residues(st.spread_kb, m, k, part[:hi - lo])
+    elif packed:
         st.workload += " as 8-B packed residues (hashed once on rank 0)"
         st.kernel_bytes["probe"] = (16.0 * n + (8.0 * n if per_step else 0.0) if rank == 0 else 8.0 * n) + nb + n
         st.pmc_key = "c2c3_packed" if per_step else None  # rank 0 reports; it probes the keys unless per step
-    if per_step and packed:
+    if spread:
+        pass
+    elif per_step and packed:
         st.bcast_lead = 2
         st.packed = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(st.bcast_lead + 1)]
         st.broadcast_bufs = st.packed
@@ -207,7 +242,8 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
         dist.broadcast(st.resident, src=0)  # the north star's broadcast of the key batch over xGMI
         torch.cuda.synchronize()
         st.bcast_buf = st.resident
-    st.parallelism = (f"filter-per-gpu x{world}, probe batch broadcast (RCCL)" if world > 1
+    st.parallelism = (f"filter-per-gpu x{world}, probe batch all-gathered (RCCL)" if spread
+                      else f"filter-per-gpu x{world}, probe batch broadcast (RCCL)" if world > 1
                       else "filter-per-gpu x1")
 
     def build(j):
@@ -220,7 +256,10 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
 
     def probe(j, buf, target):
         w = st.wbufs[j % len(st.wbufs)]
-        if per_step and packed and rank == 0:  # answers batch j + 2's keys and emits its packed form
+        if spread:  # this rank's part of batch j + 2, then the whole of batch j
+            seb.dev_pack_residues(st.spread_kb, m, k, target[:st.spread_kb.n])
+            seb.dev_probe_packed(buf, n, w, m, k, st.out)
+        elif per_step and packed and rank == 0:  # answers batch j + 2's keys and emits its packed form
             seb.dev_probe_emit_packed(st.pk[0], w, m, k, st.out, target)
         elif per_step and packed:
             seb.dev_probe_packed(buf, n, w, m, k, st.out)
@@ -941,23 +980,35 @@ def main():
     records = rr.gather_records(dist, rec, world)
     report = rr.summarize(records, world, backend)
     value = st.units_per_step * args.steps / elapsed / 1e6
-    resident = None
-    if world > 1 and args.config in ("c2c3", "c5") and args.batch == "step" and not args.no_secondary:
-        # the same job with the batch broadcast once and resident during the steps
+    def variant(note, **over):
+        # the same job in another form, set up and timed in this process after the headline
         import copy
 
         a2 = copy.copy(args)
-        a2.batch = "resident"
+        for key, v in over.items():
+            setattr(a2, key, v)
         st2 = setup(a2, seb, kg, torch, dev, rank, world, dist)
         r2 = timed_run(a2, st2, seb, torch, dist, world, rank, dev)
         torch.cuda.synchronize()
-        resident = {"value": round(st2.units_per_step * a2.steps / r2["elapsed"] / 1e6, 2), "unit": st2.unit,
-                    "ms_per_step": round(r2["elapsed"] * 1000.0 / a2.steps, 4),
-                    "kernel_ms": {k: round(v, 4) for k, v in r2["kern_ms"].items()},
-                    "parity": st2.parity(a2.warmup + a2.steps - 1), "broadcast": r2["bcast"],
-                    "note": "secondary: one batch RCCL-broadcast before the timed steps and probed resident in "
-                            "every step (its broadcast timed on its own); the headline value broadcasts a new "
-                            "batch inside every step"}
+        out = {"value": round(st2.units_per_step * a2.steps / r2["elapsed"] / 1e6, 2), "unit": st2.unit,
+               "ms_per_step": round(r2["elapsed"] * 1000.0 / a2.steps, 4),
+               "kernel_ms": {k: round(v, 4) for k, v in r2["kern_ms"].items()},
+               "wait_ms": None if r2["wait_ms"] is None else round(r2["wait_ms"], 4),
+               "parity": st2.parity(a2.warmup + a2.steps - 1), "note": note}
+        if r2["bcast"]:
+            out["broadcast"] = r2["bcast"]
+        del st2
+        return out
+
+    resident = root_bcast = None
+    if world > 1 and args.config in ("c2c3", "c5") and args.batch == "step" and not args.no_secondary:
+        if args.config == "c2c3" and args.batch_origin == "spread" and args.bcast == "packed":
+            root_bcast = variant("secondary: a new batch in every step that arrives on rank 0 and is RCCL-broadcast "
+                                 "(8-B packed residues emitted by rank 0's probe); the headline's batch arrives "
+                                 "spread over the ranks and is all-gathered", batch_origin="root")
+        resident = variant("secondary: one batch RCCL-broadcast before the timed steps and probed resident in "
+                           "every step (its broadcast timed on its own); the headline value moves a new batch "
+                           "inside every step", batch="resident")
     result = None
     if rank == 0:
         kern = {name: (ms, st.kernel_bytes[name]) for name, ms in kern_ms.items()}
@@ -991,7 +1042,9 @@ def main():
                          "other": {d: {"ms": round(v[0], 4), "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 2)}
                                    for d, v in kern.items()}},
             "parity": parity,
+            **({"kernel_timing": run["kernel_timing"]} if run["kernel_timing"] else {}),
             **({"broadcast": bcast} if bcast else {}),
+            **({"root_broadcast": root_bcast} if root_bcast else {}),
             **({"resident_batch": resident} if resident else {}),
             "launch_timers": f"HIP events (no system fence) around build and probe on every {args.time_every}th "
                              "timed step and the last; ms_per_step is the wall clock of all steps",
@@ -1059,7 +1112,11 @@ def timed_run(args, st, seb, torch, dist, world, rank, dev):
     # batch j waits on the GPU (a stream wait, not the host) for that broadcast
     # (dist_probe.BroadcastPipeline; its ordering is tested on CPU in tests/test_dist.py).
     pipe = st.pipe
-    if pipe is None and st.broadcast_bufs is not None:
+    if pipe is None and st.gather_bufs is not None:
+        import dist_probe as dp
+
+        pipe = dp.AllGatherPipeline(st.gather_bufs, st.bcast_lead, rank, world, produce=st.bcast_prologue)
+    elif pipe is None and st.broadcast_bufs is not None:
         import dist_probe as dp
 
         pipe = dp.BroadcastPipeline(st.broadcast_bufs, st.bcast_lead, rank, produce=st.bcast_prologue)
@@ -1072,7 +1129,8 @@ def timed_run(args, st, seb, torch, dist, world, rank, dev):
     # probe (no broadcast to wait for, one stream) the build's end is the probe's start.
     shared = not overlap and pipe is None
     prev_end = [None]
-    pool = [seb.Timer() for _ in range(6 * args.steps + 1)]  # created before the timed region
+    reps = args.kernel_reps if pipe is None and args.kernel_reps > 0 else 0
+    pool = [seb.Timer() for _ in range(6 * (args.steps + reps) + 1)]  # created before the timed region
     waits, host_waits = [], []  # the compute stream's stall on the batch's transfer (GPU) / the host's wait
 
     def mark(stream):
@@ -1103,7 +1161,7 @@ def timed_run(args, st, seb, torch, dist, world, rank, dev):
         if record and pipe is not None:
             host_waits.append(time.perf_counter() - h0)
             waits.append((w0, mark(sp)))
-        target = pipe.root_target(j) if pipe is not None and rank == 0 and pipe.lead > 1 else None
+        target = pipe.target(j) if pipe is not None else None
         if record:
             p_start = b_end if shared and b_end is not None else \
                 (prev_end[0] if shared and prev_end[0] is not None else mark(sp))
@@ -1146,6 +1204,24 @@ def timed_run(args, st, seb, torch, dist, world, rank, dev):
 
     kern_ms = {(st.probe_name if name == "probe" else name): float(np.mean([a.elapsed_ms(b) for a, b in pairs]))
                for name, pairs in times.items() if pairs}
+    kernel_timing = None
+    if reps:
+        # SURVEY 8(d)'s protocol beside the sampled mean: every launch of `reps` further steps timed
+        # (after the wall clock stopped; an even count keeps the double buffers' parity)
+        reps += reps % 2
+        times = {"build": [], "probe": []}
+        prev_end[0] = None
+        for j in range(args.warmup + args.steps, args.warmup + args.steps + reps):
+            step(j, True)
+        torch.cuda.synchronize()
+        kernel_timing = {"reps": reps, "note": "every launch of further steps after the timed ones, HIP events on "
+                                               "the launch stream; the roofline uses the timed steps' sampled mean"}
+        for name, pairs in times.items():
+            if pairs:
+                v = [a.elapsed_ms(b) for a, b in pairs]
+                kernel_timing[st.probe_name if name == "probe" else name] = {
+                    "median_ms": round(float(np.median(v)), 4), "min_ms": round(float(min(v)), 4),
+                    "mean_ms": round(float(np.mean(v)), 4), "max_ms": round(float(max(v)), 4)}
     bcast = None
     if world > 1 and getattr(st, "bcast_buf", None) is not None:
         # the batch's broadcast, timed on its own (once per batch; the timed steps probe it resident)
@@ -1165,7 +1241,8 @@ def timed_run(args, st, seb, torch, dist, world, rank, dev):
                  "note": "RCCL broadcast of the probe batch from rank 0, once per batch, outside the timed steps"}
     wait = {"wait_ms": float(np.mean([a.elapsed_ms(b) for a, b in waits])) if waits else None,
             "wait_host_ms": float(np.mean(host_waits)) * 1e3 if host_waits else None}
-    return {"elapsed": elapsed, "elapsed_own": own, "kern_ms": kern_ms, "bcast": bcast, "overlap": overlap, **wait}
+    return {"elapsed": elapsed, "elapsed_own": own, "kern_ms": kern_ms, "bcast": bcast, "overlap": overlap,
+            "kernel_timing": kernel_timing, **wait}
 
 
 SECONDARY = (("c4", ["--steps", "10", "--warmup", "3"]),

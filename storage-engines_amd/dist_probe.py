@@ -6,7 +6,8 @@ every SSTable filter of the node at once (BASELINE config C5):
 
   * filters are sharded contiguously over ranks (filter f lives on rank f * world // F ... see
     `FilterShard`); each GPU holds its filters' bit arrays in HBM;
-  * the key batch is RCCL-broadcast from the root over xGMI (`broadcast_keys`);
+  * the key batch is RCCL-broadcast from the root over xGMI (`broadcast_keys`), or, when it
+    arrives spread over the ranks, replicated by an all-gather (`AllGatherPipeline`);
   * each rank runs the multi-filter probe kernel over its filters (`probe_fn`), producing a mask
     plane whose bit j = local filter j's MayContain answer;
   * planes are all-gathered and assembled into one u64 mask per key, bit f = filter f's answer
@@ -200,6 +201,85 @@ class BroadcastPipeline:
         for b in sorted(self.handles):
             self._wait(b)
 
+    def target(self, j: int) -> torch.Tensor | None:
+        """What this rank writes during step j: rank 0's buffer for batch j + lead (lead > 1)."""
+        return self.root_target(j) if self.rank == 0 and self.lead > 1 else None
+
+
+def spread_bounds(n: int, world: int, rank: int) -> tuple[int, int, int]:
+    """Rank `rank`'s part of an n-key batch that arrives spread over the ranks: keys [lo, hi) of
+    equal slices of width ceil(n / world) (the last one shorter), and that width."""
+    c = -(-n // world)
+    lo = min(n, rank * c)
+    return lo, min(n, lo + c), c
+
+
+class AllGatherPipeline:
+    """Probe batches that arrive spread over the ranks (rank r holds keys [lo_r, hi_r) of every
+    batch, `spread_bounds`), replicated to every rank by an all-gather over xGMI ahead of the step
+    that probes them (bench.py c2c3 at N > 1, --batch-origin spread).
+
+    A root broadcast sends the whole batch out of one GPU: at N = 2 one xGMI link carries all of
+    it in one direction.  Here every rank contributes 1/N of the batch (its own packed residues),
+    so each link carries 1/N of the bytes and both directions work; every rank then probes the
+    whole batch.  `bufs` holds lead + 1 tensors of world * width elements; batch b lives in
+    bufs[b % (lead + 1)] and rank r's part of it in slice r (`target`).  During step j every rank
+    writes its part of batch j + lead into `target(j)` and `end_step(j)` issues the all-gather on
+    the communication stream.  `acquire(j)` waits for batch j's all-gather; waits are in batch
+    order, so by then the all-gather of batch j - 1, which last wrote the buffer that batch
+    j + lead overwrites, is done too.  `produce(b, part)` fills this rank's part of batch b < lead
+    in `prologue`.  nccl gathers in place (`all_gather_into_tensor`); gloo (rehearsals, CPU tests)
+    uses the list form over views of the buffer.
+    """
+
+    def __init__(self, bufs: Sequence[torch.Tensor], lead: int, rank: int, world: int, group=None,
+                 produce: Callable[[int, torch.Tensor], None] | None = None):
+        if lead < 1 or len(bufs) != lead + 1:
+            raise ValueError("need lead >= 1 and lead + 1 buffers")
+        if any(b.numel() % world for b in bufs):
+            raise ValueError("each buffer must hold world equal slices")
+        self.bufs, self.lead, self.rank, self.world = list(bufs), lead, rank, world
+        self.group, self.produce = group, produce
+        self.width = self.bufs[0].numel() // world
+        self.handles: dict[int, object] = {}
+        self.in_place = dist.get_backend(group) == "nccl"
+
+    def _part(self, buf: torch.Tensor) -> torch.Tensor:
+        return buf[self.rank * self.width:(self.rank + 1) * self.width]
+
+    def _gather(self, b: int) -> None:
+        buf = self.bufs[b % len(self.bufs)]
+        if self.in_place:
+            self.handles[b] = dist.all_gather_into_tensor(buf, self._part(buf), group=self.group, async_op=True)
+        else:
+            self.handles[b] = dist.all_gather(list(buf.chunk(self.world)), self._part(buf).clone(),
+                                              group=self.group, async_op=True)
+
+    def _wait(self, b: int) -> None:
+        h = self.handles.pop(b, None)
+        if h is not None:
+            h.wait()
+
+    def prologue(self) -> None:
+        for b in range(self.lead):
+            if self.produce is not None:
+                self.produce(b, self._part(self.bufs[b % len(self.bufs)]))
+            self._gather(b)
+
+    def acquire(self, j: int) -> torch.Tensor:
+        self._wait(j)
+        return self.bufs[j % len(self.bufs)]
+
+    def target(self, j: int) -> torch.Tensor:
+        """This rank's part of batch j + lead, written during step j."""
+        return self._part(self.bufs[(j + self.lead) % len(self.bufs)])
+
+    def end_step(self, j: int) -> None:
+        self._gather(j + self.lead)
+
+    def drain(self) -> None:
+        for b in sorted(self.handles):
+            self._wait(b)
 
 
 # ------------------------------------------------ C5 as a key x filter grid (--config c5_2d) ----
@@ -442,6 +522,9 @@ class GridPipeline:
 
     def root_target(self, j: int) -> torch.Tensor:
         return self._buf(j + self.lead)
+
+    def target(self, j: int) -> torch.Tensor | None:
+        return self.root_target(j) if self.ex.rank == 0 else None
 
     def end_step(self, j: int) -> None:
         b = j + self.lead

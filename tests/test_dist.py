@@ -172,6 +172,54 @@ def test_broadcast_pipeline_delivers_each_batch_in_order(world, lead):
             assert np.array_equal(got, want), (r, j)
 
 
+def _allgather_worker(rank, world, port, steps, n, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lead = 2
+        lo, hi, width = dp.spread_bounds(n, world, rank)
+        bufs = [torch.zeros(width * world, dtype=torch.int64) for _ in range(lead + 1)]
+        batches = {b: _batch(b, n) for b in range(steps + lead)}
+        pipe = dp.AllGatherPipeline(bufs, lead, rank, world,
+                                    produce=lambda b, part: part[:hi - lo].copy_(batches[b][lo:hi]))
+        pipe.prologue()
+        seen = []
+        for j in range(steps):
+            buf = pipe.acquire(j)
+            pipe.target(j)[:hi - lo].copy_(batches[j + lead][lo:hi])  # the bench packs its part of batch j+2 here
+            seen.append(buf[:n].clone())
+            pipe.end_step(j)
+        pipe.drain()
+        q.put((rank, [s.numpy() for s in seen]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 64), (3, 64), (3, 65)])
+def test_allgather_pipeline_delivers_each_batch_in_order(world, n):
+    """bench.py's default N>1 batch path (dist_probe.AllGatherPipeline, --batch-origin spread): each
+    rank writes only its part of batch j + 2 while the all-gathers of batches j + 1 and j + 2's
+    buffers' previous contents may be in flight, and every rank must see the whole of batch j at
+    step j (ragged parts when world does not divide n)."""
+    assert dp.spread_bounds(65, 3, 2) == (44, 65, 22) and dp.spread_bounds(2, 3, 2) == (2, 2, 1)
+    steps = 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_allgather_worker, args=(r, world, port, steps, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert len(results[r]) == steps
+        for j, got in enumerate(results[r]):
+            assert np.array_equal(got, _batch(j, n).numpy()), (r, j)
+
+
 # ------------------------------------------- sharded build of one filter (dist_build) ----
 
 def _oracle_build_fn(keys, words: torch.Tensor, m: int, k: int) -> None:

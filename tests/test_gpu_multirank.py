@@ -7,7 +7,9 @@ transfer through host memory); only `parity` is asserted.
     planes gathered to rank 0; its resident_batch secondary broadcasts the batch once;
   * c5_2d (dist_probe.KeyFilterGrid): key groups x filter slots, shards sent and planes returned
     in one exchange per step (the collective transport under gloo);
-  * c2c3 (the headline): a filter per rank, a new packed batch broadcast in every step.
+  * c2c3 (the headline): a filter per rank, a new packed batch in every step, spread over the
+    ranks and all-gathered (default), or broadcast from rank 0 (its root_broadcast secondary and
+    --batch-origin root); the resident_batch secondary broadcasts one batch once.
 """
 import json
 import os
@@ -57,8 +59,17 @@ def test_c5_2d_grid_two_ranks(groups):
     assert f"key groups {groups}" in d["config"]["parallelism"]
 
 
-def test_c2c3_broadcast_per_step_two_ranks():
-    d = _bench("--config", "c2c3", "--no-secondary")
+def test_c2c3_spread_batch_per_step_two_ranks():
+    d = _bench("--config", "c2c3")
     assert d["n_gpus"] == 2
     assert d["parity"].startswith("bit-exact"), d["parity"]
-    assert "in every step" in d["config"]["workload"]
+    assert "all-gather" in d["config"]["workload"] and "all-gathered" in d["config"]["parallelism"]
+    assert d["root_broadcast"]["parity"].startswith("bit-exact"), d["root_broadcast"]
+    assert d["resident_batch"]["parity"].startswith("bit-exact"), d["resident_batch"]
+
+
+def test_c2c3_broadcast_per_step_two_ranks():
+    d = _bench("--config", "c2c3", "--batch-origin", "root", "--no-secondary")
+    assert d["n_gpus"] == 2
+    assert d["parity"].startswith("bit-exact"), d["parity"]
+    assert "RCCL-broadcast from rank 0 in every step" in d["config"]["workload"]

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Multi-rank rehearsal on the one-GPU box: N ranks (default 4), all on cuda:0, gloo instead of
 # RCCL (RCCL refuses two ranks on one device).  Checks the N > 1 code paths (broadcast pipeline,
-# sharded filters, mask-plane gather, the key x filter grid, sharded build, partitioned probe) for parity; the times mean
+# all-gather pipeline, sharded filters, mask-plane gather, the key x filter grid, sharded build, partitioned probe) for parity; the times mean
 # nothing.  Usage: tools/gpu_rehearse.sh [N].  Writes gpurun_out/rehearse_N_<config>.json.
 set -e
 N=${1:-4}
@@ -9,7 +9,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
 port=29611
-for cfg in "c2c3 --bcast packed" "c2c3 --bcast keys" "c5" "c5_2d" "c5_2d --c5-groups 2" "c2_sharded" "c3_partitioned"; do
+for cfg in "c2c3" "c2c3 --batch-origin root" "c2c3 --bcast keys" "c5" "c5_2d" "c5_2d --c5-groups 2" "c2_sharded" "c3_partitioned"; do
     tag=$(echo "$cfg" | tr ' ' '_' | tr -d '-')
     port=$((port + 1))
     timeout -k 10 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" --master-addr 127.0.0.1 \
@@ -18,7 +18,8 @@ for cfg in "c2c3 --bcast packed" "c2c3 --bcast keys" "c5" "c5_2d" "c5_2d --c5-gr
     python3 -c "
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print(sys.argv[2], d['n_gpus'], d['parity'], d.get('resident_batch', {}).get('parity', ''))
+print(sys.argv[2], d['n_gpus'], d['parity'], d.get('root_broadcast', {}).get('parity', ''),
+      d.get('resident_batch', {}).get('parity', ''))
 print('   devices', d['devices'], 'rank_check', d['rank_check'])
 for r in d['per_rank']:
     print('   rank', r['rank'], r['device']['pci'], r['backend'], 'world', r['world_size'], 'ones', r['allreduce_ones'],
