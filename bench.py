@@ -217,6 +217,7 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
         st.spread_kb = seb.dev_keys(st.spread_keys, n=hi - lo, stride=16)
         st.workload += " as 8-B packed residues (each rank hashes its own 1/N)"
         st.kernel_bytes["probe"] = 24.0 * (hi - lo) + 8.0 * n + nb + n
+        st.pmc_key = "c2c3_spread"  # its own kernels (pack + packed probe): no c2c3 PMC entry applies
         st.bcast_lead = 2
         st.packed = [torch.zeros(width * world, dtype=torch.int64, device=dev) for _ in range(st.bcast_lead + 1)]
         st.gather_bufs = st.packed

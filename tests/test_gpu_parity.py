@@ -1876,6 +1876,27 @@ def test_sharded_build_nccl_one_rank(seb, golden, torch_cuda):
             dist.broadcast(b, src=0, async_op=True).wait()
             torch.cuda.synchronize()
             assert torch.equal(b, torch.arange(64, device="cuda").to(dt))
+        # bench c2c3's default N > 1 batch path: the in-place all-gather of each rank's packed part
+        # (dist_probe.AllGatherPipeline on RCCL), a different batch every step
+        nb_, steps, lead = 10_000, 5, 2
+        mp_, kp_ = seb.params(nb_, 0.01)
+        kbs = [seb.dev_keys(to_dev(torch, kg.key16(b * nb_ + np.arange(nb_))), n=nb_, stride=16)
+               for b in range(steps + lead)]
+        want = []
+        for kb in kbs:
+            w_ = torch.zeros(nb_, dtype=torch.int64, device="cuda")
+            seb.dev_pack_residues(kb, mp_, kp_, w_)
+            want.append(w_)
+        bufs = [torch.zeros(nb_, dtype=torch.int64, device="cuda") for _ in range(lead + 1)]
+        pipe = dp.AllGatherPipeline(bufs, lead, 0, 1, produce=lambda b, part: seb.dev_pack_residues(kbs[b], mp_, kp_, part))
+        assert pipe.in_place
+        pipe.prologue()
+        for j in range(steps):
+            buf = pipe.acquire(j)
+            seb.dev_pack_residues(kbs[j + lead], mp_, kp_, pipe.target(j))
+            assert torch.equal(buf, want[j]), j
+            pipe.end_step(j)
+        pipe.drain()
     finally:
         dist.destroy_process_group()
     row = next(r for r in golden["fixed16"] if r["n"] == 10_000_000)
