@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 5 checkpoint at HEAD: the whole GPU suite, smoke(), then the default bench line (with its
+# Checkpoint at HEAD: the whole GPU suite, smoke(), then the default bench line (with its
 # CPU baseline legs and secondary lines).
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
-OUT=gpurun_out/${TAG:-r5h}
+OUT=gpurun_out/${TAG:-checkpoint}
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > $OUT/tests.log 2>&1 \
     || { tail -40 $OUT/tests.log; exit 1; }

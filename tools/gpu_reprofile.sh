@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 5 re-profile at HEAD: kernel trace + PMC passes per config, through
-# tools/gpu_profile.sh.  Usage: tools/gpu_r5_prof.sh CONFIG... (c2c3 c4 c5 lsm lsm_wide)
+# Re-profile at HEAD: kernel trace + PMC passes per config, through
+# tools/gpu_profile.sh.  Usage: tools/gpu_reprofile.sh CONFIG... (c2c3 c4 c5 lsm lsm_wide)
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
 for cfg in "$@"; do
