@@ -4,6 +4,6 @@
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
 for cfg in "$@"; do
-  bash tools/gpu_profile.sh r05_$cfg --config $cfg --steps 10 --warmup 3 --no-cpu-baseline --no-host-inclusive \
+  bash tools/gpu_profile.sh ${PREFIX:-r05}_$cfg --config $cfg --steps 10 --warmup 3 --no-cpu-baseline --no-host-inclusive \
       --no-secondary || exit 1
 done
