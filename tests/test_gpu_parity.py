@@ -1439,11 +1439,13 @@ def test_registry_l0_group_table(seb, torch_cuda):
         reg.close()
 
 
-def test_registry_key_range_order_wide_partition_level(seb, torch_cuda):
+@pytest.mark.parametrize("parts", [1020, 255, 256])
+def test_registry_key_range_order_wide_partition_level(seb, torch_cuda, parts):
     """Key-range order over a partition level of 1020 files (1021 buckets, near kMgMaxBuckets =
     1025: the block scans run 4 buckets per thread), with an L1 of 60 files over it and two L0
     files, on a 300K-key batch with keys below, between and above the files: the list rows equal
-    the batch-order walk's and, on a sample, the Python model of LSM.Get's walk."""
+    the batch-order walk's and, on a sample, the Python model of LSM.Get's walk.  255 and 256
+    files straddle the bucket ids' switch from u8 (at most 256 buckets, ids up to 255) to u16."""
     torch = torch_cuda
     rng = np.random.default_rng(61)
     reg = seb.Registry(0)
@@ -1460,10 +1462,10 @@ def test_registry_key_range_order_wide_partition_level(seb, torch_cuda):
     universe = [kg.key16_bytes(int(i)) for i in range(10_000, 10_000 + 2 * 40_800, 2)]  # sorted
     for f in range(2):
         add(10 + f, 0, sorted(rng.choice(universe, 500, replace=False).tolist()))
-    for lvl, parts in ((1, 60), (2, 1020)):
-        chunks = np.array_split(np.array(universe, dtype=object), parts)
-        for j in rng.permutation(parts):
-            add(1000 * lvl + int(j), lvl, list(chunks[j])[::2])
+    for lvl, nparts in ((1, 60), (2, parts)):
+        chunks = np.array_split(np.array(universe, dtype=object), nparts)
+        for j in rng.permutation(nparts):
+            add(10_000 * lvl + int(j), lvl, list(chunks[j])[::2])
     assert reg.max_candidates() == 4
     n = 300_000
     pk = kg.key16(rng.integers(0, 100_000, n))
