@@ -67,44 +67,49 @@ struct Funnel {
     }
 };
 
-// One FNV chain (A: FNV-1a = hash1, else FNV-1 = hash2) in FnvSplit's form, for the split tail
-// waves of k_hash_varlen: the same bits as the matching half of FnvSplit / fnv_word_part.
-template <bool A>
+// One FNV chain in FnvSplit's form, for the tail waves of k_hash_varlen: FNV-1a's recurrence (xor the
+// byte, then multiply) from state (lo, acc), the same bits as the matching half of FnvSplit.
 struct FnvOne {
-    uint32_t lo = (uint32_t)kFnvOffset;
-    uint64_t acc = kFnvOffset >> 32;
+    uint32_t lo;
+    uint64_t acc;
+    __device__ __forceinline__ explicit FnvOne(uint64_t s) : lo((uint32_t)s), acc(s >> 32) {}
     __device__ __forceinline__ void word(uint32_t w) {
         uint32_t d[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t x = A ? xor_byte(lo, w, j) : lo;
+            const uint32_t x = xor_byte(lo, w, j);
             const uint64_t p = (uint64_t)x * 435u;
             d[j] = (uint32_t)(p >> 32) + (x << 8);
-            lo = A ? (uint32_t)p : xor_byte((uint32_t)p, w, j);
+            lo = (uint32_t)p;
         }
         const uint64_t t = mad_lo(d[0], pow435(3), mad_lo(d[1], pow435(2), mad_lo(d[2], 435u, d[3])));
         acc = mad_lo((uint32_t)acc, pow435(4), t);
     }
-    // bytes [0, r) of w (r < 4) with the plain 64-bit step; returns the chain's hash
+    // bytes [0, r) of w (r < 4) with the plain 64-bit step; returns the chain's state
     __device__ __forceinline__ uint64_t finish(uint32_t w, uint32_t r) const {
         uint64_t h = (acc << 32) | lo;
 #pragma unroll
         for (uint32_t j = 0; j < 3; ++j) {
-            const uint64_t b = (w >> (8 * j)) & 0xffu;
-            const uint64_t nh = A ? (h ^ b) * kFnvPrime : (h * kFnvPrime) ^ b;
+            const uint64_t nh = (h ^ ((w >> (8 * j)) & 0xffu)) * kFnvPrime;
             h = j < r ? nh : h;
         }
         return h;
     }
 };
 
-template <bool A>
-__device__ __forceinline__ uint64_t funnel_one(const uint32_t *lds, uint32_t b, uint32_t n) {
+// One chain of a key staged in LDS at byte b, n bytes: FNV-1a (fnv1 false) or FNV-1 (true), both
+// walked by FNV-1a's recurrence, so the lanes of one wave can run either with the same instructions.
+// FNV-1 is s_j = s_{j-1} * P ^ b_{j-1} from s_0 = O; t_j = s_j * P then follows t_j = (t_{j-1} ^
+// b_{j-1}) * P from t_0 = O * P, and s_n = t_{n-1} ^ b_{n-1}: FNV-1a's recurrence from O * P over the
+// first n - 1 bytes, the last byte xored in after (an empty key keeps O).
+__device__ __forceinline__ uint64_t funnel_chain(const uint32_t *lds, uint32_t b, uint32_t n, bool fnv1) {
+    const bool shifted = fnv1 && n > 0;
+    const uint32_t len = shifted ? n - 1 : n;
     uint32_t wi = b >> 2;
     const uint32_t sh = b & 3u;
     uint32_t cur = lds[wi], nxt = lds[wi + 1];
-    FnvOne<A> f;
-    const uint32_t nw = n >> 2;
+    FnvOne f(shifted ? kFnvOffset * kFnvPrime : kFnvOffset);
+    const uint32_t nw = len >> 2;
     for (uint32_t j = 0; j + 2 <= nw; j += 2) {  // read ahead and two words per step, as Funnel::walk
         const uint32_t a1 = lds[wi + 2], a2 = lds[wi + 3];
         wi += 2;
@@ -119,7 +124,12 @@ __device__ __forceinline__ uint64_t funnel_one(const uint32_t *lds, uint32_t b, 
         cur = nxt;
         nxt = ahead;
     }
-    return f.finish(__builtin_amdgcn_alignbyte(nxt, cur, sh), n & 3u);
+    uint64_t h = f.finish(__builtin_amdgcn_alignbyte(nxt, cur, sh), len & 3u);
+    if (shifted) {
+        const uint32_t p = b + n - 1;
+        h ^= (lds[p >> 2] >> (8 * (p & 3u))) & 0xffu;
+    }
+    return h;
 }
 
 // A workgroup owns KEYS consecutive keys and an LDS window of WIN bytes per key (C4 keys average
@@ -140,9 +150,12 @@ __device__ __forceinline__ void put_hash(void *out, uint64_t i, uint64_t h1, uin
 
 // NS > 0 (KEYS = 512 - 64 * NS, 512 threads): a full workgroup's 64 * NS longest keys (the last
 // slots of the length order, which otherwise set the workgroup's lifetime and hold its LDS after
-// the other waves are done) are hashed by the last 2 * NS waves, a pair per 64 keys, one wave per
-// FNV chain: each runs half the instructions.  The FNV-1 wave hands its hashes to the FNV-1a
-// wave through LDS for the packed output; the 16-B output is written in halves.
+// the other waves are done) are hashed by the last 2 * NS waves, 32 keys per wave, the longest 32
+// on the first: lane l < 32 runs key l's FNV-1a chain and lane l + 32 its FNV-1 chain (funnel_chain:
+// one instruction stream for both), so each runs half the instructions and a wave lasts as long as
+// its own 32 keys' longest (round 4 paired the 64 keys' chains over two waves, each as long as the
+// longest of all 64).  Lane l takes lane l + 32's hash by a lane shuffle for the packed output; the
+// 16-B output is written in halves.
 // P0 (with PACK): the compacted phased probe's phase 0 fused in (k_probe_c0's job for a pre-hashed
 // batch): the packed words go to LDS in key order, then each wave takes one group of 64 keys,
 // tests the positions in range 0 [0, p0.hi) and stores the live keys' words compacted in the
@@ -193,8 +206,6 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
     __shared__ uint32_t cur[kLenBuckets];
     __shared__ uint32_t slot_key[KEYS];  // sorted slot -> start byte in the window << 16 | length
     __shared__ uint16_t slot_idx[KEYS];  // sorted slot -> key within the workgroup
-    __shared__ uint64_t xh2[NS ? 64 * NS : 1];  // the FNV-1 waves' hashes for the FNV-1a waves
-    __shared__ uint32_t xflag[NS ? NS : 1];
     const uint32_t t = threadIdx.x;
     const uint64_t k0 = (uint64_t)blockIdx.x * KEYS;
     const uint64_t k1 = k0 + KEYS < n ? k0 + KEYS : n;
@@ -230,7 +241,6 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
         return;
     }
     if (t < kLenBuckets) cur[t] = 0u;
-    if (t < NS) xflag[t] = 0u;
     {  // the span, 4 chunks per thread per batch: every load issued before any LDS store (a load-store
        // pair per chunk waited for every load), through a pointer that keeps the kernel argument's
        // global address space (a uintptr_t round trip made these flat loads); clamped chunk indices
@@ -282,32 +292,20 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
     const uint32_t *lds = (const uint32_t *)stage;
     bool tail = false;
     if constexpr (NS > 0) {
-        if (cnt == KEYS && t >= KEYS - 64 * NS) {  // the longest keys: a wave pair per 64, one per chain
+        if (cnt == KEYS && t >= KEYS - 64 * NS) {  // the longest keys: 32 per wave, a lane per chain
             tail = true;
-            const uint32_t w = (t - (KEYS - 64 * NS)) >> 6, c = w >> 1, lane = t & 63;
-            const uint32_t q = KEYS - 64 * NS + 64 * c + lane;
+            const uint32_t w = (t - (KEYS - 64 * NS)) >> 6, lane = t & 63, half = lane >> 5;
+            const uint32_t q = KEYS - 32 * (w + 1) + (lane & 31);  // wave 0: the longest 32 slots
             const uint32_t sk = slot_key[q];
             const uint32_t j = slot_idx[q];
-            if ((w & 1u) == 0u) {  // FNV-1a (hash1)
-                const uint64_t h1 = funnel_one<true>(lds, sk >> 16, sk & 0xffffu);
-                if constexpr (PACK) {
-                    while (__hip_atomic_load(&xflag[c], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-                        __builtin_amdgcn_s_sleep(1);
-                    emit(j, h1, xh2[64 * c + lane]);
-                } else {
-                    ((uint2 *)hashes)[2 * (k0 + j)] = make_uint2((uint32_t)h1, (uint32_t)(h1 >> 32));
-                }
-            } else {  // FNV-1 (hash2)
-                const uint64_t h2 = funnel_one<false>(lds, sk >> 16, sk & 0xffffu);
-                if constexpr (PACK) {
-                    xh2[64 * c + lane] = h2;
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __builtin_amdgcn_wave_barrier();
-                    if (lane == 0)
-                        __hip_atomic_store(&xflag[c], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                } else {
-                    ((uint2 *)hashes)[2 * (k0 + j) + 1] = make_uint2((uint32_t)h2, (uint32_t)(h2 >> 32));
-                }
+            const uint64_t h = funnel_chain(lds, sk >> 16, sk & 0xffffu, half != 0);
+            // lane l < 32 (FNV-1a, hash1) takes lane l + 32's FNV-1 (hash2)
+            const uint32_t h2lo = (uint32_t)__shfl((int)(uint32_t)h, (int)(lane | 32u), 64);
+            const uint32_t h2hi = (uint32_t)__shfl((int)(uint32_t)(h >> 32), (int)(lane | 32u), 64);
+            if constexpr (PACK) {
+                if (half == 0) emit(j, h, (uint64_t)h2hi << 32 | h2lo);
+            } else {
+                ((uint2 *)hashes)[2 * (k0 + j) + half] = make_uint2((uint32_t)h, (uint32_t)(h >> 32));
             }
             if constexpr (!P0) return;
         }
