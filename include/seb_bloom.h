@@ -104,8 +104,9 @@ int seb_abi_version(void);
  *                     the (key-range ordered) batch, so each XCD's L2 holds its own stretch's filters
  *                     (1, default), or blocks walk the batch in launch order (0)
  *   "varlen_prehash_min_keys"  variable-length batches of this many keys are pre-hashed in LDS
- *   "varlen_tail"     pre-hash: the 64 longest keys of a workgroup run on two waves, one per FNV
- *                     chain (1, default), or one key per lane like the others (0)
+ *   "varlen_tail"     pre-hash: v = 1 (default), 2, 3: workgroups of 512 - 64 v keys whose 64 v longest
+ *                     keys run on 2 v waves of 32 keys, one lane per FNV chain; 0: 448 keys, one key per
+ *                     lane throughout
  *   "grid_cap"        maximum workgroups of the grid-stride kernels
  *   "workspace_limit_mib"  cap on library scratch and a context's build scratch (0 = none); a
  *                     request above it fails with SEB_ERR_NOMEM (MultiGet's key-range order then

@@ -162,7 +162,7 @@ static const OptionDesc kOptions[] = {
     SEB_OPT(scatter_bins, 0, 1),
     SEB_OPT(grid_cap, 1, 1 << 30),
     SEB_OPT(workspace_limit_mib, 0, 1 << 30),
-    SEB_OPT(varlen_tail, 0, 1),
+    SEB_OPT(varlen_tail, 0, 3),
     SEB_OPT(cpu_fallback, 0, 1),
     SEB_OPT(fault_inject, 0, 2),
 };

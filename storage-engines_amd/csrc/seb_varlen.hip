@@ -322,23 +322,31 @@ __global__ __launch_bounds__(KEYS + 64 * NS) void k_hash_varlen(const uint8_t *_
     if constexpr (P0) varlen_phase0<KEYS>((uint64_t *)stage, has, my_j, my_pw, k0, cnt, md, p0);
 }
 
-// 448 keys per workgroup, a 64-B window per key, the top 64 split over two chain waves
-// (varlen_tail 1, default: 512 threads) or hashed one per lane like the rest (0: 448 threads).
+// 512 threads per workgroup, 512 - 64 v keys of which the 64 v longest run on 2 v tail waves
+// (varlen_tail v = 1, default: 448 keys; 2: 384; 3: 320), a 64-B window per key; or 448 keys hashed one
+// per lane (0: 448 threads).
 // 256/384/512/1024-key workgroups, 48-80-B windows, no chain waves and two
 // ways of giving the chain waves' lanes more keys measured slower.
 constexpr uint32_t kVarKeys = 448, kVarWin = 64;
+
+template <bool PACK, bool P0, uint32_t NS>
+static void launch_hash_varlen_ns(const KeyBatch &kb, void *out, const ModArg &md, hipStream_t s, Phase0Arg p0) {
+    constexpr uint32_t keys = NS ? 512 - 64 * NS : kVarKeys;
+    const uint64_t ntiles = (kb.n + keys - 1) / keys;
+    hipLaunchKernelGGL((k_hash_varlen<keys, kVarWin, PACK, NS, P0>), dim3((unsigned)ntiles), dim3(keys + 64 * NS), 0,
+                       s, kb.data, kb.offsets, kb.n, out, md, p0);
+}
 
 template <bool PACK, bool P0 = false>
 static hipError_t launch_hash_varlen_any(const KeyBatch &kb, void *out, const ModArg &md, hipStream_t s,
                                         Phase0Arg p0 = {}) {
     if (!kb.offsets || kb.n == 0) return hipSuccess;
-    const uint64_t ntiles = (kb.n + kVarKeys - 1) / kVarKeys;
-    if (options().varlen_tail == 0)
-        hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, 0, P0>), dim3((unsigned)ntiles), dim3(kVarKeys), 0,
-                           s, kb.data, kb.offsets, kb.n, out, md, p0);
-    else
-        hipLaunchKernelGGL((k_hash_varlen<kVarKeys, kVarWin, PACK, 1, P0>), dim3((unsigned)ntiles),
-                           dim3(kVarKeys + 64), 0, s, kb.data, kb.offsets, kb.n, out, md, p0);
+    switch (options().varlen_tail) {
+    case 0: launch_hash_varlen_ns<PACK, P0, 0>(kb, out, md, s, p0); break;
+    case 2: launch_hash_varlen_ns<PACK, P0, 2>(kb, out, md, s, p0); break;
+    case 3: launch_hash_varlen_ns<PACK, P0, 3>(kb, out, md, s, p0); break;
+    default: launch_hash_varlen_ns<PACK, P0, 1>(kb, out, md, s, p0); break;
+    }
     return hipGetLastError();
 }
 

@@ -474,13 +474,14 @@ def test_c4_varlen_device(seb, golden, torch_cuda, n, build_algo):
     assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
 
 
-@pytest.mark.parametrize("tail", [0, 1])
+@pytest.mark.parametrize("tail", [0, 1, 2, 3])
 @pytest.mark.parametrize("algo", [0, 2])
 def test_c4_prehash_golden(seb, golden, torch_cuda, algo, tail):
     """C4's zipf lengths (the spans fit the LDS window, so the sorted and split-chain hashing
     paths run rather than the overflow fallback), pre-hashed to 16-B hashes (LDS-resident build,
     unphased probe) and to packed residues (bucketed build), reproduce the C4 golden digests;
-    with the 64 longest keys of a workgroup on two chain waves (varlen_tail 1) and without (0)."""
+    with the 64 v longest keys of a workgroup on 2 v tail waves, a lane per chain (varlen_tail v =
+    1, 2, 3), and without (0)."""
     torch = torch_cuda
     n = 100000
     row = next(r for r in golden["varlen"] if r["n"] == n)
@@ -495,6 +496,31 @@ def test_c4_prehash_golden(seb, golden, torch_cuda, algo, tail):
         seb.dev_probe(seb.dev_keys(to_dev(torch, pdata), to_dev(torch, poff)), words, m, k, out)
         torch.cuda.synchronize()
         assert sha(out.cpu().numpy().tobytes()) == row["probe_sha256"]
+
+
+@pytest.mark.parametrize("tail", [0, 1, 2, 3])
+def test_varlen_prehash_tiny_keys(seb, torch_cuda, tail):
+    """Batches of only empty and 1-3-byte keys, so the tail waves' keys (a workgroup's longest) are
+    empty or shorter than a word: FNV-1 of an empty key is the offset basis, and a 1-byte key's
+    FNV-1 is the basis times the prime xor its byte (the tail lanes run FNV-1 as FNV-1a's recurrence
+    over n - 1 bytes); a batch of all-empty keys too."""
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    for lens in (rng.choice([0, 1, 2, 3], size=5000, p=[0.4, 0.3, 0.2, 0.1]), np.zeros(3000, np.int64)):
+        n = lens.size
+        off = np.zeros(n + 1, np.uint64)
+        np.cumsum(lens, out=off[1:])
+        data = rng.integers(0, 256, max(int(off[-1]), 1), dtype=np.uint8)[: int(off[-1])]
+        m, k = oc.params(n, 0.01)
+        ref = oc.build(m, k, data, n, offsets=off)
+        with seb.option("varlen_prehash_min_keys", 0), seb.option("varlen_tail", tail):
+            kd = seb.dev_keys(to_dev(torch, np.concatenate([data, np.zeros(16, np.uint8)])), to_dev(torch, off))
+            words, bits = dev_build_bits(seb, torch, kd, m, k)
+            assert np.array_equal(bits, ref)
+            out = torch.empty(n, dtype=torch.uint8, device="cuda")
+            seb.dev_probe(kd, words, m, k, out)
+            torch.cuda.synchronize()
+            assert bool(out.all())
 
 
 @pytest.mark.parametrize("prehash_min", [0, 1 << 40], ids=["prehash", "direct"])
@@ -525,10 +551,10 @@ def test_varlen_processing_order_invisible(seb, torch_cuda, prehash_min, build_a
 
 
 @pytest.mark.parametrize("packed", [0, 1], ids=["small_filter", "packed_paths"])
-@pytest.mark.parametrize("tail", [0, 1])
+@pytest.mark.parametrize("tail", [0, 1, 2, 3])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_varlen_prehash_edge_lengths(seb, torch_cuda, seed, tail, packed):
-    """The pre-hash (448-key workgroups, 64-B window per key, with and without the split-chain tail
+    """The pre-hash (448/384/320-key workgroups, 64-B window per key, with and without the tail
     waves) hashes like the oracle over lengths that mix empty, sub-word, bucket-edge, 48/49-B and
     window-overflowing keys, and a ragged last workgroup; the answers of a half-present batch
     equal the oracle's key by key; with a two-range filter and the bucketed build as well, so the
