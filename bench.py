@@ -11,13 +11,16 @@ words written whole by seb_dev_build_fresh, no separate clear; --fresh-build 0: 
 from 10M x 16-B keys @1% FPR (BASELINE C2; m = 95,850,584, k = 7) and probe a 10M-key batch
 against it (C3, 50% present).  Rank g builds the filter of its own SSTable (keys key16(g*n + i));
 every rank probes every key of a new batch in every step.  Since every rank's filter has the same
-(m, k), the batch travels as 8-byte packed residues.  By default (--batch-origin spread) each batch
+(m, k), the batch travels as 8-byte packed residues.  By default (--batch-origin root, the north
+star's form) each batch arrives on rank 0 and is RCCL-broadcast over xGMI, its packed words
+emitted by rank 0's own probe (--bcast keys sends the 16-B keys); --batch-origin spread: it
 arrives spread over the ranks, 1/N per GPU, each rank packs its part and an RCCL all-gather
-replicates the whole batch ahead of the step that probes it, so the transfer overlaps compute
-and every xGMI link carries 1/N of the batch; --batch-origin root: the batch arrives on rank 0
-and is RCCL-broadcast (its packed words emitted by rank 0's own probe; --bcast keys sends the
-16-B keys), also measured on the default line as its root_broadcast secondary.  Per-GPU work is fixed as N grows (weak scaling); value =
-(build + probe keys over all ranks) / max-over-ranks wall time, inputs already resident in HBM.
+replicates the whole batch ahead of the step that probes it, so every xGMI link carries 1/N of
+it (measured on the default N > 1 line as its all_gather_spread secondary).  Per-GPU work is
+fixed as N grows (weak scaling); value = (build + probe keys over all ranks) / max-over-ranks
+wall time, inputs already resident in HBM.  At N > 1 the default line also runs the north
+star's C5 (c5: 64 filters sharded over the ranks, a new batch broadcast every step; c5_spread;
+c5_2d) in the same processes after the headline (dist_variants).
 c4: the same with variable-length keys (8-256 B, zipf); no broadcast.
 c2_sharded / c3_partitioned: ONE filter over the ranks: its 10M keys built from key
 shards (all-to-all + OR kernel + all-gather), or its 10M-key probe batch split by key with the
@@ -124,12 +127,15 @@ def parse():
                     help="c2c3/c5, N > 1: 'step' (default, the headline) broadcasts a new probe batch from rank 0 "
                          "in every timed step (pipelined two steps ahead); 'resident' broadcasts it once before "
                          "the timed steps (measured as the line's resident_batch secondary as well)")
-    ap.add_argument("--batch-origin", default="spread", choices=["spread", "root"],
-                    help="c2c3, N > 1, --batch step: 'spread' (default) - each new batch arrives spread over the "
-                         "ranks (rank r holds 1/N of its keys, as when each GPU ingests its share over its own "
-                         "PCIe link) and is replicated by an RCCL all-gather of the ranks' packed residues; 'root' "
-                         "- it arrives on rank 0 and is RCCL-broadcast (measured as the line's root_broadcast "
-                         "secondary as well)")
+    ap.add_argument("--batch-origin", default="root", choices=["root", "spread"],
+                    help="c2c3/c5, N > 1, --batch step: 'root' (default, the north star's form) - each new batch "
+                         "arrives on rank 0 and is RCCL-broadcast over xGMI; 'spread' - it arrives spread over the "
+                         "ranks (rank r holds 1/N of its keys, as when each GPU ingests its share over its own PCIe "
+                         "link) and is replicated by an RCCL all-gather of the ranks' packed residues (measured as "
+                         "the default line's all_gather_spread / c5_spread secondaries)")
+    ap.add_argument("--pack6", type=int, default=1,
+                    help="c5/c5_2d, N > 1: the batch travels as 6-byte packed residues when the filters allow "
+                         "(k == 7, m < 2^21: the 100K-key compaction filters), else 8-byte")
     ap.add_argument("--c5-groups", type=int, default=None,
                     help="c5_2d: key groups R (default: the world size, i.e. every GPU holds all 64 filters)")
     ap.add_argument("--overlap", type=int, default=0,
@@ -218,6 +224,7 @@ def setup_c2c3(args, seb, kg, torch, dev, rank, world, dist):
         st.workload += " as 8-B packed residues (each rank hashes its own 1/N)"
         st.kernel_bytes["probe"] = 24.0 * (hi - lo) + 8.0 * n + nb + n
         st.pmc_key = "c2c3_spread"  # its own kernels (pack + packed probe): no c2c3 PMC entry applies
+        st.scaled_keys = hi - lo    # the pack's share of the batch (pmc_traffic's per_key_bytes)
         st.bcast_lead = 2
         st.packed = [torch.zeros(width * world, dtype=torch.int64, device=dev) for _ in range(st.bcast_lead + 1)]
         st.gather_bufs = st.packed
@@ -410,6 +417,13 @@ def setup_c4(args, seb, kg, torch, dev, rank, world, dist):
     return st
 
 
+def c5_batch_keys(kg, nf, per, q):
+    """C5's probe keys for batch positions q: even q -> present in exactly filter
+    (q/2) mod 64; odd q -> absent from every filter."""
+    half = q // 2
+    return kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q))
+
+
 def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
     import dist_probe as dp
 
@@ -424,67 +438,112 @@ def setup_c5(args, seb, kg, torch, dev, rank, world, dist):
         seb.dev_build_many(seb.dev_keys(fkeys, n=shard.count * per, stride=16),
                            [j * per for j in range(shard.count + 1)], st.local)
     torch.cuda.synchronize()
-    q = np.arange(n, dtype=np.int64)
-    half = q // 2
-    probe_host = kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q)) if rank == 0 else None
-    st.pbufs = [torch.zeros((n, 16), dtype=torch.uint8, device=dev) for _ in range(2)]
-    if rank == 0:
-        st.pbufs[0].copy_(torch.from_numpy(probe_host))
-        st.pbufs[1].copy_(st.pbufs[0])
-    st.pk = [seb.dev_keys(b, n=n, stride=16) for b in st.pbufs]
+    nb = (m + 7) // 8
     st.plane = torch.zeros(n, dtype=shard.plane_dtype(), device=dev)
     st.planes = [torch.empty_like(st.plane) for _ in range(world)]
     plane_b, planes_b = dp.comm_view(st.plane), [dp.comm_view(p) for p in st.planes]  # byte views to communicate
-    st.kernel_bytes = {"probe": 16.0 * n + shard.count * ((m + 7) // 8) + st.plane.element_size() * n}
     st.units_per_step = float(n)
     st.scaling = "strong"
     st.workload = ("C5: 64 SSTable filters (100K keys each, m=958,506, k=7) sharded over the GPUs; a 10M-key "
                    "batch RCCL-broadcast from rank 0, multi-filter probe, answer planes gathered to rank 0")
-    # N > 1: the 64 filters share (m, k), so the batch travels as 8-B packed residues (80 MB per step
-    # instead of 160 MB of keys): rank 0 packs batch j+2 in step j (seb_dev_pack_residues) and every
-    # rank probes the packed words of batch j (seb_dev_probe_multi_packed).
-    # Default at N > 1 (--batch step): a new batch is broadcast in every step (pipelined two steps
-    # ahead), so the transfer is inside the timed region; --batch resident broadcasts it once before
-    # the timed steps (the resident_batch secondary).  The planes are gathered to rank 0 in every
-    # step either way.
+    # N > 1: the 64 filters share (m, k), so the batch travels as packed residues instead of the
+    # 16-B keys: 6 bytes per key when m < 2^21 (seb_dev_pack_residues6: 60 MB per step instead of
+    # 160 MB of keys), else 8.  --batch step (default): a new batch every step, pipelined two steps
+    # ahead, so the transfer is inside the timed region:
+    #   --batch-origin root (default, BASELINE configs[4]): rank 0 packs batch j+2 in step j and
+    #     RCCL-broadcasts it at the end of the step;
+    #   --batch-origin spread: rank r holds 1/N of every batch (64-key aligned slices), packs its
+    #     part of batch j+2 in step j and one RCCL all-gather replicates it (both directions of
+    #     every link carry 1/N of the batch).
+    # Every rank probes the packed words of batch j against its filters (the interleaved table).
+    # --batch resident broadcasts one batch before the timed steps (the resident_batch secondary).
+    # The planes are gathered to rank 0 in every step either way.
     packed = world > 1 and args.bcast == "packed" and k == 7 and m < (1 << 29)
+    pack6 = packed and bool(args.pack6) and seb.pack6_supported(m, k)
+    W = 6 if pack6 else 8
     per_step = world > 1 and args.batch == "step"
-    if packed and per_step:
+    spread = per_step and packed and args.batch_origin == "spread"
+    lay = dp.Packed6Layout() if pack6 else dp.RowLayout()
+
+    def packed_buf(keys):  # a buffer for `keys` keys of packed words in this width
+        return (torch.zeros(lay.rows(keys), dtype=torch.uint8, device=dev) if pack6
+                else torch.zeros(keys, dtype=torch.int64, device=dev))
+
+    def pack(kd, buf):
+        (seb.dev_pack_residues6 if pack6 else seb.dev_pack_residues)(kd, m, k, buf)
+
+    def probe_packed(buf):
+        (seb.dev_probe_multi_packed6 if pack6 else seb.dev_probe_multi_packed)(buf, n, st.local, st.plane)
+
+    if spread:
+        lo, hi, width = dp.spread_bounds(n, world, rank, align=lay.align)
+        st.spread_kb = seb.dev_keys(torch.from_numpy(c5_batch_keys(kg, nf, per, np.arange(lo, hi))).to(dev),
+                                    n=hi - lo, stride=16)
         st.bcast_lead = 2
-        st.packed = [torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(st.bcast_lead + 1)]
+        st.packed = [packed_buf(width * world) for _ in range(st.bcast_lead + 1)]
+        st.gather_bufs = st.packed
+        st.bcast_prologue = lambda b, part: pack(st.spread_kb, part) if hi > lo else None
+        st.kernel_bytes = {"probe": (16.0 + W) * (hi - lo) + W * n + shard.count * nb + st.plane.element_size() * n}
+        st.workload = ("C5: 64 SSTable filters (100K keys each, m=958,506, k=7) sharded over the GPUs; a new 10M-key "
+                       f"batch every step arriving spread over the ranks (1/N each), replicated by an RCCL all-gather "
+                       f"as {W}-B packed residues; multi-filter probe, answer planes gathered to rank 0")
+        st.pmc_key = f"c5_spread{W}@{world}"  # per-launch traffic depends on the filters per rank
+        st.scaled_keys = hi - lo
+    else:
+        if rank == 0:
+            st.pbuf = torch.from_numpy(c5_batch_keys(kg, nf, per, np.arange(n, dtype=np.int64))).to(dev)
+            st.pk = seb.dev_keys(st.pbuf, n=n, stride=16)
+        st.kernel_bytes = {"probe": 16.0 * n + shard.count * nb + st.plane.element_size() * n}
+    if spread:
+        pass
+    elif packed and per_step:
+        st.bcast_lead = 2
+        st.packed = [packed_buf(n) for _ in range(st.bcast_lead + 1)]
         st.broadcast_bufs = st.packed
-        st.bcast_prologue = lambda b, buf: seb.dev_pack_residues(st.pk[0], m, k, buf)
-        st.kernel_bytes["probe"] = (24.0 * n if rank == 0 else 0.0) + 8.0 * n + shard.count * ((m + 7) // 8) + \
+        st.bcast_prologue = lambda b, buf: pack(st.pk, buf)
+        st.kernel_bytes["probe"] = ((16.0 + W) * n if rank == 0 else 0.0) + W * n + shard.count * nb + \
             st.plane.element_size() * n
-        st.workload += " (a new batch every step, as 8-B packed residues hashed once on rank 0)"
-        st.pmc_key = "c5_packed"
+        st.workload += f" (a new batch every step, as {W}-B packed residues hashed once on rank 0)"
+        st.pmc_key = f"c5_packed{W}@{world}"
+        st.scaled_keys = n if rank == 0 else 0
     elif per_step:
-        st.broadcast_bufs = st.pbufs
+        if rank > 0:
+            st.pbuf = torch.zeros((n, 16), dtype=torch.uint8, device=dev)
+            st.pk = seb.dev_keys(st.pbuf, n=n, stride=16)
+        st.broadcast_bufs = [st.pbuf, torch.empty_like(st.pbuf) if rank > 0 else st.pbuf.clone()]
+        st.pks = [seb.dev_keys(b, n=n, stride=16) for b in st.broadcast_bufs]
     elif world > 1:
-        st.resident = torch.zeros(n, dtype=torch.int64, device=dev) if packed else st.pbufs[0]
+        st.resident = packed_buf(n) if packed else st.pbuf if rank == 0 else \
+            torch.zeros((n, 16), dtype=torch.uint8, device=dev)
         if packed and rank == 0:
-            seb.dev_pack_residues(st.pk[0], m, k, st.resident)
+            pack(st.pk, st.resident)
         torch.cuda.synchronize()
         dist.broadcast(st.resident, src=0)
         torch.cuda.synchronize()
         st.bcast_buf = st.resident
+        if not packed and rank > 0:
+            st.pk = seb.dev_keys(st.resident, n=n, stride=16)
         if packed and rank > 0:
-            st.kernel_bytes["probe"] = 8.0 * n + shard.count * ((m + 7) // 8) + st.plane.element_size() * n
+            st.kernel_bytes["probe"] = W * n + shard.count * nb + st.plane.element_size() * n
         st.workload += " (broadcast once, resident during the timed steps" + \
-            (", as 8-B packed residues)" if packed else ")")
-    st.parallelism = f"filters sharded {nf}/{world} per gpu, batch broadcast + plane gather (RCCL)"
+            (f", as {W}-B packed residues)" if packed else ")")
+    st.parallelism = (f"filters sharded {nf}/{world} per gpu, batch " +
+                      ("all-gathered" if spread else "broadcast") + " + plane gather (RCCL)")
 
     def probe(j, buf, target):
         if packed and per_step:
-            if rank == 0:  # the broadcast form of batch j + 2
-                seb.dev_pack_residues(st.pk[0], m, k, target)
+            if not spread and rank == 0:  # the broadcast form of batch j + 2
+                pack(st.pk, target)
+            elif spread and st.spread_kb.n:  # this rank's part of batch j + 2
+                pack(st.spread_kb, target)
             if shard.count:
-                seb.dev_probe_multi_packed(buf, n, st.local, st.plane)
+                probe_packed(buf)
         elif packed and rank > 0:
             if shard.count:
-                seb.dev_probe_multi_packed(st.resident, n, st.local, st.plane)
+                probe_packed(st.resident)
         elif shard.count:
-            seb.dev_probe_multi(st.pk[j % 2], st.local, st.plane)
+            kd = st.pks[j % 2] if per_step else st.pk
+            seb.dev_probe_multi(kd, st.local, st.plane)
         if world > 1:  # only rank 0 assembles masks: gather the answer planes there
             dist.gather(plane_b, gather_list=planes_b if rank == 0 else None, dst=0)
 
@@ -513,7 +572,10 @@ def setup_c5_2d(args, seb, kg, torch, dev, rank, world, dist):
     m, k = seb.params(per, 0.01)
     st.m, st.k, st.n = m, k, n
     groups = args.c5_groups or world
-    grid = dp.KeyFilterGrid(nf, rank, world, groups)
+    pack6 = world > 1 and bool(args.pack6) and seb.pack6_supported(m, k)
+    lay = dp.Packed6Layout() if pack6 else dp.RowLayout()
+    W = 6 if pack6 else 8
+    grid = dp.KeyFilterGrid(nf, rank, world, groups, align=lay.align)
     shard = grid.shard
     fkeys = torch.from_numpy(kg.key16(shard.lo * per + np.arange(shard.count * per))).to(dev)
     st.local = [(seb.new_words(m, device=dev), m, k) for _ in range(shard.count)]
@@ -523,15 +585,14 @@ def setup_c5_2d(args, seb, kg, torch, dev, rank, world, dist):
     torch.cuda.synchronize()
     if rank == 0:
         q = np.arange(n, dtype=np.int64)
-        half = q // 2
-        st.pbuf = torch.from_numpy(kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf, nf * per + q))).to(dev)
+        st.pbuf = torch.from_numpy(c5_batch_keys(kg, nf, per, q)).to(dev)
         st.pk = seb.dev_keys(st.pbuf, n=n, stride=16)
     nb = (m + 7) // 8
     st.units_per_step = float(n)
     st.scaling = "strong"
     st.workload = (f"C5 as a key x filter grid: 64 SSTable filters (100K keys each, m={m:,}, k={k}); {groups} key "
                    f"group(s) x {world // groups} filter slot(s); a new 10M-key batch every step, rank 0 sends each "
-                   "group its key shard as 8-B packed residues (RCCL point to point) and gets the u64 mask planes "
+                   f"group its key shard as {W}-B packed residues (RCCL point to point) and gets the u64 mask planes "
                    "back in the same exchange")
     st.parallelism = f"key groups {groups} x filter slots {world // groups}"
     if world == 1:
@@ -553,20 +614,24 @@ def setup_c5_2d(args, seb, kg, torch, dev, rank, world, dist):
         raise SystemExit("c5_2d at N > 1 sends packed residues: needs k == 7 and m < 2^29")
     mode = "p2p" if args.dist_backend == "nccl" else "collective"  # gloo cannot send device tensors p2p
     dist.barrier()  # a collective first: every rank joins the communicator before the first grouped p2p call
-    ex = dp.GridExchange(grid, n, (), torch.int64, dev, nbufs=3, mode=mode)
-    produce = (lambda b, buf: seb.dev_pack_residues(st.pk, m, k, buf[:n])) if rank == 0 else None
+    ex = dp.GridExchange(grid, n, (), torch.uint8 if pack6 else torch.int64, dev, nbufs=3, mode=mode, layout=lay)
+    pack = seb.dev_pack_residues6 if pack6 else seb.dev_pack_residues
+    probe_packed = seb.dev_probe_multi_packed6 if pack6 else seb.dev_probe_multi_packed
+    produce = (lambda b, buf: pack(st.pk, m, k, buf[:lay.rows(n)])) if rank == 0 else None
     st.pipe = dp.GridPipeline(ex, lead=2, produce=produce)
-    cnt = ex.hi - ex.lo
-    st.kernel_bytes = {"probe": (24.0 * n if rank == 0 else 0.0) + 8.0 * cnt + shard.count * nb
+    cnt = ex.shard_keys
+    st.kernel_bytes = {"probe": ((16.0 + W) * n if rank == 0 else 0.0) + W * cnt + shard.count * nb
                        + ex.pdtype.itemsize * cnt}
+    st.pmc_key = f"c5_2d{W}@{world}"
+    st.scaled_keys = n if rank == 0 else 0
     st.parallelism += f", {mode} exchange"
 
     def probe(j, buf, target):
         if rank == 0:  # the broadcast root's packing pass: batch j + 2, sent at the end of this step
-            seb.dev_pack_residues(st.pk, m, k, target[:n])
+            pack(st.pk, m, k, target[:lay.rows(n)])
         plane = ex.plane(j)
-        if shard.count and buf.shape[0]:
-            seb.dev_probe_multi_packed(buf, buf.shape[0], st.local, plane)
+        if shard.count and cnt:
+            probe_packed(buf, cnt, st.local, plane)
 
     def parity(j):
         if n != 10_000_000 or rank != 0:
@@ -750,6 +815,11 @@ def setup_wal(args, seb, kg, torch, dev, rank, world, dist):
     return st
 
 
+SETUPS = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "c5_2d": setup_c5_2d, "lsm": setup_lsm,
+          "lsm_wide": setup_lsm, "route": setup_route, "many": setup_many, "wal": setup_wal,
+          "c2_sharded": setup_c2_sharded, "c3_partitioned": setup_c3_partitioned}
+
+
 def free_port() -> int:
     import socket
 
@@ -824,9 +894,16 @@ def launch_check(args, world, rank):
     dist.all_reduce(t)
     rec = rr.rank_record(rank, int(os.environ.get("LOCAL_RANK", rank)), dist.get_world_size(), "gloo", None,
                          rr.allreduce_ones(torch, dist, None))
+    # the N > 1 line's same-process variants and this rank's share of each C5 form's batch, from
+    # the helpers the setups use (no GPU): their shape, checked by tests/test_bench_launch.py
+    import dist_probe as dp
+
+    rec["c5_plan"] = [dp.c5_rank_plan(args.keys, world, rank, form, 6) for form in ("root", "spread", "grid")]
     recs = rr.gather_records(dist, rec, world)
     if rank == 0:
         print(json.dumps({"n_gpus": dist.get_world_size(), "rank_sum": int(t.item()),
+                          "variants": [{"key": key, "config": cfg, "overrides": over}
+                                       for key, cfg, over, _ in dist_variants(args, world)],
                           "master": f"{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}",
                           "per_rank": recs, **rr.summarize(recs, world, "gloo")}), flush=True)
     dist.barrier()
@@ -959,10 +1036,7 @@ def main():
         if v is not None:
             seb.set_option(o, v)
 
-    setup = {"c2c3": setup_c2c3, "c4": setup_c4, "c5": setup_c5, "c5_2d": setup_c5_2d, "lsm": setup_lsm,
-             "lsm_wide": setup_lsm, "route": setup_route, "many": setup_many, "wal": setup_wal,
-             "c2_sharded": setup_c2_sharded, "c3_partitioned": setup_c3_partitioned}[args.config]
-    st = setup(args, seb, kg, torch, dev, rank, world, dist)
+    st = SETUPS[args.config](args, seb, kg, torch, dev, rank, world, dist)
     run = timed_run(args, st, seb, torch, dist, world, rank, dev)
     # Parity of the last timed step's outputs, checked after the timed region: a large pageable
     # D2H (.cpu()) delays the next kernel launch by ~20 ms on this runtime (tools/dbg_sharded_timing.py),
@@ -981,47 +1055,12 @@ def main():
     records = rr.gather_records(dist, rec, world)
     report = rr.summarize(records, world, backend)
     value = st.units_per_step * args.steps / elapsed / 1e6
-    def variant(note, **over):
-        # the same job in another form, set up and timed in this process after the headline
-        import copy
-
-        a2 = copy.copy(args)
-        for key, v in over.items():
-            setattr(a2, key, v)
-        st2 = setup(a2, seb, kg, torch, dev, rank, world, dist)
-        r2 = timed_run(a2, st2, seb, torch, dist, world, rank, dev)
-        torch.cuda.synchronize()
-        out = {"value": round(st2.units_per_step * a2.steps / r2["elapsed"] / 1e6, 2), "unit": st2.unit,
-               "ms_per_step": round(r2["elapsed"] * 1000.0 / a2.steps, 4),
-               "kernel_ms": {k: round(v, 4) for k, v in r2["kern_ms"].items()},
-               "wait_ms": None if r2["wait_ms"] is None else round(r2["wait_ms"], 4),
-               "parity": st2.parity(a2.warmup + a2.steps - 1), "note": note}
-        if r2["bcast"]:
-            out["broadcast"] = r2["bcast"]
-        del st2
-        return out
-
-    resident = root_bcast = None
-    if world > 1 and args.config in ("c2c3", "c5") and args.batch == "step" and not args.no_secondary:
-        if args.config == "c2c3" and args.batch_origin == "spread" and args.bcast == "packed":
-            root_bcast = variant("secondary: a new batch in every step that arrives on rank 0 and is RCCL-broadcast "
-                                 "(8-B packed residues emitted by rank 0's probe); the headline's batch arrives "
-                                 "spread over the ranks and is all-gathered", batch_origin="root")
-        resident = variant("secondary: one batch RCCL-broadcast before the timed steps and probed resident in "
-                           "every step (its broadcast timed on its own); the headline value moves a new batch "
-                           "inside every step", batch="resident")
+    extra = {}
+    for key, cfg, over, note in dist_variants(args, world):
+        # the same processes, after the headline: another form of the job or the north star's C5
+        extra[key] = run_variant(args, cfg, over, note, seb, kg, torch, dist, world, rank, local, dev)
     result = None
     if rank == 0:
-        kern = {name: (ms, st.kernel_bytes[name]) for name, ms in kern_ms.items()}
-        dom = max(kern, key=lambda x: kern[x][0])
-        traffic = traffic_src = None  # PMC-measured HBM bytes of the dominant step (the newest round's profile that has it)
-        for pmc_path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")), reverse=True):
-            with open(pmc_path) as f:
-                traffic = json.load(f).get(st.pmc_key or args.config, {}).get(dom, {}).get("hbm_bytes_per_launch")
-            if traffic is not None:
-                traffic_src = f"{os.path.relpath(pmc_path, ROOT)}[{st.pmc_key or args.config}][{dom}]"
-                break
-        ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
         result = {
             "metric": METRIC if args.config in ("c2c3", "c4", "c5", "c5_2d", "lsm", "lsm_wide", "c2_sharded",
                                                 "c3_partitioned")
@@ -1034,19 +1073,11 @@ def main():
                        "num_hashes": st.k, "parallelism": st.parallelism},
             **{f"{name}_gkeys_s": round(st.n / (ms * 1e-3) / 1e9, 3) for name, ms in kern_ms.items()},
             **{f"{name}_ms": round(ms, 4) for name, ms in kern_ms.items()},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": int(kern[dom][1]),
-                         "time_source": "mean HIP-event launch time of the dominant call over the sampled "
-                                        "timed steps (launch_timers), on its launch stream; not the wall-clock step",
-                         "other": {d: {"ms": round(v[0], 4), "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 2)}
-                                   for d, v in kern.items()}},
+            "roofline": roofline_of(st, kern_ms, args.config),
             "parity": parity,
             **({"kernel_timing": run["kernel_timing"]} if run["kernel_timing"] else {}),
             **({"broadcast": bcast} if bcast else {}),
-            **({"root_broadcast": root_bcast} if root_bcast else {}),
-            **({"resident_batch": resident} if resident else {}),
+            **extra,
             "launch_timers": f"HIP events (no system fence) around build and probe on every {args.time_every}th "
                              "timed step and the last; ms_per_step is the wall clock of all steps",
             "options": {**{o: option_value(seb, o) for o in OPTIONS}, "overlap": int(overlap)},
@@ -1094,6 +1125,120 @@ def main():
     if report["problems"]:  # e.g. RCCL ranks that did not land on N distinct GPUs: not a valid N-GPU line
         print(f"bench.py: rank {rank}: " + "; ".join(report["problems"]), file=sys.stderr)
         sys.exit(4)
+
+
+def pmc_traffic(key: str, step: str, st) -> tuple:
+    """PMC-measured HBM bytes per launch of `step` under profiles/pmc_r*.json[key] (the newest
+    round that has it), and its source.  An entry may carry `per_key_bytes` (a kernel whose traffic
+    scales with this rank's share of the batch, measured per key, e.g. the spread path's pack of
+    1/N of the keys): its bytes x st.scaled_keys are added."""
+    for pmc_path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")), reverse=True):
+        with open(pmc_path) as f:
+            ent = json.load(f).get(key, {}).get(step)
+        if ent and ent.get("hbm_bytes_per_launch") is not None:
+            t = ent["hbm_bytes_per_launch"]
+            if ent.get("per_key_bytes") is not None:
+                t += ent["per_key_bytes"] * getattr(st, "scaled_keys", 0)
+            return int(t), f"{os.path.relpath(pmc_path, ROOT)}[{key}][{step}]"
+    return None, None
+
+
+def roofline_of(st, kern_ms: dict, config: str) -> dict:
+    """The dominant call's roofline: algorithmic bytes per launch (st.kernel_bytes) over its mean
+    HIP-event launch time, against the HBM peak, with the PMC-measured traffic when profiled."""
+    kern = {name: (ms, st.kernel_bytes[name]) for name, ms in kern_ms.items()}
+    dom = max(kern, key=lambda x: kern[x][0])
+    traffic, traffic_src = pmc_traffic(st.pmc_key or config, dom, st)
+    ach = kern[dom][1] / (kern[dom][0] * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS,
+            "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic,
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": int(kern[dom][1]),
+            "time_source": "mean HIP-event launch time of the dominant call over the sampled "
+                           "timed steps (launch_timers), on its launch stream; not the wall-clock step",
+            "other": {d: {"ms": round(v[0], 4), "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 2)}
+                      for d, v in kern.items()}}
+
+
+C5_VARIANT_STEPS = {"steps": 10, "warmup": 3}  # at most: a shorter headline run shortens them too
+
+
+def dist_variants(args, world: int) -> list:
+    """What the N > 1 line runs after its headline, in the same processes: (key, config,
+    overrides, note).  With the default config that is the headline's other batch forms and the
+    north star's own multi-GPU config, C5 (BASELINE.json configs[4]: 64 compaction-sized filters,
+    lsm/compaction.go:253,286, sharded over the GPUs; a new key batch over RCCL every step; the
+    per-Get fan-out of lsm/lsm.go:168-198), in its three forms."""
+    if world <= 1 or args.no_secondary or args.batch != "step":
+        return []
+    out = []
+    if args.config == "c2c3":
+        if args.bcast == "packed":
+            if args.batch_origin == "root":
+                out.append(("all_gather_spread", "c2c3", {"batch_origin": "spread"},
+                            "secondary: a new batch in every step that arrives spread over the ranks (1/N each) and "
+                            "is replicated by an RCCL all-gather of the ranks' packed residues; the headline's batch "
+                            "arrives on rank 0 and is RCCL-broadcast"))
+            else:
+                out.append(("root_broadcast", "c2c3", {"batch_origin": "root"},
+                            "secondary: a new batch in every step that arrives on rank 0 and is RCCL-broadcast"))
+        out.append(("resident_batch", "c2c3", {"batch": "resident"},
+                    "secondary: one batch RCCL-broadcast before the timed steps and probed resident in every step "
+                    "(its broadcast timed on its own); the headline value moves a new batch inside every step"))
+        out.append(("c5", "c5", {"batch_origin": "root", **C5_VARIANT_STEPS},
+                    "BASELINE configs[4] (north star): 64 filters of 100K keys sharded over the GPUs, a new 10M-key "
+                    "batch RCCL-broadcast from rank 0 every step as packed residues, planes gathered to rank 0"))
+        out.append(("c5_spread", "c5", {"batch_origin": "spread", **C5_VARIANT_STEPS},
+                    "C5 with each new batch arriving spread over the ranks and replicated by an RCCL all-gather"))
+        out.append(("c5_2d", "c5_2d", {"c5_groups": None, **C5_VARIANT_STEPS},
+                    "C5 as a key x filter grid with R = N key groups: every GPU holds all 64 filters, rank 0 sends "
+                    "each GPU its 1/N of every new batch and gets the mask planes back (RCCL point to point)"))
+    elif args.config == "c5":
+        other = "spread" if args.batch_origin == "root" else "root"
+        if args.bcast == "packed":
+            out.append(("c5_spread" if other == "spread" else "c5_root", "c5", {"batch_origin": other},
+                        f"secondary: the same job with --batch-origin {other}"))
+        out.append(("resident_batch", "c5", {"batch": "resident"},
+                    "secondary: one batch RCCL-broadcast before the timed steps and probed resident"))
+    return out
+
+
+def run_variant(args, cfg, over, note, seb, kg, torch, dist, world, rank, local, dev):
+    """One dist_variants entry, set up and timed (W + K steps between barriers, max over ranks)
+    in this process after the headline; every rank takes part.  Rank 0 gets its summary: value,
+    step time, parity against the golden digest, the dominant call's roofline and every rank's
+    batch-transfer wait."""
+    import copy
+
+    import rank_report as rr
+
+    a2 = copy.copy(args)
+    a2.config = cfg
+    for key, v in over.items():
+        setattr(a2, key, min(v, getattr(args, key)) if key in C5_VARIANT_STEPS else v)
+    st2 = SETUPS[cfg](a2, seb, kg, torch, dev, rank, world, dist)
+    r2 = timed_run(a2, st2, seb, torch, dist, world, rank, dev)
+    torch.cuda.synchronize()
+    parity = st2.parity(a2.warmup + a2.steps - 1)
+    rec = rr.rank_record(rank, local, world, args.dist_backend, None, world, r2["kern_ms"], r2["wait_ms"],
+                         r2["wait_host_ms"], r2["elapsed_own"])
+    recs = rr.gather_records(dist, rec, world)
+    out = None
+    if rank == 0:
+        out = {"config": cfg, "value": round(st2.units_per_step * a2.steps / r2["elapsed"] / 1e6, 2), "unit": st2.unit,
+               "scaling": st2.scaling, "steps": a2.steps, "warmup": a2.warmup,
+               "ms_per_step": round(r2["elapsed"] * 1000.0 / a2.steps, 4),
+               "kernel_ms": {k: round(v, 4) for k, v in r2["kern_ms"].items()},
+               "roofline": roofline_of(st2, r2["kern_ms"], cfg),
+               "wait_ms": None if r2["wait_ms"] is None else round(r2["wait_ms"], 4),
+               "per_rank": [{"rank": r["rank"], "kernel_ms": r["kernel_ms"], "wait_ms": r["wait_ms"],
+                             "wait_host_ms": r["wait_host_ms"], "elapsed_s": r["elapsed_s"]} for r in recs],
+               "parity": parity, "workload": st2.workload, "parallelism": st2.parallelism, "note": note}
+        if r2["bcast"]:
+            out["broadcast"] = r2["bcast"]
+    del st2
+    torch.cuda.synchronize()
+    return out
 
 
 def timed_run(args, st, seb, torch, dist, world, rank, dev):

@@ -158,6 +158,19 @@ int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *wor
  * have the packed batch's (num_bits, num_hashes). */
 int seb_dev_probe_multi_packed(const uint64_t *packed, uint64_t n, const seb_filter_ref *filters, uint32_t num_filters,
                                void *mask, uint32_t mask_bytes, void *stream);
+/* Narrow packed residues (6 bytes per key) for num_hashes == 7 and num_bits < 2^21, e.g. the
+ * compaction-sized filters of lsm/compaction.go:253,286 (m = 958,506): the same three fields as
+ * seb_dev_pack_residues at 21 / 21 / 6 bits, v = r0 | b << 21 | carries << 42, stored in blocks of
+ * 64 keys (key i in block i / 64): 64 little-endian u32 low words, then 64 u16 high halves, 384
+ * bytes per block; the buffer holds seb_packed6_bytes(n) bytes and must be 4-byte aligned.  A slice
+ * of the batch that starts at a multiple of 64 keys is the contiguous byte range from its first
+ * block, so a batch split in 64-key multiples travels as plain byte ranges (a quarter fewer bytes
+ * over xGMI than the 8-byte form).  seb_dev_probe_multi_packed6 gives the masks
+ * seb_dev_probe_multi gives for the keys. */
+uint64_t seb_packed6_bytes(uint64_t n);
+int seb_dev_pack_residues6(const seb_keys *keys, uint64_t num_bits, uint32_t num_hashes, void *packed6, void *stream);
+int seb_dev_probe_multi_packed6(const void *packed6, uint64_t n, const seb_filter_ref *filters, uint32_t num_filters,
+                                void *mask, uint32_t mask_bytes, void *stream);
 /* seb_dev_probe plus the batch's packed residues in one pass (the broadcast root's probe). */
 int seb_dev_probe_emit_packed(const seb_keys *keys, const uint32_t *words, uint64_t num_bits, uint32_t num_hashes,
                               uint8_t *out, uint64_t *packed, void *stream);

@@ -343,6 +343,34 @@ __device__ __forceinline__ void packed_positions(uint64_t v, uint32_t m, uint32_
     }
 }
 
+// The narrow form (m < 2^kPack6Bits): the same fields at 21 / 21 / 6 bits, 48 bits per key, in
+// blocks of 64 keys: low words at u32 index 96 * block + lane, high halves at u16 index
+// 192 * block + 128 + lane (seb_kernels.h kPack6Block).
+__device__ __forceinline__ uint64_t pack_residue6(uint64_t h1, uint64_t h2, const ModArg &md) {
+    const uint64_t r0 = mod_m31(h1, (uint32_t)md.m, md.mu), b = mod_m31(h2, (uint32_t)md.m, md.mu);
+    uint64_t f = 0, x = h1;
+#pragma unroll
+    for (uint32_t q = 1; q < 7; ++q) {
+        const uint64_t xn = x + h2;
+        f |= (uint64_t)(xn < x) << (q - 1);
+        x = xn;
+    }
+    return r0 | (b << kPack6Bits) | (f << (2 * kPack6Bits));
+}
+__device__ __forceinline__ void store_packed6(uint8_t *base, uint64_t i, uint64_t v) {
+    const uint64_t blk = i >> 6;
+    const uint32_t lane = (uint32_t)i & 63u;
+    __builtin_nontemporal_store((uint32_t)v, (uint32_t *)(base + blk * kPack6Block) + lane);
+    __builtin_nontemporal_store((uint16_t)(v >> 32), (uint16_t *)(base + blk * kPack6Block + 256) + lane);
+}
+__device__ __forceinline__ uint64_t load_packed6(const uint8_t *base, uint64_t i) {
+    const uint64_t blk = i >> 6;
+    const uint32_t lane = (uint32_t)i & 63u;
+    const uint32_t lo = __builtin_nontemporal_load((const uint32_t *)(base + blk * kPack6Block) + lane);
+    const uint16_t hi = __builtin_nontemporal_load((const uint16_t *)(base + blk * kPack6Block + 256) + lane);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
 // A batch given as packed residues (the variable-length pre-hash writes these when the filter
 // allows): load(i) carries the 8-byte word in .x/.y; kernels take the positions from it directly.
 struct KeysPacked {

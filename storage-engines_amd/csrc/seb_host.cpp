@@ -684,6 +684,33 @@ extern "C" int seb_dev_probe_packed(const uint64_t *packed, uint64_t n, const ui
     return SEB_OK;
 }
 
+// Narrow packed residues: 6 bytes per key in 64-key blocks, for k == 7 and m < 2^21.
+static int check_packed6_args(uint64_t m, uint32_t k, const char *who) {
+    int rc = check_filter_args(m, k, who);
+    if (rc) return rc;
+    if (k != 7 || m >= (1ull << kPack6Bits))
+        return fail(SEB_ERR_INVALID, "%s: 6-byte packed residues need k == 7 and m < 2^%u (k=%u m=%llu)", who,
+                    kPack6Bits, k, (unsigned long long)m);
+    return SEB_OK;
+}
+
+extern "C" uint64_t seb_packed6_bytes(uint64_t n) { return packed6_bytes(n); }
+
+extern "C" int seb_dev_pack_residues6(const seb_keys *keys, uint64_t m, uint32_t k, void *packed6, void *stream) {
+    WsCall ws_call;
+    enter();
+    int rc;
+    if ((rc = check_keys(keys, "seb_dev_pack_residues6")) || (rc = check_packed6_args(m, k, "seb_dev_pack_residues6")))
+        return rc;
+    if (!packed6 && keys->n) return fail(SEB_ERR_INVALID, "seb_dev_pack_residues6: null packed6");
+    if (((uintptr_t)packed6 & 3) != 0) return fail(SEB_ERR_INVALID, "seb_dev_pack_residues6: packed6 not 4-byte aligned");
+    KeyBatch kb = key_batch(keys);
+    void *ws;
+    if ((rc = prepare_probe_keys(kb, (hipStream_t)stream, 0, &ws))) return rc;
+    HIP_OR_FAIL(launch_pack_residues6(kb, mod_arg(m, k), (uint8_t *)packed6, (hipStream_t)stream));
+    return SEB_OK;
+}
+
 extern "C" int seb_dev_probe_emit_packed(const seb_keys *keys, const uint32_t *words, uint64_t m, uint32_t k,
                                          uint8_t *out, uint64_t *packed, void *stream) {
     WsCall ws_call;
@@ -768,6 +795,29 @@ extern "C" int seb_dev_probe_multi_packed(const uint64_t *packed, uint64_t n, co
     void *ws = nullptr;
     if ((rc = cached_workspace(s, (tb + 255) & ~255ull, &ws))) return rc;
     HIP_OR_FAIL(launch_probe_interleaved_packed(packed, n, ma, mask, mask_bytes, ws, s));
+    return SEB_OK;
+}
+
+extern "C" int seb_dev_probe_multi_packed6(const void *packed6, uint64_t n, const seb_filter_ref *filters,
+                                           uint32_t nf, void *mask, uint32_t mask_bytes, void *stream) {
+    WsCall ws_call;
+    enter();
+    int rc;
+    MultiArg ma;
+    if ((rc = fill_multi(filters, nf, mask_bytes, &ma, "seb_dev_probe_multi_packed6"))) return rc;
+    for (uint32_t f = 0; f < nf; ++f)
+        if (ma.f[f].md.m != ma.f[0].md.m || ma.f[f].md.k != ma.f[0].md.k)
+            return fail(SEB_ERR_INVALID, "seb_dev_probe_multi_packed6: filters must share (num_bits, num_hashes)");
+    if ((rc = check_packed6_args(ma.f[0].md.m, ma.f[0].md.k, "seb_dev_probe_multi_packed6"))) return rc;
+    if (n && (!packed6 || !mask)) return fail(SEB_ERR_INVALID, "seb_dev_probe_multi_packed6: null pointer");
+    if (((uintptr_t)packed6 & 3) != 0)
+        return fail(SEB_ERR_INVALID, "seb_dev_probe_multi_packed6: packed6 not 4-byte aligned");
+    if (n == 0) return SEB_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t tb = ((ma.f[0].md.m + 31) / 32) * 32 * mask_bytes;
+    void *ws = nullptr;
+    if ((rc = cached_workspace(s, (tb + 255) & ~255ull, &ws))) return rc;
+    HIP_OR_FAIL(launch_probe_interleaved_packed6((const uint8_t *)packed6, n, ma, mask, mask_bytes, ws, s));
     return SEB_OK;
 }
 

@@ -189,6 +189,16 @@ hipError_t launch_build_many_lds(const KeyBatch &kb, const ManyArg &ma, uint32_t
 // Packed residues (k == 7, m < 2^kPackBits): 8 bytes per key instead of the key itself.
 constexpr uint32_t kPackBits = 29;
 hipError_t launch_pack_residues(const KeyBatch &kb, const ModArg &md, uint64_t *packed, hipStream_t s);
+// Narrow packed residues (k == 7, m < 2^kPack6Bits, e.g. the 958,506-bit compaction filters): the
+// same three fields in 48 bits (21-bit r0, 21-bit b, 6 carries), 6 bytes per key, stored in blocks
+// of 64 keys (64 u32 low words, then 64 u16 high words: kPack6Block bytes), so a wave moves a block
+// with two coalesced loads and a slice starting at a multiple of 64 keys is one contiguous range.
+constexpr uint32_t kPack6Bits = 21;
+constexpr uint32_t kPack6Block = 384;
+constexpr uint64_t packed6_bytes(uint64_t n) { return ((n + 63) / 64) * kPack6Block; }
+hipError_t launch_pack_residues6(const KeyBatch &kb, const ModArg &md, uint8_t *packed6, hipStream_t s);
+hipError_t launch_probe_interleaved_packed6(const uint8_t *packed6, uint64_t n, const MultiArg &ma, void *mask,
+                                            uint32_t mask_bytes, void *ws, hipStream_t s);
 // out[w] = OR over s < nslices of in[s * slice_words + w] (the sharded build's reduction step)
 hipError_t launch_or_slices(const uint32_t *in, uint32_t nslices, uint64_t slice_words, uint32_t *out, hipStream_t s);
 hipError_t launch_probe_packed(const uint64_t *packed, uint64_t n, const uint32_t *words, const ModArg &md,

@@ -152,6 +152,18 @@ __global__ __launch_bounds__(256) void k_pack_residues(Src src, uint64_t n, ModA
     }
 }
 
+// The narrow 6-byte form (m < 2^kPack6Bits): 64-key blocks, one u32 and one u16 store per lane,
+// each wave writing one block's two rows whole.
+template <typename Src>
+__global__ __launch_bounds__(256) void k_pack_residues6(Src src, uint64_t n, ModArg md, uint8_t *__restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t h1, h2;
+        src.hash(i, h1, h2);
+        store_packed6(out, i, pack_residue6(h1, h2, md));
+    }
+}
+
 // Sliced probe from keys that also writes each key's packed residues: the root of a
 // multi-GPU probe answers a batch for its own filter and produces the broadcast form in one pass.
 template <typename Src, int KPT>
@@ -592,16 +604,18 @@ __global__ __launch_bounds__(256) void k_probe_interleaved(Src src, uint64_t n, 
     }
 }
 
-// Interleaved multi-filter probe over packed residues (k_pack_residues' layout): the broadcast
-// form of a batch probed against same-size filters on several GPUs (C5 at N > 1).
-template <typename MaskT>
-__global__ __launch_bounds__(256) void k_probe_interleaved_packed(const uint64_t *__restrict__ packed, uint64_t n,
+// Interleaved multi-filter probe over packed residues: the broadcast form of a batch probed
+// against same-size filters on several GPUs (C5 at N > 1).  W = 8: k_pack_residues' 8-byte words
+// (29-bit fields); W = 6: the narrow 48-bit form in 64-key blocks (k_pack_residues6, 21-bit fields).
+template <typename MaskT, int W>
+__global__ __launch_bounds__(256) void k_probe_interleaved_packed(const void *__restrict__ packed, uint64_t n,
                                                                   const MaskT *__restrict__ table, ModArg md,
                                                                   MaskT *__restrict__ mask, uint32_t slice_shift,
                                                                   uint32_t nslices) {
     constexpr int KPT = 2;
+    constexpr uint32_t kBits = W == 8 ? kPackBits : kPack6Bits;
+    constexpr uint64_t kMask = (1ull << kBits) - 1;
     const uint32_t m = (uint32_t)md.m, c = (uint32_t)md.c;
-    constexpr uint64_t kMask = (1ull << kPackBits) - 1;
     const uint64_t span = (uint64_t)blockDim.x * KPT;
     for (uint64_t base = (uint64_t)blockIdx.x * span; base < n; base += (uint64_t)gridDim.x * span) {
         uint32_t pos[KPT][7];
@@ -609,9 +623,15 @@ __global__ __launch_bounds__(256) void k_probe_interleaved_packed(const uint64_t
 #pragma unroll
         for (int r = 0; r < KPT; ++r) {
             const uint64_t i = base + (uint64_t)r * blockDim.x + threadIdx.x;
-            const uint64_t v = i < n ? __builtin_nontemporal_load(packed + i) : 0ull;
+            uint64_t v = 0;
+            if (i < n) {
+                if constexpr (W == 8)
+                    v = __builtin_nontemporal_load((const uint64_t *)packed + i);
+                else
+                    v = load_packed6((const uint8_t *)packed, i);
+            }
             uint32_t x = (uint32_t)(v & kMask);
-            const uint32_t b = (uint32_t)((v >> kPackBits) & kMask), f = (uint32_t)(v >> (2 * kPackBits));
+            const uint32_t b = (uint32_t)((v >> kBits) & kMask), f = (uint32_t)(v >> (2 * kBits));
             const uint32_t nb = m - b, bc = b >= c ? b - c : b + (m - c), nd = m - bc;
             pos[r][0] = x;
 #pragma unroll
@@ -922,8 +942,8 @@ static hipError_t interleaved_mask(const KeyBatch &kb, const MultiArg &ma, void 
     });
 }
 
-template <typename MaskT>
-static hipError_t interleaved_mask_packed(const uint64_t *packed, uint64_t n, const MultiArg &ma, void *mask, void *ws,
+template <typename MaskT, int W>
+static hipError_t interleaved_mask_packed(const void *packed, uint64_t n, const MultiArg &ma, void *mask, void *ws,
                                           hipStream_t s) {
     const ModArg &md = ma.f[0].md;
     MaskT *table = (MaskT *)ws;
@@ -931,7 +951,7 @@ static hipError_t interleaved_mask_packed(const uint64_t *packed, uint64_t n, co
     const uint32_t shift = table_slice_shift<MaskT>();
     const uint32_t nsl = (uint32_t)((md.m + (1ull << shift) - 1) >> shift);
     const unsigned g = grid_for((n + 1) / 2, 256, options().grid_cap);
-    hipLaunchKernelGGL((k_probe_interleaved_packed<MaskT>), dim3(g), dim3(256), 0, s, packed, n, (const MaskT *)table, md,
+    hipLaunchKernelGGL((k_probe_interleaved_packed<MaskT, W>), dim3(g), dim3(256), 0, s, packed, n, (const MaskT *)table, md,
                        (MaskT *)mask, shift, nsl);
     return hipGetLastError();
 }
@@ -940,10 +960,21 @@ hipError_t launch_probe_interleaved_packed(const uint64_t *packed, uint64_t n, c
                                            uint32_t mask_bytes, void *ws, hipStream_t s) {
     if (n == 0) return hipSuccess;
     switch (mask_bytes) {
-        case 1: return interleaved_mask_packed<uint8_t>(packed, n, ma, mask, ws, s);
-        case 2: return interleaved_mask_packed<uint16_t>(packed, n, ma, mask, ws, s);
-        case 4: return interleaved_mask_packed<uint32_t>(packed, n, ma, mask, ws, s);
-        default: return interleaved_mask_packed<uint64_t>(packed, n, ma, mask, ws, s);
+        case 1: return interleaved_mask_packed<uint8_t, 8>(packed, n, ma, mask, ws, s);
+        case 2: return interleaved_mask_packed<uint16_t, 8>(packed, n, ma, mask, ws, s);
+        case 4: return interleaved_mask_packed<uint32_t, 8>(packed, n, ma, mask, ws, s);
+        default: return interleaved_mask_packed<uint64_t, 8>(packed, n, ma, mask, ws, s);
+    }
+}
+
+hipError_t launch_probe_interleaved_packed6(const uint8_t *packed6, uint64_t n, const MultiArg &ma, void *mask,
+                                            uint32_t mask_bytes, void *ws, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    switch (mask_bytes) {
+        case 1: return interleaved_mask_packed<uint8_t, 6>(packed6, n, ma, mask, ws, s);
+        case 2: return interleaved_mask_packed<uint16_t, 6>(packed6, n, ma, mask, ws, s);
+        case 4: return interleaved_mask_packed<uint32_t, 6>(packed6, n, ma, mask, ws, s);
+        default: return interleaved_mask_packed<uint64_t, 6>(packed6, n, ma, mask, ws, s);
     }
 }
 
@@ -1030,6 +1061,16 @@ hipError_t launch_pack_residues(const KeyBatch &kb, const ModArg &md, uint64_t *
         using S = decltype(src);
         hipLaunchKernelGGL(k_pack_residues<S>, dim3(grid_for(kb.n, 256, options().grid_cap)), dim3(256), 0, s, src,
                            kb.n, md, packed);
+        return hipGetLastError();
+    });
+}
+
+hipError_t launch_pack_residues6(const KeyBatch &kb, const ModArg &md, uint8_t *packed6, hipStream_t s) {
+    if (kb.n == 0) return hipSuccess;
+    return with_src(kb, [&](auto src) {
+        using S = decltype(src);
+        hipLaunchKernelGGL(k_pack_residues6<S>, dim3(grid_for(kb.n, 256, options().grid_cap)), dim3(256), 0, s, src,
+                           kb.n, md, packed6);
         return hipGetLastError();
     });
 }

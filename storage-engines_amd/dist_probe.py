@@ -206,12 +206,44 @@ class BroadcastPipeline:
         return self.root_target(j) if self.rank == 0 and self.lead > 1 else None
 
 
-def spread_bounds(n: int, world: int, rank: int) -> tuple[int, int, int]:
+def spread_bounds(n: int, world: int, rank: int, align: int = 1) -> tuple[int, int, int]:
     """Rank `rank`'s part of an n-key batch that arrives spread over the ranks: keys [lo, hi) of
-    equal slices of width ceil(n / world) (the last one shorter), and that width."""
+    equal slices of width ceil(n / world) rounded up to a multiple of `align` (the last ones
+    shorter or empty), and that width.  align = 64 keeps every slice whole 64-key blocks of the
+    6-byte packed form (Packed6Layout)."""
     c = -(-n // world)
+    c = -(-c // align) * align
     lo = min(n, rank * c)
     return lo, min(n, lo + c), c
+
+
+class RowLayout:
+    """How a batch of keys sits in a communication buffer: one row per key (16-B keys, 8-B packed
+    words).  rows(n): buffer rows for n keys; span(lo, hi): the rows holding keys [lo, hi)."""
+
+    align = 1
+
+    def rows(self, n: int) -> int:
+        return n
+
+    def span(self, lo: int, hi: int) -> tuple[int, int]:
+        return lo, hi
+
+
+class Packed6Layout(RowLayout):
+    """6-byte packed residues (include/seb_bloom.h seb_dev_pack_residues6) in a uint8 buffer:
+    64-key blocks of 384 bytes, so key ranges that start at a multiple of 64 are byte ranges."""
+
+    align = 64
+    block = 384
+
+    def rows(self, n: int) -> int:
+        return -(-n // 64) * self.block
+
+    def span(self, lo: int, hi: int) -> tuple[int, int]:
+        if lo % 64:
+            raise ValueError(f"a 6-byte packed slice must start at a multiple of 64 keys (lo={lo})")
+        return lo // 64 * self.block, -(-hi // 64) * self.block
 
 
 class AllGatherPipeline:
@@ -296,10 +328,13 @@ class KeyFilterGrid:
     rank: int
     world: int
     groups: int
+    align: int = 1  # key shards start at multiples of this (64: the 6-byte packed form's blocks)
 
     def __post_init__(self):
         if self.groups < 1 or self.world % self.groups:
             raise ValueError(f"{self.groups} key groups do not divide {self.world} ranks")
+        if self.align < 1:
+            raise ValueError("align must be >= 1")
 
     @property
     def slots(self) -> int:
@@ -320,12 +355,18 @@ class KeyFilterGrid:
         """This rank's filters."""
         return FilterShard(self.num_filters, self.slot_of(self.rank), self.slots)
 
+    def _edge(self, n: int, g: int) -> int:
+        a = self.align
+        return min(n, -(-(n * g // self.groups) // a) * a)
+
     def key_bounds(self, n: int, g: int) -> tuple[int, int]:
-        return n * g // self.groups, n * (g + 1) // self.groups
+        return self._edge(n, g), self._edge(n, g + 1)
 
     def width(self, n: int) -> int:
-        """Rows of the largest key shard (every shard fits a buffer of this many rows)."""
-        return -(-n // self.groups)
+        """Keys of the largest key shard (every shard fits a buffer of this many keys)."""
+        if self.align == 1:
+            return -(-n // self.groups)
+        return max(1, max(hi - lo for lo, hi in (self.key_bounds(n, g) for g in range(self.groups))))
 
     def filter_lo(self, r: int) -> int:
         return FilterShard.bounds(self.num_filters, self.slots, self.slot_of(r))[0]
@@ -353,15 +394,22 @@ class GridExchange:
     (the collective path's equal pieces; receivers ignore the rows past their shard)."""
 
     def __init__(self, grid: KeyFilterGrid, n: int, row_shape: tuple, dtype, device, nbufs: int = 1,
-                 mode: str = "p2p", group=None):
+                 mode: str = "p2p", group=None, layout: RowLayout | None = None):
         if mode not in ("p2p", "collective"):
             raise ValueError(mode)
+        self.layout = layout or RowLayout()
+        if grid.align % self.layout.align:
+            raise ValueError(f"the grid's key shards (align {grid.align}) must start on the layout's "
+                             f"boundaries (align {self.layout.align})")
         self.grid, self.n, self.mode, self.group = grid, n, mode, group
         self.rank, self.world = grid.rank, grid.world
         self.lo, self.hi = grid.key_bounds(n, grid.group)
         self.width = grid.width(n)
         self.pdtype = grid.shard.plane_dtype()
-        rows = n + grid.groups if self.rank == 0 else self.width
+        L = self.layout
+        self.piece_rows = L.rows(self.width)  # rows of one equal-width piece (the collective transport)
+        rows = (max(L.span(*grid.key_bounds(n, g))[0] for g in range(grid.groups)) + self.piece_rows + grid.groups
+                if self.rank == 0 else self.piece_rows)
         self.bufs = [torch.zeros((rows, *row_shape), dtype=dtype, device=device) for _ in range(nbufs)]
         self.direct = mode == "p2p" and grid.slots == 1 and self.pdtype == torch.int64
         self.masks = ([torch.zeros(max(n, 1), dtype=torch.int64, device=device) for _ in range(2)]
@@ -374,10 +422,16 @@ class GridExchange:
 
     # ---------------------------------------------------------------- views of one batch ----
     def shard_view(self, buf: torch.Tensor) -> torch.Tensor:
-        """This rank's keys of the batch in `buf` (root: its own shard of the whole batch)."""
+        """The rows of this rank's keys of the batch in `buf` (root: its own shard of the whole
+        batch); they hold `shard_keys` keys."""
         if self.rank == 0:
-            return buf[self.lo: self.hi]
-        return buf[: self.hi - self.lo]
+            a, b = self.layout.span(self.lo, self.hi)
+            return buf[a:b]
+        return buf[: self.layout.rows(self.hi - self.lo)]
+
+    @property
+    def shard_keys(self) -> int:
+        return self.hi - self.lo
 
     def plane(self, j: int) -> torch.Tensor:
         """Where this rank's probe of step j writes its plane (hi - lo keys)."""
@@ -392,8 +446,9 @@ class GridExchange:
     def _pieces(self, buf: torch.Tensor) -> list:
         out = []
         for r in range(self.world):
-            lo, _ = self.grid.key_bounds(self.n, self.grid.group_of(r))
-            out.append(buf[lo: lo + self.width])
+            lo, hi = self.grid.key_bounds(self.n, self.grid.group_of(r))
+            a, _ = self.layout.span(lo, hi)
+            out.append(buf[a: a + self.piece_rows])
         return out
 
     def exchange(self, send_buf: torch.Tensor | None, recv_buf: torch.Tensor | None, plane_step: int | None) -> list:
@@ -408,9 +463,11 @@ class GridExchange:
                     for r in range(1, self.world):
                         lo, hi = self.grid.key_bounds(self.n, self.grid.group_of(r))
                         if hi > lo:
-                            ops.append(dist.P2POp(dist.isend, send_buf[lo:hi], r, group=self.group))
+                            a, b = self.layout.span(lo, hi)
+                            ops.append(dist.P2POp(dist.isend, send_buf[a:b], r, group=self.group))
                 elif self.hi > self.lo:
-                    ops.append(dist.P2POp(dist.irecv, recv_buf[: self.hi - self.lo], 0, group=self.group))
+                    ops.append(dist.P2POp(dist.irecv, recv_buf[: self.layout.rows(self.hi - self.lo)], 0,
+                                          group=self.group))
             if plane_step is not None:
                 if self.rank == 0:
                     for r in range(1, self.world):
@@ -431,7 +488,7 @@ class GridExchange:
                     self._root_piece = torch.empty_like(pieces[0])
                 mine = self._root_piece
             else:
-                mine = recv_buf[: self.width]
+                mine = recv_buf[: self.piece_rows]
             works.append(dist.scatter(mine, scatter_list=pieces, src=0, group=self.group, async_op=True))
         if plane_step is not None:
             src = self.planes[plane_step % 2] if self.planes is not None else None
@@ -533,3 +590,32 @@ class GridPipeline:
 
     def drain(self) -> None:
         self._wait_through(max(self.works, default=-1))
+
+
+def c5_rank_plan(n: int, world: int, rank: int, form: str, width: int, num_filters: int = 64) -> dict:
+    """What one rank of the N > 1 C5 step does with one batch, from the same helpers the bench's
+    setups use (bench.py setup_c5 / setup_c5_2d): the keys it packs, the keys and filters it probes,
+    and the batch bytes it sends and receives per step (`width` = bytes per packed key, 6 or 8;
+    planes not counted).  form: "root" (rank 0 packs and broadcasts the batch), "spread" (every
+    rank packs its 1/N, all-gather) or "grid" (R = N key groups, rank 0 sends each its shard)."""
+    lay = Packed6Layout() if width == 6 else RowLayout()
+    unit = 1 if width == 6 else width  # bytes per buffer row
+    if form == "grid":
+        grid = KeyFilterGrid(num_filters, rank, world, world, align=lay.align)
+        lo, hi = grid.key_bounds(n, grid.group)
+        shard_rows = [lay.rows(grid.key_bounds(n, g)[1] - grid.key_bounds(n, g)[0]) * unit for g in range(world)]
+        return {"rank": rank, "form": form, "pack_keys": n if rank == 0 else 0, "probe_keys": hi - lo,
+                "filters": grid.shard.count, "send_bytes": sum(shard_rows[1:]) if rank == 0 else 0,
+                "recv_bytes": 0 if rank == 0 else shard_rows[rank]}
+    shard = FilterShard(num_filters, rank, world)
+    total = lay.rows(n) * unit
+    if form == "root":
+        return {"rank": rank, "form": form, "pack_keys": n if rank == 0 else 0, "probe_keys": n,
+                "filters": shard.count, "send_bytes": total if rank == 0 else 0,
+                "recv_bytes": 0 if rank == 0 else total}
+    if form != "spread":
+        raise ValueError(form)
+    lo, hi, w = spread_bounds(n, world, rank, align=lay.align)
+    part = lay.rows(w) * unit
+    return {"rank": rank, "form": form, "pack_keys": hi - lo, "probe_keys": n, "filters": shard.count,
+            "send_bytes": part, "recv_bytes": part * (world - 1)}

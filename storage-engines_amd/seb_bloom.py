@@ -121,6 +121,9 @@ _SIGS = {
     "seb_dev_probe_packed": (_i, [_vp, _u64, _vp, _u64, _u32, _vp, _vp]),
     "seb_dev_probe_emit_packed": (_i, [C.POINTER(seb_keys), _vp, _u64, _u32, _vp, _vp, _vp]),
     "seb_dev_probe_multi_packed": (_i, [_vp, _u64, C.POINTER(seb_filter_ref), _u32, _vp, _u32, _vp]),
+    "seb_packed6_bytes": (_u64, [_u64]),
+    "seb_dev_pack_residues6": (_i, [C.POINTER(seb_keys), _u64, _u32, _vp, _vp]),
+    "seb_dev_probe_multi_packed6": (_i, [_vp, _u64, C.POINTER(seb_filter_ref), _u32, _vp, _u32, _vp]),
     "seb_timer_create": (_i, [C.POINTER(_vp)]),
     "seb_timer_record": (_i, [_vp, _vp]),
     "seb_timer_elapsed_ms": (_i, [_vp, _vp, C.POINTER(C.c_float)]),
@@ -541,6 +544,32 @@ def dev_probe_multi_packed(packed, n: int, filters: list[tuple[object, int, int]
     refs = (seb_filter_ref * len(filters))(*[seb_filter_ref(w.data_ptr(), m, k, 0) for w, m, k in filters])
     check(lib().seb_dev_probe_multi_packed(packed.data_ptr(), n, refs, len(filters), mask.data_ptr(),
                                            mask.element_size(), _stream(stream)))
+
+
+PACK6_BITS = 21      # narrow packed residues: m < 2^21 (include/seb_bloom.h)
+PACK6_BLOCK = 384    # bytes per 64-key block (64 u32 low words + 64 u16 high halves)
+
+
+def packed6_bytes(n: int) -> int:
+    """Bytes of an n-key batch of 6-byte packed residues (whole 64-key blocks)."""
+    return -(-n // 64) * PACK6_BLOCK
+
+
+def pack6_supported(m: int, k: int) -> bool:
+    return k == 7 and 0 < m < (1 << PACK6_BITS)
+
+
+def dev_pack_residues6(keys: seb_keys, m: int, k: int, packed6, stream=None) -> None:
+    """6-byte packed residues per key in 64-key blocks (k == 7, m < 2^21): a quarter fewer bytes
+    than dev_pack_residues for the batch a compaction-sized filter set shares."""
+    check(lib().seb_dev_pack_residues6(C.byref(keys), m, k, packed6.data_ptr(), _stream(stream)))
+
+
+def dev_probe_multi_packed6(packed6, n: int, filters: list[tuple[object, int, int]], mask, stream=None) -> None:
+    """dev_probe_multi over 6-byte packed residues (filters of one (m, k); k == 7, m < 2^21)."""
+    refs = (seb_filter_ref * len(filters))(*[seb_filter_ref(w.data_ptr(), m, k, 0) for w, m, k in filters])
+    check(lib().seb_dev_probe_multi_packed6(packed6.data_ptr(), n, refs, len(filters), mask.data_ptr(),
+                                            mask.element_size(), _stream(stream)))
 
 
 def dev_probe_multi(keys: seb_keys, filters: list[tuple[object, int, int]], mask, stream=None) -> None:

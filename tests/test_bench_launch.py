@@ -42,6 +42,56 @@ def test_gpus_n_spawns_n_ranks(n):
         assert r["device"] is None and r["local_rank"] == r["rank"] and r["host"]
         assert set(r) >= {"kernel_ms", "wait_ms", "wait_host_ms", "elapsed_s"}
     assert d["devices"] == 0 and d["problems"] == []
+    # the default N > 1 line: the headline's batch broadcast from rank 0 (the
+    # north star's form), then in the same processes its all-gather and resident forms and C5 in
+    # its three forms (north star configs[4])
+    assert [(v["key"], v["config"]) for v in d["variants"]] == [
+        ("all_gather_spread", "c2c3"), ("resident_batch", "c2c3"), ("c5", "c5"), ("c5_spread", "c5"),
+        ("c5_2d", "c5_2d")]
+    assert d["variants"][2]["overrides"]["batch_origin"] == "root"
+    assert d["variants"][3]["overrides"]["batch_origin"] == "spread"
+    # each form's batch, 6-byte packed residues of the 10M keys: every rank probes every key
+    # against its 64/N filters (root, spread) or its 1/N of the keys against all 64 (grid)
+    keys, blk = 10_000_000, 384
+    plans = {f: [r["c5_plan"][i] for r in recs] for i, f in enumerate(("root", "spread", "grid"))}
+    for f, rows in plans.items():
+        assert [p["rank"] for p in rows] == list(range(n)) and all(p["form"] == f for p in rows)
+    total = -(-keys // 64) * blk  # 60 MB: 6 B per key in 64-key blocks
+    assert sum(p["filters"] for p in plans["root"]) == 64
+    assert plans["root"][0]["pack_keys"] == keys and all(p["pack_keys"] == 0 for p in plans["root"][1:])
+    assert plans["root"][0]["send_bytes"] == total and all(p["recv_bytes"] == total for p in plans["root"][1:])
+    assert all(p["probe_keys"] == keys for p in plans["root"] + plans["spread"])
+    assert sum(p["pack_keys"] for p in plans["spread"]) == keys
+    assert all(p["send_bytes"] % blk == 0 and p["recv_bytes"] == p["send_bytes"] * (n - 1) for p in plans["spread"])
+    assert sum(p["probe_keys"] for p in plans["grid"]) == keys and all(p["filters"] == 64 for p in plans["grid"])
+    assert plans["grid"][0]["send_bytes"] == sum(p["recv_bytes"] for p in plans["grid"][1:])
+    assert all(p["recv_bytes"] % blk == 0 for p in plans["grid"])
+
+
+def test_c5_plan_alignment():
+    """The 6-byte form's slices start at multiples of 64 keys at every world size the driver runs;
+    the 8-byte form keeps key-granular slices."""
+    sys.path.insert(0, os.path.join(ROOT, "storage-engines_amd"))
+    import dist_probe as dp
+
+    for world in (2, 3, 4, 8):
+        for n in (10_000_000, 1_000_003, 130):
+            spread = [dp.spread_bounds(n, world, r, align=64) for r in range(world)]
+            assert spread[0][0] == 0 and spread[-1][1] == n
+            assert all((lo % 64 == 0 or lo == n) and hi >= lo for lo, hi, _ in spread)
+            assert all(a[1] == b[0] for a, b in zip(spread, spread[1:]))
+            g = [dp.KeyFilterGrid(64, r, world, world, align=64) for r in range(world)]
+            bounds = [g[0].key_bounds(n, x) for x in range(world)]
+            assert bounds[0][0] == 0 and bounds[-1][1] == n and all(lo % 64 == 0 or lo == n for lo, _ in bounds)
+            assert g[0].width(n) == max(hi - lo for lo, hi in bounds)
+            for r in range(world):
+                p = dp.c5_rank_plan(n, world, r, "spread", 8)
+                lo, hi, w = dp.spread_bounds(n, world, r)
+                assert p["pack_keys"] == hi - lo and p["send_bytes"] == 8 * w
+    lay = dp.Packed6Layout()
+    assert lay.span(128, 200) == (768, 1536) and lay.rows(65) == 768
+    with pytest.raises(ValueError):
+        lay.span(1, 64)
 
 
 def test_rank_report_summary():

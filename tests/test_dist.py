@@ -12,6 +12,7 @@ import torch.multiprocessing as mp
 
 import dist_probe as dp
 import keygen as kg
+from oracle import bloom_np as bnp
 from oracle import oracle_c as oc
 
 
@@ -395,18 +396,152 @@ def test_grid_probe_matches_oracle(world, nf, groups, mode):
     assert np.all(((ref[0::2] >> owner[0::2].astype(np.uint64)) & np.uint64(1)) == 1)
 
 
-def _grid_pipe_worker(rank, world, port, nf, per, nprobe, groups, mode, steps, q):
+def _pack6(keys: np.ndarray, m: int) -> np.ndarray:
+    """Test-side seb_dev_pack_residues6 (include/seb_bloom.h): each key's r0 = hash1 mod m,
+    b = hash2 mod m and the 6 wrap flags of hash1 + q*hash2 (lsm/bloom.go:58-67) as 21/21/6-bit
+    fields, in 64-key blocks of 64 u32 low words then 64 u16 high halves."""
+    n = keys.shape[0]
+    h1, h2 = bnp.fnv_fixed(keys)
+    flags = np.zeros(n, np.uint64)
+    x = h1.copy()
+    with np.errstate(over="ignore"):
+        for q in range(1, 7):
+            xn = x + h2
+            flags |= (xn < x).astype(np.uint64) << np.uint64(q - 1)
+            x = xn
+    v = (h1 % np.uint64(m)) | ((h2 % np.uint64(m)) << np.uint64(21)) | (flags << np.uint64(42))
+    nb = -(-n // 64)
+    vv = np.zeros(nb * 64, np.uint64)
+    vv[:n] = v
+    vv = vv.reshape(nb, 64)
+    out = np.zeros((nb, 384), np.uint8)
+    out[:, :256] = (vv & np.uint64(0xFFFFFFFF)).astype("<u4").view(np.uint8).reshape(nb, 256)
+    out[:, 256:] = (vv >> np.uint64(32)).astype("<u2").view(np.uint8).reshape(nb, 128)
+    return out.ravel()
+
+
+def _oracle_probe6_fn(rows: torch.Tensor, n: int, local_filters, plane: torch.Tensor) -> None:
+    """The multi-filter MayContain of a 6-byte packed batch (`rows`, n keys) against the oracle's
+    filter bytes: bit f of plane[i] = every one of key i's 7 positions set in filter f."""
+    blocks = rows.numpy()[: -(-n // 64) * 384].reshape(-1, 384)
+    lo = blocks[:, :256].copy().view("<u4").astype(np.uint64).ravel()[:n]
+    hi = blocks[:, 256:].copy().view("<u2").astype(np.uint64).ravel()[:n]
+    v = lo | (hi << np.uint64(32))
+    mask = np.zeros(n, np.int64)
+    for f, (bits, m, k) in enumerate(local_filters):
+        assert k == 7
+        c = (1 << 64) % m
+        r = (v & np.uint64((1 << 21) - 1)).astype(np.int64)
+        b = ((v >> np.uint64(21)) & np.uint64((1 << 21) - 1)).astype(np.int64)
+        fl = (v >> np.uint64(42)).astype(np.int64)
+        ok = (bits[r >> 3] >> (r & 7)) & 1
+        for q in range(1, 7):
+            r = (r + b - c * ((fl >> (q - 1)) & 1)) % m
+            ok &= (bits[r >> 3] >> (r & 7)) & 1
+        mask |= ok.astype(np.int64) << f
+    plane.copy_(torch.from_numpy(mask).to(plane.dtype))
+
+
+def _c5_origin_worker(rank, world, port, origin, nf, per, nprobe, steps, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        grid = dp.KeyFilterGrid(nf, rank, world, groups)
+        m, _ = oc.params(per, 0.01)
+        shard = dp.FilterShard(nf, rank, world)
+        local = _filters(nf, per)[shard.lo: shard.hi]
+        lay, lead = dp.Packed6Layout(), 2
+        if origin == "root":  # rank 0 packs every batch and broadcasts it (bench.py c5, the default)
+            bufs = [torch.zeros(lay.rows(nprobe), dtype=torch.uint8) for _ in range(lead + 1)]
+
+            def produce(b, buf):
+                buf[: lay.rows(nprobe)].copy_(torch.from_numpy(_pack6(_c5_batch(nf, per, nprobe, salt=b), m)))
+
+            pipe = dp.BroadcastPipeline(bufs, lead, rank, produce=produce)
+        else:  # every rank packs its 64-key-aligned slice, all-gathered (bench.py c5 --batch-origin spread)
+            lo, hi, width = dp.spread_bounds(nprobe, world, rank, align=lay.align)
+            bufs = [torch.zeros(lay.rows(width) * world, dtype=torch.uint8) for _ in range(lead + 1)]
+
+            def produce(b, part):
+                if hi > lo:
+                    part[: lay.rows(hi - lo)].copy_(torch.from_numpy(_pack6(_c5_batch(nf, per, nprobe, salt=b)[lo:hi], m)))
+
+            pipe = dp.AllGatherPipeline(bufs, lead, rank, world, produce=produce)
+        pipe.prologue()
+        plane = torch.zeros(nprobe, dtype=shard.plane_dtype())
+        planes = [torch.empty_like(plane) for _ in range(world)]
+        got = {}
+        for j in range(steps):
+            buf = pipe.acquire(j)
+            target = pipe.target(j)
+            if target is not None:
+                produce(j + lead, target)
+            plane.zero_()
+            if shard.count:
+                _oracle_probe6_fn(buf, nprobe, local, plane)
+            dist.gather(dp.comm_view(plane), gather_list=[dp.comm_view(p) for p in planes] if rank == 0 else None,
+                        dst=0)
+            if rank == 0:
+                got[j] = dp.assemble_mask(planes, nf)
+            pipe.end_step(j)
+        pipe.drain()
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,origin", [(2, "root"), (3, "root"), (2, "spread"), (3, "spread")])
+def test_c5_packed6_both_origins(world, origin):
+    """bench.py's C5 at N > 1: a new batch every step as 6-byte packed
+    residues, broadcast from rank 0 or spread over the ranks in 64-key-aligned slices and
+    all-gathered; each rank probes its filters, the planes gathered to rank 0 equal the oracle's
+    masks for that step's batch (a batch that is not a multiple of 64 keys)."""
+    nf, per, nprobe, steps = 8, 1500, 1201, 5
+    results = _run(_c5_origin_worker, world, origin, nf, per, nprobe, steps)
+    filters = _filters(nf, per)
+    got = results[0]
+    assert sorted(got) == list(range(steps))
+    for j in range(steps):
+        ref = oc.probe_multi(filters, _c5_batch(nf, per, nprobe, salt=j), nprobe, stride=16)
+        assert np.array_equal(got[j], ref), j
+
+
+def test_pack6_layout_matches_8_byte_fields():
+    """The test-side 6-byte packer's fields are the 8-byte form's (the _batch words above)."""
+    n = 130
+    m, _ = oc.params(10_000, 0.01)
+    w8 = _batch(0, n).numpy().view(np.uint64)
+    buf = _pack6(kg.key16(np.arange(n)), m).reshape(-1, 384)
+    lo = buf[:, :256].copy().view("<u4").astype(np.uint64).ravel()[:n]
+    hi = buf[:, 256:].copy().view("<u2").astype(np.uint64).ravel()[:n]
+    w6 = lo | (hi << np.uint64(32))
+    f21, f29 = np.uint64((1 << 21) - 1), np.uint64((1 << 29) - 1)
+    assert np.array_equal(w6 & f21, w8 & f29)
+    assert np.array_equal((w6 >> np.uint64(21)) & f21, (w8 >> np.uint64(29)) & f29)
+    assert np.array_equal(w6 >> np.uint64(42), w8 >> np.uint64(58))
+
+
+def _grid_pipe_worker(rank, world, port, nf, per, nprobe, groups, mode, steps, pack6, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lay = dp.Packed6Layout() if pack6 else dp.RowLayout()
+        grid = dp.KeyFilterGrid(nf, rank, world, groups, align=lay.align)
         local = _filters(nf, per)[grid.shard.lo: grid.shard.hi]
         lead = 2
-        ex = dp.GridExchange(grid, nprobe, (16,), torch.uint8, "cpu", nbufs=lead + 1, mode=mode)
+        m, _ = oc.params(per, 0.01)
+        if pack6:  # bench.py c5_2d at N > 1: 6-byte packed residues in a byte buffer
+            ex = dp.GridExchange(grid, nprobe, (), torch.uint8, "cpu", nbufs=lead + 1, mode=mode, layout=lay)
+        else:
+            ex = dp.GridExchange(grid, nprobe, (16,), torch.uint8, "cpu", nbufs=lead + 1, mode=mode)
 
         def produce(b, buf):
-            buf[:nprobe].copy_(torch.from_numpy(_c5_batch(nf, per, nprobe, salt=b)))
+            batch = _c5_batch(nf, per, nprobe, salt=b)
+            if pack6:
+                buf[: lay.rows(nprobe)].copy_(torch.from_numpy(_pack6(batch, m)))
+            else:
+                buf[:nprobe].copy_(torch.from_numpy(batch))
 
         pipe = dp.GridPipeline(ex, lead=lead, produce=produce)
         pipe.prologue()
@@ -419,8 +554,11 @@ def _grid_pipe_worker(rank, world, port, nf, per, nprobe, groups, mode, steps, q
                 produce(j + lead, pipe.root_target(j))
             plane = ex.plane(j)
             plane.zero_()
-            if grid.shard.count and shard.shape[0]:
-                _oracle_probe_fn(shard, local, plane)
+            if grid.shard.count and ex.shard_keys:
+                if pack6:
+                    _oracle_probe6_fn(shard, ex.shard_keys, local, plane)
+                else:
+                    _oracle_probe_fn(shard, local, plane)
             pipe.end_step(j)
         pipe.drain()
         if rank == 0:
@@ -431,13 +569,16 @@ def _grid_pipe_worker(rank, world, port, nf, per, nprobe, groups, mode, steps, q
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,groups,mode", [(2, 2, "p2p"), (3, 3, "collective"), (2, 1, "p2p")])
-def test_grid_pipeline_each_step_its_own_batch(world, groups, mode):
+@pytest.mark.parametrize("world,groups,mode,pack6", [(2, 2, "p2p", False), (3, 3, "collective", False),
+                                                    (2, 1, "p2p", False), (2, 2, "collective", True),
+                                                    (3, 3, "collective", True), (2, 2, "p2p", True)])
+def test_grid_pipeline_each_step_its_own_batch(world, groups, mode, pack6):
     """bench.py c5_2d's pipelined exchange (dist_probe.GridPipeline): a new batch every step, its
     shards sent two steps ahead while the planes of the step before come back; the root's masks
-    of every step equal the oracle's for that step's batch."""
+    of every step equal the oracle's for that step's batch.  pack6: the batch as 6-byte packed
+    residues (64-key-aligned shards of a byte buffer, dist_probe.Packed6Layout), as at N > 1."""
     nf, per, nprobe, steps = 8, 1500, 1201, 6
-    results = _run(_grid_pipe_worker, world, nf, per, nprobe, groups, mode, steps)
+    results = _run(_grid_pipe_worker, world, nf, per, nprobe, groups, mode, steps, pack6)
     filters = _filters(nf, per)
     got = results[0]
     assert sorted(got) == list(range(steps))

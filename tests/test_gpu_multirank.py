@@ -7,9 +7,10 @@ transfer through host memory); only `parity` is asserted.
     planes gathered to rank 0; its resident_batch secondary broadcasts the batch once;
   * c5_2d (dist_probe.KeyFilterGrid): key groups x filter slots, shards sent and planes returned
     in one exchange per step (the collective transport under gloo);
-  * c2c3 (the headline): a filter per rank, a new packed batch in every step, spread over the
-    ranks and all-gathered (default), or broadcast from rank 0 (its root_broadcast secondary and
-    --batch-origin root); the resident_batch secondary broadcasts one batch once.
+  * c2c3 (the headline): a filter per rank, a new packed batch in every step, broadcast from
+    rank 0 (default) or spread over the ranks and all-gathered (its all_gather_spread secondary
+    and --batch-origin spread); the resident_batch secondary broadcasts one batch once; then C5
+    in its three forms (c5, c5_spread, c5_2d) as the default line's same-process variants.
 """
 import json
 import os
@@ -44,11 +45,27 @@ def _bench(*args, timeout=170):
     return d
 
 
+def _variant_ok(v, n_ranks=2):
+    assert v["parity"].startswith("bit-exact"), v
+    assert v["value"] > 0 and v["ms_per_step"] > 0
+    assert v["roofline"]["achieved"] > 0 and v["roofline"]["algorithmic_bytes_per_launch"] > 0
+    assert [r["rank"] for r in v["per_rank"]] == list(range(n_ranks))
+    assert all(r["wait_ms"] is not None and r["kernel_ms"] for r in v["per_rank"]), v["per_rank"]
+
+
 def test_c5_filter_split_two_ranks():
     d = _bench("--config", "c5")
     assert d["n_gpus"] == 2
     assert d["parity"].startswith("bit-exact"), d["parity"]
+    assert "6-B packed residues" in d["config"]["workload"]
+    _variant_ok(d["c5_spread"])
     assert d["resident_batch"]["parity"].startswith("bit-exact"), d["resident_batch"]
+
+
+def test_c5_8_byte_batch_two_ranks():
+    d = _bench("--config", "c5", "--pack6", "0", "--no-secondary")
+    assert d["parity"].startswith("bit-exact"), d["parity"]
+    assert "8-B packed residues" in d["config"]["workload"]
 
 
 @pytest.mark.parametrize("groups", [2, 1])
@@ -57,19 +74,26 @@ def test_c5_2d_grid_two_ranks(groups):
     assert d["n_gpus"] == 2
     assert d["parity"].startswith("bit-exact"), d["parity"]
     assert f"key groups {groups}" in d["config"]["parallelism"]
+    assert "6-B packed residues" in d["config"]["workload"]
 
 
 def test_c2c3_spread_batch_per_step_two_ranks():
-    d = _bench("--config", "c2c3")
+    """The default N > 1 line: the headline's batch broadcast from rank 0 every step (the north
+    star's form), then in the same processes its all-gather and resident forms and the north
+    star's C5 in its three forms, every one bit-exact with per-rank waits."""
+    d = _bench("--config", "c2c3", timeout=420)
     assert d["n_gpus"] == 2
     assert d["parity"].startswith("bit-exact"), d["parity"]
-    assert "all-gather" in d["config"]["workload"] and "all-gathered" in d["config"]["parallelism"]
-    assert d["root_broadcast"]["parity"].startswith("bit-exact"), d["root_broadcast"]
+    assert "RCCL-broadcast from rank 0 in every step" in d["config"]["workload"]
+    for key in ("all_gather_spread", "c5", "c5_spread", "c5_2d"):
+        _variant_ok(d[key])
+    assert "all-gather" in d["all_gather_spread"]["workload"]
+    assert d["c5"]["scaling"] == "strong" and "6-B packed" in d["c5"]["workload"]
     assert d["resident_batch"]["parity"].startswith("bit-exact"), d["resident_batch"]
 
 
 def test_c2c3_broadcast_per_step_two_ranks():
-    d = _bench("--config", "c2c3", "--batch-origin", "root", "--no-secondary")
+    d = _bench("--config", "c2c3", "--batch-origin", "spread", "--no-secondary")
     assert d["n_gpus"] == 2
     assert d["parity"].startswith("bit-exact"), d["parity"]
-    assert "RCCL-broadcast from rank 0 in every step" in d["config"]["workload"]
+    assert "all-gather" in d["config"]["workload"] and "all-gathered" in d["config"]["parallelism"]

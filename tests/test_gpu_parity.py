@@ -394,6 +394,87 @@ def test_multi_packed_matches_multi(seb, golden, torch_cuda):
                                    torch.zeros(nn, dtype=torch.int16, device="cuda"))
 
 
+def unpack6(buf: np.ndarray, n: int) -> np.ndarray:
+    """Test-side reading of seb_dev_pack_residues6's 64-key blocks into one 48-bit word per key."""
+    blocks = buf[: -(-n // 64) * 384].reshape(-1, 384)
+    lo = blocks[:, :256].copy().view("<u4").astype(np.uint64)
+    hi = blocks[:, 256:].copy().view("<u2").astype(np.uint64)
+    return (lo | (hi << np.uint64(32))).ravel()[:n]
+
+
+def test_multi_packed6(seb, golden, torch_cuda):
+    """The narrow (6-byte, m < 2^21) packed residues: the same fields as the 8-byte form at 21-bit
+    width, the C5 golden masks from them for 64 filters, an 8-filter ragged batch equal to the
+    oracle (the bytes past the batch untouched), a pre-hashed variable-length batch equal to the
+    probe of its keys, and the cases the narrow form cannot take rejected."""
+    torch = torch_cuda
+    nf, per, n = 64, 100_000, 10_000_000
+    m, k = seb.params(per, 0.01)
+    assert seb.pack6_supported(m, k) and seb.lib().seb_packed6_bytes(n) == seb.packed6_bytes(n) == 60_000_000
+    fkeys = torch.from_numpy(kg.key16(np.arange(nf * per))).cuda()
+    filters = [(seb.new_words(m), m, k) for _ in range(nf)]
+    seb.dev_build_many(seb.dev_keys(fkeys, n=nf * per, stride=16), [j * per for j in range(nf + 1)], filters)
+    q = np.arange(n, dtype=np.int64)
+    half = q // 2
+    pk = seb.dev_keys(torch.from_numpy(kg.key16(np.where(q % 2 == 0, (half % nf) * per + half // nf,
+                                                          nf * per + q))).cuda(), n=n, stride=16)
+    p6 = torch.zeros(seb.packed6_bytes(n), dtype=torch.uint8, device="cuda")
+    seb.dev_pack_residues6(pk, m, k, p6)
+    mask = torch.zeros(n, dtype=torch.int64, device="cuda")
+    seb.dev_probe_multi_packed6(p6, n, filters, mask)
+    p8 = torch.zeros(n, dtype=torch.int64, device="cuda")
+    seb.dev_pack_residues(pk, m, k, p8)
+    torch.cuda.synchronize()
+    assert sha(mask.cpu().numpy().view(np.uint64).astype("<u8").tobytes()) == golden["c5"]["mask_sha256"]
+    # field by field against the 8-byte words (r0 | b << 29 | carries << 58)
+    w6, w8 = unpack6(p6.cpu().numpy(), n), p8.cpu().numpy().view(np.uint64)
+    f21, f29 = np.uint64((1 << 21) - 1), np.uint64((1 << 29) - 1)
+    assert np.array_equal(w6 & f21, w8 & f29)
+    assert np.array_equal((w6 >> np.uint64(21)) & f21, (w8 >> np.uint64(29)) & f29)
+    assert np.array_equal(w6 >> np.uint64(42), w8 >> np.uint64(58))
+    # 8 filters, u8 masks, a ragged batch (not a multiple of 64 keys) against the oracle
+    nn = 100_003
+    sub = filters[:8]
+    keys8 = kg.key16(np.where(q[:nn] % 2 == 0, (half[:nn] % 8) * per + half[:nn] // 8, nf * per + q[:nn]))
+    pk8 = seb.dev_keys(torch.from_numpy(keys8).cuda(), n=nn, stride=16)
+    b6 = torch.full((seb.packed6_bytes(nn) + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    seb.dev_pack_residues6(pk8, m, k, b6)
+    host = [(seb.words_to_bits(w, m), m, k) for w, m, k in sub]
+    ref = oc.probe_multi(host, keys8, nn, stride=16)
+    m8 = torch.full((nn + 1,), 7, dtype=torch.uint8, device="cuda")
+    seb.dev_probe_multi_packed6(b6, nn, sub, m8)
+    torch.cuda.synchronize()
+    got = m8.cpu().numpy()
+    assert np.array_equal(got[:nn].astype(np.uint64), ref)
+    assert got[nn] == 7
+    assert (b6.cpu().numpy()[seb.packed6_bytes(nn):] == 0xA5).all()
+    # a variable-length batch (pre-hashed on the device first) gives the masks of its keys
+    nv = 70_001
+    vd, vo = kg.varlen_keys(np.arange(nv))
+    vkd = seb.dev_keys(torch.from_numpy(vd).cuda(), torch.from_numpy(vo.view(np.int64)).cuda())
+    v6 = torch.zeros(seb.packed6_bytes(nv), dtype=torch.uint8, device="cuda")
+    seb.dev_pack_residues6(vkd, m, k, v6)
+    mv6 = torch.zeros(nv, dtype=torch.int64, device="cuda")
+    seb.dev_probe_multi_packed6(v6, nv, filters, mv6)
+    mvk = torch.zeros(nv, dtype=torch.int64, device="cuda")
+    seb.dev_probe_multi(vkd, filters, mvk)
+    torch.cuda.synchronize()
+    assert torch.equal(mv6, mvk)
+    # rejected: m >= 2^21, k != 7, mixed sizes, a misaligned buffer
+    mb, kb = seb.params(300_000, 0.01)
+    assert mb >= 1 << 21
+    with pytest.raises(seb.SebError):
+        seb.dev_pack_residues6(pk8, mb, kb, b6)
+    with pytest.raises(seb.SebError):
+        seb.dev_pack_residues6(pk8, m, 5, b6)
+    m2, k2 = seb.params(per + 1, 0.01)
+    with pytest.raises(seb.SebError):
+        seb.dev_probe_multi_packed6(b6, nn, sub + [(seb.new_words(m2), m2, k2)], torch.zeros(nn, dtype=torch.int16,
+                                                                                           device="cuda"))
+    with pytest.raises(seb.SebError):
+        seb.dev_probe_multi_packed6(b6[1:], nn, sub, m8)
+
+
 def unpack_positions(packed: np.ndarray, m: int) -> np.ndarray:
     """Test-side decoding of seb_dev_pack_residues' words into the 7 positions (the recurrence
     of for_positions, in Python integers)."""
