@@ -275,24 +275,60 @@ int oracle_build_mt_atomic(uint8_t *bits, uint64_t m, uint32_t k, const uint8_t 
     return run_mt(build_worker, b, n, threads);
 }
 
-/* SURVEY.md 8(d)(ii)'s multi-threaded build: per-thread private filters OR-merged.  Each thread
- * allocates a zeroed private filter (NewBloomFilter's make, lsm/bloom.go:34-37, first touched by
- * its own thread), runs the scalar Add loop (lsm/bloom.go:70-77) over its contiguous key shard,
- * and after a barrier ORs byte range t of every private filter into `bits` (so the merge reads
- * T filters once, split over the T threads).  OR is commutative, so the result equals the
- * sequential build's. */
+/* SURVEY.md 8(d)(ii)'s multi-threaded build: private filters OR-merged, at most kMaxPrivate of
+ * them (memory stays <= kMaxPrivate filters at any thread count: never T x 12 MB).  Thread t runs
+ * the scalar Add loop (lsm/bloom.go:70-77) over its contiguous key shard into private filter
+ * t mod P (P = min(T, kMaxPrivate)); a filter shared by several threads takes relaxed atomic byte
+ * ORs, one owned by a single thread plain ones.  After a barrier thread t ORs byte range t of
+ * every private filter into `bits` (the merge reads the P filters once, split over the T
+ * threads).  OR is commutative, so the result equals the sequential build's. */
+enum { kMaxPrivate = 16 };
+
+/* A barrier whose participant count can shrink: when a thread cannot be created the ones already
+ * running are released instead of waiting forever (the call then returns -1). */
+typedef struct {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int expected, arrived;
+    unsigned phase;
+} mt_barrier;
+
+static void bar_wait(mt_barrier *b) {
+    pthread_mutex_lock(&b->mu);
+    const unsigned ph = b->phase;
+    if (++b->arrived >= b->expected) {
+        b->arrived = 0;
+        b->phase++;
+        pthread_cond_broadcast(&b->cv);
+    } else {
+        while (ph == b->phase) pthread_cond_wait(&b->cv, &b->mu);
+    }
+    pthread_mutex_unlock(&b->mu);
+}
+
+static void bar_shrink(mt_barrier *b, int expected) {
+    pthread_mutex_lock(&b->mu);
+    b->expected = expected;
+    if (b->arrived > 0 && b->arrived >= expected) {
+        b->arrived = 0;
+        b->phase++;
+        pthread_cond_broadcast(&b->cv);
+    }
+    pthread_mutex_unlock(&b->mu);
+}
+
 typedef struct {
     mt_job job;
     uint8_t **priv;
-    int t, threads;
+    int t, threads, npriv;
     uint64_t nbytes;
-    pthread_barrier_t *bar;
+    mt_barrier *bar;
     int err;
 } priv_job;
 
 /* A zeroed private filter on 2 MiB pages where the kernel allows them (madvise; 6 TLB entries for
  * a 12 MB filter instead of ~3000, which the random byte ORs would otherwise miss in), first
- * touched by its own thread. */
+ * touched by the thread that allocates it. */
 static uint8_t *private_filter(uint64_t nbytes) {
     const size_t huge = (size_t)2 << 20;
     const size_t size = ((nbytes ? nbytes : 1) + huge - 1) / huge * huge;
@@ -307,24 +343,34 @@ static uint8_t *private_filter(uint64_t nbytes) {
 
 static void *build_private_worker(void *arg) {
     priv_job *j = (priv_job *)arg;
-    uint8_t *mine = private_filter(j->nbytes);
-    j->priv[j->t] = mine;
+    if (j->t < j->npriv) j->priv[j->t] = private_filter(j->nbytes);
+    bar_wait(j->bar);
+    uint8_t *mine = j->priv[j->t % j->npriv];
+    const int shared = j->threads > j->npriv;  /* more threads than filters: filters are shared */
     if (mine) {
         for (uint64_t i = j->job.lo; i < j->job.hi; i++) {
             uint64_t len;
             const uint8_t *key = key_at(j->job.data, j->job.offsets, j->job.stride, i, &len);
-            oracle_add(mine, j->job.m, j->job.k, key, len);
+            if (!shared) {
+                oracle_add(mine, j->job.m, j->job.k, key, len);
+                continue;
+            }
+            const uint64_t h1 = oracle_fnv1a64(key, len), h2 = oracle_fnv1_64(key, len);
+            for (uint32_t q = 0; q < j->job.k; q++) {
+                const uint64_t h = (h1 + (uint64_t)q * h2) % j->job.m;
+                __atomic_fetch_or(&mine[h / 8], (uint8_t)(1u << (h % 8)), __ATOMIC_RELAXED);
+            }
         }
     } else {
         j->err = 1;
     }
-    pthread_barrier_wait(j->bar);
+    bar_wait(j->bar);
     /* merge: this thread's 8-B aligned slice of the byte array, across every private filter */
     const uint64_t words = (j->nbytes + 7) / 8;
     uint64_t lo = words * (uint64_t)j->t / (uint64_t)j->threads * 8;
     uint64_t hi = words * (uint64_t)(j->t + 1) / (uint64_t)j->threads * 8;
     if (hi > j->nbytes) hi = j->nbytes;
-    for (int q = 0; q < j->threads; q++) {
+    for (int q = 0; q < j->npriv; q++) {
         const uint8_t *src = j->priv[q];
         if (!src) continue;
         uint64_t b = lo;
@@ -337,8 +383,8 @@ static void *build_private_worker(void *arg) {
         }
         for (; b < hi; b++) j->job.wbits[b] |= src[b];
     }
-    pthread_barrier_wait(j->bar);
-    free(mine);
+    bar_wait(j->bar);
+    if (j->t < j->npriv) free(j->priv[j->t]);
     return NULL;
 }
 
@@ -348,26 +394,40 @@ int oracle_build_mt(uint8_t *bits, uint64_t m, uint32_t k, const uint8_t *data, 
     if (threads > 256) threads = 256;
     pthread_t tid[256];
     priv_job jobs[256];
-    uint8_t *priv[256];
-    pthread_barrier_t bar;
-    if (pthread_barrier_init(&bar, NULL, (unsigned)threads) != 0) return -1;
+    uint8_t *priv[kMaxPrivate];
+    mt_barrier bar;
+    if (pthread_mutex_init(&bar.mu, NULL) != 0) return -1;
+    if (pthread_cond_init(&bar.cv, NULL) != 0) {
+        pthread_mutex_destroy(&bar.mu);
+        return -1;
+    }
+    bar.expected = threads;
+    bar.arrived = 0;
+    bar.phase = 0;
     const uint64_t nbytes = (m + 7) / 8;
+    const int nprivate = threads < kMaxPrivate ? threads : kMaxPrivate;
     int started = 0, rc = 0;
+    for (int q = 0; q < kMaxPrivate; q++) priv[q] = NULL;
     for (int t = 0; t < threads; t++) {
-        priv[t] = NULL;
         mt_job b = {NULL, bits, m, k, data, offsets, stride, n * (uint64_t)t / (uint64_t)threads,
                     n * (uint64_t)(t + 1) / (uint64_t)threads, NULL};
-        jobs[t] = (priv_job){b, priv, t, threads, nbytes, &bar, 0};
+        jobs[t] = (priv_job){b, priv, t, threads, nprivate, nbytes, &bar, 0};
     }
     for (int t = 0; t < threads; t++) {
-        /* a thread that cannot start leaves the barrier incomplete: abort (checker code only) */
-        if (pthread_create(&tid[t], NULL, build_private_worker, &jobs[t]) != 0) abort();
+        if (pthread_create(&tid[t], NULL, build_private_worker, &jobs[t]) != 0) {
+            /* release the threads already running (their keys and byte ranges are incomplete:
+             * the call fails, never hangs or aborts) */
+            rc = -1;
+            bar_shrink(&bar, t);
+            break;
+        }
         started++;
     }
     for (int t = 0; t < started; t++) {
         pthread_join(tid[t], NULL);
         if (jobs[t].err) rc = -1;
     }
-    pthread_barrier_destroy(&bar);
+    pthread_cond_destroy(&bar.cv);
+    pthread_mutex_destroy(&bar.mu);
     return rc;
 }

@@ -91,7 +91,8 @@ def build(m: int, k: int, data: np.ndarray, n: int, stride: int = 0, offsets: np
     if bits is None:
         bits = np.zeros(max((m + 7) // 8, 1), dtype=np.uint8)
     if threads > 1:
-        lib().oracle_build_mt(_p(bits), m, k, _p(d), _p(off, u64p), stride, n, threads)
+        if lib().oracle_build_mt(_p(bits), m, k, _p(d), _p(off, u64p), stride, n, threads) != 0:
+            raise RuntimeError(f"oracle_build_mt: {threads} threads could not all start or allocate")
     else:
         lib().oracle_build(_p(bits), m, k, _p(d), _p(off, u64p), stride, n)
     return bits[: (m + 7) // 8]

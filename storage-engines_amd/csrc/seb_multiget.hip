@@ -331,9 +331,15 @@ __device__ __forceinline__ void chunk_positions(const uint32_t (&bk)[kMgSteps], 
             const uint64_t bal = __ballot(set);
             peers &= set ? bal : ~bal;
         }
-        uint32_t before = 0;
-        if (b < nb) before = mine[b];  // every lane of the peer group reads before its leader writes
-        if (b < nb && (peers & lt) == 0) mine[b] = before + (uint32_t)__popcll(peers);
+        // the group's lowest lane alone reads and advances the count, and hands the value it read
+        // to its peers: no lane of the group depends on the order of another lane's LDS accesses
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)peers) - 1u;
+        uint32_t got = 0;
+        if (b < nb && lane == leader) {
+            got = mine[b];
+            mine[b] = got + (uint32_t)__popcll(peers);
+        }
+        const uint32_t before = __shfl(got, (int)leader, 64);
         pos[s] = before + (uint32_t)__popcll(peers & lt);
     }
     __syncthreads();

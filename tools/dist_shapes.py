@@ -22,8 +22,7 @@ profiles/PMC_JSON under the keys bench.py's N > 1 setups look up (st.pmc_key):
   c5_spread6@N          c5p6_f(64/N) + per_key_bytes(pack6) x the rank's keys
   c5_2d6@N              c5_2d6_wN + per_key_bytes(pack6) x 10M on rank 0
 FETCH_SIZE correction (MI355X_MICROARCH.md section HBM, tools/summarize_profile.py): + half of each
-16-B-per-lane stream (the 16-B keys read by pack8 / pack6 / emit's phase 0, the packed words
-emit's later phases read as u32x4)."""
+coalesced stream FETCH_SIZE tallies at half (WIDE below)."""
 from __future__ import annotations
 
 import argparse
@@ -140,7 +139,21 @@ def run(reps: int) -> None:
     print(json.dumps({"reps": reps, "shapes": [s for s, _, _ in shapes()], "checked": True}), flush=True)
 
 
-WIDE = {"pack8": 16 * N, "pack6": 16 * N, "emit": 16 * N + 2 * 8 * N}  # 16-B-per-lane streams per call
+# Coalesced streams per call that FETCH_SIZE counts at half: the 16-B-per-lane ones
+# (MI355X_MICROARCH.md section HBM: the keys read by pack8 / pack6 / emit's phase 0, the packed words
+# emit's later phases read as u32x4), and the dense packed-word reads at 8 B (k_probe_c0 over
+# packed words) and 4 + 2 B per lane (the 6-byte form).  Calibration of the narrow widths (the guide
+# leaves them uncalibrated): c5p6_f8 moves 60 MB of packed words + 10 MB of u8 plane + ~2 MB of
+# filters and table, and its FETCH_SIZE + WRITE_SIZE come to 45.8 MB (profiles/r06_dist_shapes.json
+# before this correction): the 60 MB read is tallied at 30.
+WIDE = {"pack8": 16 * N, "pack6": 16 * N, "emit": 16 * N + 2 * 8 * N, "probe8": 8 * N,
+        **{f"c5p6_f{NF // w}": 6 * N for w in WORLDS}}
+
+
+def wide(shape: str) -> int:
+    if shape.startswith("c5_2d6_w"):
+        return 6 * c2d_keys(int(shape.split("_w")[1]))
+    return WIDE.get(shape, 0)
 
 
 def summarize(tag: str, pmc_json: str) -> None:
@@ -196,9 +209,9 @@ def summarize(tag: str, pmc_json: str) -> None:
         ms = dur[s] / max(1, calls_t[s]) / 1e6
         if s.startswith("c5_2d6"):
             f, w, ms = f + tab_f, w + tab_w, ms + tab_ms
-        read = f * 1024 + WIDE.get(s, 0) / 2
+        read = f * 1024 + wide(s) / 2
         per[s] = {"hbm_bytes_per_call": int(read + w * 1024), "read_bytes": int(read), "write_bytes": int(w * 1024),
-                  "fetch_size_kib": f, "write_size_kib": w, "wide_stream_bytes": WIDE.get(s, 0), "ms": round(ms, 4),
+                  "fetch_size_kib": f, "write_size_kib": w, "wide_stream_bytes": wide(s), "ms": round(ms, 4),
                   "calls": {"trace": calls_t[s], "fetch": calls_f[s], "write": calls_w[s]}}
     src_rel = f"profiles/{tag}_shapes.json"
     with open(os.path.join(ROOT, src_rel), "w") as fh:
