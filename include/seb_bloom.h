@@ -96,8 +96,9 @@ int seb_abi_version(void);
  *                     positions placed through fixed per-bucket LDS bins, the claims pipelined
  *                     against the hashing (1, default), or by a counting sort (0)
  *   "multi_interleave" multi-filter probes with shared (m, k): bit-transposed table (0/1)
- *   "multiget_order"  registry MultiGet walks batches of >= 64K keys in key-range order (1, default)
- *                     or batch order (0)
+ *   "multiget_order"  registry MultiGet walks batches of >= 64K keys in key-range order (1, default:
+ *                     aligned 16-B keys sorted by bucket within 2048-key chunks and read through
+ *                     segment tables; 2: moved across the batch by a scatter pass) or batch order (0)
  *   "multiget_l0_group" registry MultiGet tests the L0 files that share (m, k) through one
  *                     bit-interleaved table, one gather per position for all of them (1, default)
  *   "multiget_xcd"    registry MultiGet: the workgroups that share an XCD walk one contiguous eighth of

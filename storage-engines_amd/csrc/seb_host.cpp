@@ -150,7 +150,7 @@ struct OptionDesc {
 static const OptionDesc kOptions[] = {
     SEB_OPT(build_algo, 0, 4),
     SEB_OPT(multi_interleave, 0, 1),
-    SEB_OPT(multiget_order, 0, 1),
+    SEB_OPT(multiget_order, 0, 2),
     SEB_OPT(multiget_l0_group, 0, 1),
     SEB_OPT(multiget_xcd, 0, 1),
     SEB_OPT(varlen_prehash_min_keys, 0, INT64_MAX),
@@ -2121,7 +2121,7 @@ static int multiget_order(seb_registry *r, KeyBatch &kb, uint64_t answer_bytes, 
     *mo = MgOrder{};
     if (!options().multiget_order || r->part_hi <= r->part_lo || kb.n < 65536 || kb.n > 0xffffffffull) return SEB_OK;
     void *ws = nullptr;
-    int rc = cached_workspace(s, multiget_order_bytes(kb, answer_bytes), &ws, 3);
+    int rc = cached_workspace(s, multiget_order_bytes(kb, answer_bytes, r->part_hi - r->part_lo + 1), &ws, 3);
     if (rc == SEB_ERR_NOMEM) {  // the order is only a speed-up: batch order needs no scratch
         t_err.clear();
         return SEB_OK;
@@ -2144,7 +2144,8 @@ static int multiget_launch(seb_registry *r, KeyBatch kb, uint64_t *maybe, uint16
     if ((rc = multiget_order(r, kb, answer_bytes, s, &mo))) return rc;
     HIP_OR_FAIL(launch_multiget(kb, (const RegSlot *)r->dslots.p, r->nslots, mg_layout(r), (const uint8_t *)r->dranges.p,
                                 mo.active ? (maybe ? (uint64_t *)mo.answers : nullptr) : maybe,
-                                mo.active ? (maybe ? nullptr : (uint16_t *)mo.answers) : cand, cap, s, mo.key_order));
+                                mo.active ? (maybe ? nullptr : (uint16_t *)mo.answers) : cand, cap, s, mo.key_order,
+                                mo.seg));
     if (mo.active)
         HIP_OR_FAIL(launch_multiget_unpermute(mo, maybe ? (void *)maybe : (void *)cand, answer_bytes, s));
     return SEB_OK;

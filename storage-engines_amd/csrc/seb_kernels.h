@@ -87,12 +87,21 @@ hipError_t launch_route_partition(const KeyBatch &kb, uint32_t bits, uint32_t *p
                                   uint16_t *shard_out, void *ws, uint64_t ws_bytes, hipStream_t s);
 hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mode, uint32_t *crc, uint8_t *ok,
                           hipStream_t s);
+// The scatter-free order's segment tables (multiget_order 1): segment s = b * C + c is bucket b's
+// run of chunk c; segrow[s] its first sorted row (non-decreasing in s), wstart[w] the segment of
+// row 64 w, cloc[c * nb + b] the run's offset inside the chunk's bucket-sorted keys.
+struct MgSeg {
+    const uint32_t *segrow = nullptr;  // null: rows are read linearly (or through key_order)
+    const uint32_t *wstart = nullptr;
+    const uint16_t *cloc = nullptr;
+    uint32_t nseg = 0, C = 0, nb = 0, pad = 0;
+};
 // cand != null: the list form (cap u16 slots per key, any nslots) instead of masks.
 constexpr uint32_t kRegMaxFiles = 4096;  // registry capacity (u16 slot ids, 0xFFFF = none)
 // Answer j goes to row j of maybe / cand; key_order != null: key j is read as key key_order[j] of kb.
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
                            const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap, hipStream_t s,
-                           const uint32_t *key_order);
+                           const uint32_t *key_order, const MgSeg &seg = MgSeg{});
 // Key-range order for MultiGet: buckets = files of slots [lo, hi) (a disjoint, MinKey-ordered
 // level) with MinKey <= key.  The MultiGet then answers into mo.answers (sorted rows) and
 // launch_multiget_unpermute writes them to the caller's output in batch order.
@@ -107,10 +116,13 @@ struct MgOrder {
     const uint32_t *key_order = nullptr;  // batches that are not moved: key index of each sorted row
     const uint8_t *keys = nullptr;        // aligned fixed 16-B batches: the keys moved into that order
     void *answers = nullptr;              // n * answer_bytes: the MultiGet's answers in sorted rows
+    MgSeg seg;                            // the scatter-free order: keys read through segments
 };
-// Aligned fixed 16-B batches are moved into that order (16 B more per key), others get an index.
+// Aligned fixed 16-B batches are sorted by bucket inside each chunk and read through the segment
+// tables (multiget_order 1) or moved into that order (multiget_order 2; 16 B more per key), others
+// get an index.  nb: the partition level's bucket count (its files + 1).
 bool multiget_order_moves(const KeyBatch &kb);
-uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes);
+uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes, uint32_t nb);
 hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
                                  const uint8_t *ranges, void *ws, MgOrder *mo, hipStream_t s);
 hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answer_bytes, hipStream_t s);
@@ -122,7 +134,9 @@ struct Options {
     int build_algo = 0;           // 0 auto, 1 device-scope atomics, 2 radix-partitioned (bucketed), 3 LDS-resident
                                   // filter (atomic merge), 4 LDS images + OR kernel
     int multi_interleave = 1;     // multi-filter probe: interleaved table when filters share (m, k)
-    int multiget_order = 1;       // MultiGet: probe batches of >= 64K keys in key-range order (1) or batch order (0)
+    int multiget_order = 1;       // MultiGet: probe batches of >= 64K keys in key-range order (1: aligned 16-B keys
+                                  // sorted within chunks and read through segment tables; 2: moved across the
+                                  // batch by a scatter pass, round 5's form) or in batch order (0)
     int multiget_l0_group = 1;    // MultiGet: L0 files of one (m, k) tested through one interleaved table
     int multiget_xcd = 1;         // MultiGet: the blocks sharing an XCD walk one contiguous eighth of the batch
                                   // (1, default: 575 vs 596 us per 10M-key k_multiget on 28 files), or not (0)

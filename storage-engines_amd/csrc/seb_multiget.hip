@@ -91,6 +91,9 @@ __device__ __forceinline__ uint32_t test_l0_group(const RegLayout &lay, uint64_t
     return alive;
 }
 
+struct MgSeg;
+__device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uint64_t j);
+
 // MODE 0: u64 mask, slot table in LDS.  MODE 1: candidate list, slot table in LDS.  MODE 2:
 // candidate list, slot table read from HBM/L2 (more than kMaxSlots files: an LSM past L1 holds
 // hundreds, lsm/levels.go:10-14 with ~4 MB files, lsm/compaction.go:253).  (Testing filters 4 at a
@@ -100,7 +103,7 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                                                   uint32_t nslots, RegLayout lay, const uint8_t *__restrict__ ranges,
                                                   uint64_t *__restrict__ maybe, uint16_t *__restrict__ cand,
                                                   uint32_t cap, const uint32_t *__restrict__ key_order,
-                                                  uint32_t xcd) {
+                                                  uint32_t xcd, MgSeg seg) {
     constexpr bool kLds = MODE < 2, kList = MODE > 0;
     __shared__ RegSlot lslots[kLds ? kMaxSlots : 1];
     if constexpr (kLds) {
@@ -123,12 +126,17 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         const uint32_t q = gridDim.x / 8, r = gridDim.x % 8, x = blockIdx.x % 8;
         wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
     }
-    for (uint64_t j = (uint64_t)wg * blockDim.x + threadIdx.x; j < kb.n; j += stride) {
+    // one iteration per wave-uniform row group (its lanes stay together for mg_seg_key's shuffles)
+    for (uint64_t jw = (uint64_t)wg * blockDim.x + (threadIdx.x & ~63u); jw < kb.n; jw += stride) {
         // Answer j goes to row j.  In key-range order (multiget_order) that is the sorted position:
-        // the keys were moved into that order by k_mg_scatter or are read through key_order, and
-        // k_mg_unpermute brings the answers back to batch order as whole lines.
+        // the keys are read through the segment tables (seg), were moved into that order by
+        // k_mg_scatter or are read through key_order, and k_mg_unpermute brings the answers back
+        // to batch order as whole lines.
+        const uint64_t j = jw + (threadIdx.x & 63u);
+        const uint64_t segkey = seg.segrow ? mg_seg_key(seg, jw, j < kb.n ? j : kb.n - 1) : 0;
+        if (j >= kb.n) continue;
         const uint64_t oi = j;
-        const uint64_t i = key_order ? (uint64_t)key_order[j] : j;
+        const uint64_t i = seg.segrow ? segkey : key_order ? (uint64_t)key_order[j] : j;
         const uint8_t *key;
         uint32_t klen;
         if (kb.offsets) {
@@ -571,6 +579,145 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const B *__restr
     }
 }
 
+// ---- the scatter-free order (multiget_order 1, aligned 16-B keys; round 6).  The
+// sorted rows are those k_mg_scatter produced (bucket-major, batch order within a bucket), but no
+// pass moves the keys across the batch:
+//   k_mg_bucket_sort  chunk c: each key's bucket, the chunk's stable ranks (chunk_positions) and its
+//                     keys written back sorted by bucket inside the chunk's own 32 KB (keys_cs), its
+//                     bucket counts cnt[b * C + c] and chunk-local offsets cloc[c * nb + b]
+//   k_mg_rows         scans each bucket's row of C chunk counts
+//   k_mg_segrows      segment (b, c) = bucket b's run of chunk c: its first sorted row segrow[b * C + c]
+//                     (non-decreasing in b * C + c), runs[c * nb + b] for k_mg_unpermute, and the
+//                     segment holding row 64 w of every wave w (wstart)
+// k_multiget finds each row's segment from its wave's start and a 64-entry window of segrow
+// (mg_seg_key) and reads the key from keys_cs: each segment's keys are contiguous there.
+__device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uint64_t j) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t r = (uint32_t)j;
+    const uint32_t s0 = sg.wstart[jw >> 6];
+    const uint32_t e = s0 + lane < sg.nseg ? sg.segrow[s0 + lane] : 0xFFFFFFFFu;
+    uint32_t i = 0;  // the last window entry <= r (entry 0 is: it holds row jw <= r)
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1) {
+        const uint32_t v = (uint32_t)__shfl((int)e, (int)(i + step), 64);
+        if (v <= r) i += step;
+    }
+    uint32_t sgi = s0 + i;
+    if (i == 63) {  // the row may lie past the window (a run of empty segments): bisect the rest
+        uint32_t a = sgi, b = sg.nseg;
+        while (b - a > 1) {
+            const uint32_t mid = (a + b) >> 1;
+            if (sg.segrow[mid] <= r)
+                a = mid;
+            else
+                b = mid;
+        }
+        sgi = a;
+    }
+    const uint32_t bk = sgi / sg.C, c = sgi - bk * sg.C;
+    return (uint64_t)c * kMgChunk + sg.cloc[(uint64_t)c * sg.nb + bk] + (r - sg.segrow[sgi]);
+}
+
+// LDS (dynamic): stage uint4[kMgChunk] | pmin u64[2 (nb - 1)] | cw u32[kMgWaves nb] | loc u32[nb + 1] | wsum u32[4]
+static size_t mg_bucket_sort_lds(uint32_t nb) {
+    return (size_t)kMgChunk * 16 + (size_t)16 * (nb - 1) + 4 * ((size_t)kMgWaves * nb + nb + 1 + 4);
+}
+
+template <typename B>
+__global__ __launch_bounds__(256) void k_mg_bucket_sort(uint64_t n, const uint4 *__restrict__ keys,
+                                                        const RegSlot *__restrict__ slots, uint32_t lo, uint32_t hi,
+                                                        const uint8_t *__restrict__ ranges, uint32_t bits,
+                                                        B *__restrict__ bucket, uint32_t *__restrict__ cnt,
+                                                        uint16_t *__restrict__ cloc, uint4 *__restrict__ keys_cs,
+                                                        uint32_t C) {
+    extern __shared__ uint4 mgb_lds[];
+    const uint32_t nb = hi - lo + 1;
+    uint4 *stage = mgb_lds;
+    uint64_t *pmin = (uint64_t *)(stage + kMgChunk);
+    uint32_t *cw = (uint32_t *)(pmin + 2 * (nb - 1));
+    uint32_t *loc = cw + kMgWaves * nb;
+    uint32_t *wsum = loc + nb + 1;
+    for (uint32_t u = threadIdx.x; u < nb - 1; u += blockDim.x) {
+        pmin[2 * u] = slots[lo + u].min_be[0];
+        pmin[2 * u + 1] = slots[lo + u].min_be[1];
+    }
+    const uint64_t c0 = (uint64_t)blockIdx.x * kMgChunk;
+    const uint32_t cn = (uint32_t)min((uint64_t)kMgChunk, n - c0);
+    uint4 v[kMgSteps];
+#pragma unroll
+    for (uint32_t s = 0; s < kMgSteps; ++s) v[s] = keys[c0 + min(chunk_key(s), cn - 1)];  // clamped: no branch
+    __syncthreads();
+    uint32_t bk[kMgSteps], pos[kMgSteps];
+#pragma unroll
+    for (uint32_t s = 0; s < kMgSteps; ++s) {
+        const uint32_t q = chunk_key(s);
+        bk[s] = nb;
+        if (q < cn) {
+            const uint64_t k0 = __builtin_bswap64((uint64_t)v[s].x | ((uint64_t)v[s].y << 32));
+            const uint64_t k1 = __builtin_bswap64((uint64_t)v[s].z | ((uint64_t)v[s].w << 32));
+            bk[s] = mg_bisect((const uint8_t *)(keys + c0 + q), 16, k0, k1, slots, lo, hi, ranges, pmin) - lo;
+        }
+    }
+    chunk_positions(bk, cn, nb, bits, cw, loc, wsum, pos);
+#pragma unroll
+    for (uint32_t s = 0; s < kMgSteps; ++s)
+        if (bk[s] < nb) {
+            stage[pos[s]] = v[s];
+            bucket[c0 + chunk_key(s)] = (B)bk[s];
+        }
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {
+        cnt[(uint64_t)u * C + blockIdx.x] = loc[u + 1] - loc[u];
+        cloc[(uint64_t)blockIdx.x * nb + u] = (uint16_t)loc[u];
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < cn; q += blockDim.x) keys_cs[c0 + q] = stage[q];
+}
+
+// block b: exclusive scan of row b (len entries) in place, in LDS-sized pieces; totals[b] = its sum
+constexpr uint32_t kMgRowPiece = 4096;
+__global__ __launch_bounds__(256) void k_mg_rows_long(uint32_t *__restrict__ rows, uint32_t len,
+                                                      uint32_t *__restrict__ totals) {
+    __shared__ uint32_t row[kMgRowPiece];
+    __shared__ uint32_t wsum[4];
+    uint32_t *g = rows + (uint64_t)blockIdx.x * len;
+    uint32_t carry = 0;
+    for (uint32_t p0 = 0; p0 < len; p0 += kMgRowPiece) {
+        const uint32_t pl = min(kMgRowPiece, len - p0);
+        for (uint32_t u = threadIdx.x; u < pl; u += blockDim.x) row[u] = g[p0 + u];
+        __syncthreads();
+        const uint32_t total = block_scan_lds(row, pl, wsum);
+        for (uint32_t u = threadIdx.x; u < pl; u += blockDim.x) g[p0 + u] = row[u] + carry;
+        carry += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+}
+
+// every segment s = b * C + c: its first sorted row, its runs entry, and the waves whose first row
+// it holds; each block first scans the bucket totals into bases
+__global__ __launch_bounds__(256) void k_mg_segrows(const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ totals,
+                                                    uint32_t nb, uint32_t C, uint32_t n, uint32_t *__restrict__ segrow,
+                                                    uint32_t *__restrict__ runs, uint32_t *__restrict__ wstart) {
+    __shared__ uint32_t base[kMgMaxBuckets + 1];
+    __shared__ uint32_t wsum[4];
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] = totals[u];
+    __syncthreads();
+    block_scan_lds(base, nb, wsum);
+    const uint64_t nseg = (uint64_t)nb * C;
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseg) return;
+    const uint32_t b = (uint32_t)(s / C), c = (uint32_t)(s - (uint64_t)b * C);
+    const uint32_t row = base[b] + cnt[s];
+    uint32_t next = n;
+    if (s + 1 < nseg) {
+        const uint32_t b1 = (uint32_t)((s + 1) / C);
+        next = base[b1] + cnt[s + 1];
+    }
+    segrow[s] = row;
+    runs[(uint64_t)c * nb + b] = row;
+    for (uint32_t w = (row + 63) / 64; w < (next + 63) / 64; ++w) wstart[w] = (uint32_t)s;
+}
+
 // Each key's answer back from its sorted row to batch order, one workgroup per chunk of kMgChunk
 // keys: the chunk's stable ranks are derived again from its bucket ids (chunk_positions, as the
 // scatter ranked them), so key q of bucket b sits at row runs[chunk][b] + its rank; the chunk's runs
@@ -688,10 +835,73 @@ static uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
 
 static uint64_t run_bytes(uint64_t n) { return al256(4ull * kMgMaxBuckets * ((n + kMgChunk - 1) / kMgChunk)); }
 
-uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes) {
+static bool order_segments(const KeyBatch &kb) { return multiget_order_moves(kb) && options().multiget_order != 2; }
+
+// The segment path's tables after the bucket ids: cnt, segrow (+1), cloc, wstart, totals.
+static uint64_t seg_bytes(uint64_t n, uint32_t nb) {
+    const uint64_t C = (n + kMgChunk - 1) / kMgChunk, ns = C * nb;
+    return al256(4 * ns) + al256(4 * (ns + 1)) + al256(2 * ns) + al256(4 * ((n + 63) / 64)) + al256(4 * kMgMaxBuckets);
+}
+
+uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes, uint32_t nb) {
     const uint64_t n = kb.n;
+    const uint64_t C = (n + kMgChunk - 1) / kMgChunk;
+    if (order_segments(kb))  // bucket ids | tables | bucket-sorted keys | runs | answers
+        return al256(n * 2) + seg_bytes(n, nb) + al256(n * 16) + al256(4ull * nb * C) + al256(n * answer_bytes);
     return al256(n * 2) + al256(4ull * kMgMaxBuckets * order_tiles(n)) + al256(4 * kMgMaxBuckets) +
            al256(multiget_order_moves(kb) ? n * 16 : n * 4) + run_bytes(n) + al256(n * answer_bytes);
+}
+
+// multiget_order 1 for aligned fixed 16-B keys: k_mg_bucket_sort, k_mg_rows_long, k_mg_segrows.
+static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
+                                            const uint8_t *ranges, void *ws, MgOrder *mo, hipStream_t s) {
+    const uint32_t nb = hi - lo + 1;
+    const uint64_t n = kb.n, C = (n + kMgChunk - 1) / kMgChunk, ns = C * nb;
+    uint8_t *p = (uint8_t *)ws;
+    void *bucket = p;
+    uint32_t *cnt = (uint32_t *)(p += al256(n * 2));
+    uint32_t *segrow = (uint32_t *)(p += al256(4 * ns));
+    uint16_t *cloc = (uint16_t *)(p += al256(4 * (ns + 1)));
+    uint32_t *wstart = (uint32_t *)(p += al256(2 * ns));
+    uint32_t *totals = (uint32_t *)(p += al256(4 * ((n + 63) / 64)));
+    uint4 *keys_cs = (uint4 *)(p += al256(4 * kMgMaxBuckets));
+    uint32_t *runs = (uint32_t *)(p += al256(n * 16));
+    void *answers = p + al256(4ull * nb * C);
+    const bool b8 = nb <= 256;
+    uint32_t bits = 0;
+    while ((1u << bits) <= nb) ++bits;
+    const size_t lds = mg_bucket_sort_lds(nb);
+    auto sort = [&](auto bt) -> hipError_t {
+        using B = decltype(bt);
+        hipError_t a = hipFuncSetAttribute((const void *)k_mg_bucket_sort<B>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+        if (a != hipSuccess) return a;
+        hipLaunchKernelGGL(k_mg_bucket_sort<B>, dim3((unsigned)C), dim3(256), lds, s, n, (const uint4 *)kb.data, slots, lo,
+                           hi, ranges, bits, (B *)bucket, cnt, cloc, keys_cs, (uint32_t)C);
+        return hipGetLastError();
+    };
+    hipError_t e = b8 ? sort(uint8_t{}) : sort(uint16_t{});
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_mg_rows_long, dim3(nb), dim3(256), 0, s, cnt, (uint32_t)C, totals);
+    hipLaunchKernelGGL(k_mg_segrows, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, cnt, totals, nb, (uint32_t)C,
+                       (uint32_t)n, segrow, runs, wstart);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    mo->active = true;
+    mo->n = n;
+    mo->nb = nb;
+    mo->bits = bits;
+    mo->bucket = bucket;
+    mo->bucket8 = b8;
+    mo->runs = runs;
+    mo->keys = (const uint8_t *)keys_cs;
+    mo->answers = answers;
+    mo->seg.segrow = segrow;
+    mo->seg.wstart = wstart;
+    mo->seg.cloc = cloc;
+    mo->seg.nseg = (uint32_t)ns;
+    mo->seg.C = (uint32_t)C;
+    mo->seg.nb = nb;
+    return hipSuccess;
 }
 
 hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
@@ -699,6 +909,7 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
     *mo = MgOrder{};
     const uint32_t nb = hi - lo + 1;
     if (kb.n == 0 || nb > kMgMaxBuckets || nb < 2 || kb.n > 0xffffffffull) return hipSuccess;
+    if (order_segments(kb)) return launch_multiget_order_seg(kb, slots, lo, hi, ranges, ws, mo, s);
     const uint32_t T = order_tiles(kb.n), tl = tile_keys(kb.n);
     uint8_t *p = (uint8_t *)ws;
     void *bucket = p;
@@ -774,7 +985,7 @@ hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answ
 
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
                            const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap, hipStream_t s,
-                           const uint32_t *key_order) {
+                           const uint32_t *key_order, const MgSeg &seg) {
     if (kb.n == 0) return hipSuccess;
     if (!cand && nslots > kMaxSlots) return hipErrorInvalidValue;  // the mask form stages slots in LDS
     uint64_t g = (kb.n + 255) / 256;
@@ -784,7 +995,7 @@ hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t ns
         using S = decltype(src);
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe, cand,
-                               cap, key_order, (uint32_t)options().multiget_xcd);
+                               cap, key_order, (uint32_t)options().multiget_xcd, seg);
             return hipGetLastError();
         };
         if (lay.all_k7_m32) {

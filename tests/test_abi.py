@@ -125,7 +125,7 @@ def test_options_round_trip_and_reject_bad_values(seb):
     with seb.option("probe_phases", 5):
         assert seb.get_option("probe_phases") == 5
     for name, bad in (("build_algo", 5), ("probe_phases", 65), ("many_splits", -1), ("grid_cap", 0),
-                      ("multiget_order", 2), ("multiget_l0_group", 2), ("probe_compact", 2), ("nonexistent", 1), ("probe_mode", 8), ("scatter_xcd", 0),
+                      ("multiget_order", 3), ("multiget_l0_group", 2), ("probe_compact", 2), ("nonexistent", 1), ("probe_mode", 8), ("scatter_xcd", 0),
                       ("clear_kernel", 1)):
         before = seb.get_option(name) if name in OPTION_NAMES else None
         with pytest.raises(seb.SebError):

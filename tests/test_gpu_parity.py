@@ -1406,8 +1406,10 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
         want_list = reg.multiget_list(probes)
         want_odd = reg.multiget_list(probes, cap=5)  # odd rows: the unpermute moves u16 granules
         want_wide = reg.multiget_list(probes, cap=20)  # 40-B rows: u32 granules staged in 3 passes
-    for xcd in (0, 1):  # multiget_xcd: the XCD-contiguous block remap walks the same rows
-        with seb.option("multiget_order", 1), seb.option("multiget_xcd", xcd):
+    # multiget_xcd: the XCD-contiguous block remap walks the same rows; order 1 reads fixed keys
+    # through segment tables, order 2 (round 5's form) moves them by a scatter pass
+    for order, xcd in ((1, 0), (1, 1), (2, 1)):
+        with seb.option("multiget_order", order), seb.option("multiget_xcd", xcd):
             got_mask = reg.multiget(probes)
             got_list = reg.multiget_list(probes)
             got_odd = reg.multiget_list(probes, cap=5)
@@ -1422,7 +1424,7 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
     nf = fixed.size // 16
     dk = seb.dev_keys(to_dev(torch, fixed), n=nf, stride=16)
     outs, lists = [], []
-    for order in (0, 1):
+    for order in (0, 1, 2):
         with seb.option("multiget_order", order):
             out = torch.zeros(nf, dtype=torch.int64, device="cuda")
             reg.multiget_dev(dk, out)
@@ -1431,8 +1433,8 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
             torch.cuda.synchronize()
             outs.append(out.cpu().numpy())
             lists.append(lst.cpu().numpy().view(np.uint16))
-    assert np.array_equal(outs[0], outs[1])
-    assert np.array_equal(lists[0], lists[1])
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
+    assert np.array_equal(lists[0], lists[1]) and np.array_equal(lists[0], lists[2])
     # The order's scratch cannot be had (a 1 MiB workspace cap; its first request is ~2.6 MB):
     # MultiGet falls back to batch order and answers the same.  A failed HIP call made just before
     # (the caller's hipMalloc of 2^60 B, its error left unread) must not leak into the MultiGet's
@@ -1477,13 +1479,13 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
     big = to_dev(torch, kg.key16(rng.integers(0, 64000, nbig)))
     dbig = seb.dev_keys(big, n=nbig, stride=16)
     res = []
-    for order in (0, 1):
+    for order in (0, 1, 2):
         with seb.option("multiget_order", order):
             out = torch.zeros(nbig, dtype=torch.int64, device="cuda")
             reg.multiget_dev(dbig, out)
             torch.cuda.synchronize()
             res.append(out.cpu().numpy())
-    assert np.array_equal(res[0], res[1])
+    assert np.array_equal(res[0], res[1]) and np.array_equal(res[0], res[2])
     reg.close()
 
 
@@ -1585,7 +1587,9 @@ def test_registry_key_range_order_wide_partition_level(seb, torch_cuda, parts):
         out = torch.zeros((n, 4), dtype=torch.int16, device="cuda")
         reg.multiget_list_dev(dk, out, 4)
         torch.cuda.synchronize()
-    assert np.array_equal(got, want)
+    with seb.option("multiget_order", 2):  # round 5's scatter form
+        got2 = reg.multiget_list(probes)
+    assert np.array_equal(got, want) and np.array_equal(got2, want)
     assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
     sample = list(range(0, n, 499))
     assert np.array_equal(want[sample], _walk_rows(files, [probes[i].tobytes() for i in sample], 4))
