@@ -63,7 +63,7 @@ GOLDEN_ROUTE = "d4ba568830284e7cac12e54c58ea3b6e35b5acd0fbe1cafe90269f177f778ff0
 GOLDEN_ROUTE_BEGIN = "0afec9b77141e0845ef7750736ed4667d1d1adf3df91c0ab47e85c09302ba1ff"  # sha256(u64 shard_begin)
 GOLDEN_MANY = "18f390ebd4082f2282f8f6352c2e02f946e855b57078fcd4f21e81956050baa7"  # sha256 of the 64 C5 filter digests
 GOLDEN_WAL = "7d661e321c2804cebf541abd9c1a34463b70fe27fce3c5459a71408ac91b3e01"  # sha256(u32 CRCs), 2M records
-OPTIONS = ("build_algo", "multi_interleave", "multiget_order", "multiget_l0_group", "multiget_xcd", "varlen_prehash_min_keys", "bucket_min_keys",
+OPTIONS = ("build_algo", "multi_interleave", "multiget_order", "multiget_piece_mib", "multiget_l0_group", "multiget_xcd", "varlen_prehash_min_keys", "bucket_min_keys",
            "lds_min_keys", "many_splits", "probe_phases", "probe_compact", "grid_cap", "workspace_limit_mib",
            "varlen_tail", "scatter_bins", "cpu_fallback")
 
@@ -1093,6 +1093,7 @@ def main():
                              "timed step and the last; ms_per_step is the wall clock of all steps",
             "options": {**{o: option_value(seb, o) for o in OPTIONS}, "overlap": int(overlap)},
             "cpu_fallbacks": seb.fallback_count(),
+            "multiget_order_fallbacks": int(seb.lib().seb_multiget_order_fallbacks()),
             "per_rank": records,
             "rank_check": {x: report[x] for x in report if x != "devices"},
         }

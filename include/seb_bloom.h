@@ -99,6 +99,8 @@ int seb_abi_version(void);
  *   "multiget_order"  registry MultiGet walks batches of >= 64K keys in key-range order (1, default:
  *                     aligned 16-B keys sorted by bucket within 2048-key chunks and read through
  *                     segment tables; 2: moved across the batch by a scatter pass) or batch order (0)
+ *   "multiget_piece_mib" registry MultiGet: a batch whose key-range order would need more scratch
+ *                     than this (MiB, default 1024) is walked in pieces of whole 2048-key chunks
  *   "multiget_l0_group" registry MultiGet tests the L0 files that share (m, k) through one
  *                     bit-interleaved table, one gather per position for all of them (1, default)
  *   "multiget_xcd"    registry MultiGet: the workgroups that share an XCD walk one contiguous eighth of
@@ -269,6 +271,10 @@ int seb_filter_flush(seb_filter *f);
 /* How many Go-API-mirror builds / batched probes ran on the host copy because the device path
  * failed (the "cpu_fallback" option); 0 on a healthy GPU. */
 uint64_t seb_fallback_count(void);
+/* Registry MultiGets (seb_registry_multiget*) that ran in batch order because the key-range
+ * order's scratch could not be had (SEB_ERR_NOMEM under "workspace_limit_mib" or the device): the
+ * answers are the same, only slower; a benchmark reports it to show which path it measured. */
+uint64_t seb_multiget_order_fallbacks(void);
 
 /* ------------------ device-resident filter registry + batched LSM lookup ---- */
 /* One registry per LSM instance.  seb_registry_put decodes an SSTable's bloom block (the bytes

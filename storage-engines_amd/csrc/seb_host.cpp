@@ -162,6 +162,7 @@ static const OptionDesc kOptions[] = {
     SEB_OPT(scatter_bins, 0, 1),
     SEB_OPT(grid_cap, 1, 1 << 30),
     SEB_OPT(workspace_limit_mib, 0, 1 << 30),
+    SEB_OPT(multiget_piece_mib, 1, 1 << 20),
     SEB_OPT(varlen_tail, 0, 3),
     SEB_OPT(cpu_fallback, 0, 1),
     SEB_OPT(fault_inject, 0, 2),
@@ -2117,13 +2118,21 @@ static RegLayout mg_layout(const seb_registry *r) {
 // multiget_order: the batch's key-range order over the registry's partition level, in the
 // stream's scratch (tag 3); mo->active false when off, too small a batch or no disjoint level of
 // >= 2 files.  On success kb reads the moved keys, if they were moved.
+static std::atomic<uint64_t> g_mg_batch_order{0};
+extern "C" uint64_t seb_multiget_order_fallbacks(void) { return g_mg_batch_order.load(std::memory_order_relaxed); }
+
+static bool multiget_ordered(const seb_registry *r, uint64_t n) {
+    return options().multiget_order && r->part_hi > r->part_lo && n >= 65536 && n <= 0xffffffffull;
+}
+
 static int multiget_order(seb_registry *r, KeyBatch &kb, uint64_t answer_bytes, hipStream_t s, MgOrder *mo) {
     *mo = MgOrder{};
-    if (!options().multiget_order || r->part_hi <= r->part_lo || kb.n < 65536 || kb.n > 0xffffffffull) return SEB_OK;
+    if (!multiget_ordered(r, kb.n)) return SEB_OK;
     void *ws = nullptr;
     int rc = cached_workspace(s, multiget_order_bytes(kb, answer_bytes, r->part_hi - r->part_lo + 1), &ws, 3);
     if (rc == SEB_ERR_NOMEM) {  // the order is only a speed-up: batch order needs no scratch
         t_err.clear();
+        g_mg_batch_order.fetch_add(1, std::memory_order_relaxed);  // seb_multiget_order_fallbacks
         return SEB_OK;
     }
     if (rc) return rc;
@@ -2136,8 +2145,34 @@ static int multiget_order(seb_registry *r, KeyBatch &kb, uint64_t answer_bytes, 
 // One MultiGet launch (mask form: maybe; list form: cand rows of cap u16) over kb, in key-range
 // order when the registry has a partition level (answers in sorted rows, then unpermuted into the
 // output), else in batch order.
+// Largest ordered piece: the order's scratch (bucket ids, tables, sorted keys, sorted-row answers)
+// stays near multiget_piece_mib (1 GiB) however large the batch or its rows; a larger batch is
+// walked in pieces of whole 2048-key chunks, each in key-range order.
+
+static int multiget_piece(seb_registry *r, KeyBatch kb, uint64_t *maybe, uint16_t *cand, uint32_t cap, hipStream_t s);
+
 static int multiget_launch(seb_registry *r, KeyBatch kb, uint64_t *maybe, uint16_t *cand, uint32_t cap,
                            hipStream_t s) {
+    const uint64_t answer_bytes = maybe ? 8 : 2ull * cap;
+    const uint64_t scratch = (uint64_t)options().multiget_piece_mib << 20;
+    const uint64_t piece = std::max<uint64_t>(65536, (scratch / (answer_bytes + 40)) & ~2047ull);
+    if (!multiget_ordered(r, kb.n) || kb.n <= piece) return multiget_piece(r, kb, maybe, cand, cap, s);
+    for (uint64_t off = 0; off < kb.n; off += piece) {
+        KeyBatch p = kb;
+        p.n = std::min(piece, kb.n - off);
+        if (kb.offsets)
+            p.offsets = kb.offsets + off;  // absolute offsets into the same data
+        else
+            p.data = kb.data + off * kb.stride;
+        if (kb.hashes) p.hashes = kb.hashes + off;
+        const int rc = multiget_piece(r, p, maybe ? maybe + off : nullptr, cand ? cand + off * cap : nullptr, cap, s);
+        if (rc) return rc;
+    }
+    return SEB_OK;
+}
+
+static int multiget_piece(seb_registry *r, KeyBatch kb, uint64_t *maybe, uint16_t *cand, uint32_t cap,
+                          hipStream_t s) {
     const uint64_t answer_bytes = maybe ? 8 : 2ull * cap;
     MgOrder mo;
     int rc;

@@ -150,6 +150,7 @@ struct Options {
     int probe_phases = 0;         // phased probe: number of filter ranges (0 = one per 4 MiB of filter)
     unsigned grid_cap = 1u << 20; // grid-stride kernels: most workgroups per launch
     uint64_t workspace_limit_mib = 0;  // library scratch cap (0 = none); a larger request fails SEB_ERR_NOMEM
+    uint64_t multiget_piece_mib = 1024;  // registry MultiGet: a key-range ordered walk's scratch per piece of the batch
     int varlen_tail = 1;          // pre-hash: the 64 * v longest keys of a workgroup of 512 - 64 * v keys on
                                   // 2 * v waves of 32 keys, a lane per chain (v = 1, 2, 3), or one key per
                                   // lane throughout (0, measured slower: DESIGN.md 5.5)

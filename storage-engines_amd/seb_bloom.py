@@ -98,6 +98,7 @@ _SIGS = {
     "seb_filter_pending": (_u64, [_vp]),
     "seb_filter_flush": (_i, [_vp]),
     "seb_fallback_count": (_u64, []),
+    "seb_multiget_order_fallbacks": (_u64, []),
     "seb_registry_new": (_vp, [_i]),
     "seb_registry_free": (None, [_vp]),
     "seb_registry_put": (_i, [_vp, _u64, _i, _vp, _u64, _vp, _u64, _vp, _u64]),

@@ -112,7 +112,7 @@ def test_no_silent_fallback_without_library(seb, monkeypatch, tmp_path):
 
 OPTION_NAMES = ["build_algo", "multi_interleave", "multiget_order", "multiget_l0_group", "varlen_prehash_min_keys",
                 "bucket_min_keys", "lds_min_keys", "many_splits", "probe_phases", "probe_compact", "grid_cap",
-                "workspace_limit_mib"]
+                "workspace_limit_mib", "multiget_piece_mib"]
 
 
 def test_options_round_trip_and_reject_bad_values(seb):
@@ -125,7 +125,7 @@ def test_options_round_trip_and_reject_bad_values(seb):
     with seb.option("probe_phases", 5):
         assert seb.get_option("probe_phases") == 5
     for name, bad in (("build_algo", 5), ("probe_phases", 65), ("many_splits", -1), ("grid_cap", 0),
-                      ("multiget_order", 3), ("multiget_l0_group", 2), ("probe_compact", 2), ("nonexistent", 1), ("probe_mode", 8), ("scatter_xcd", 0),
+                      ("multiget_order", 3), ("multiget_piece_mib", 0), ("multiget_l0_group", 2), ("probe_compact", 2), ("nonexistent", 1), ("probe_mode", 8), ("scatter_xcd", 0),
                       ("clear_kernel", 1)):
         before = seb.get_option(name) if name in OPTION_NAMES else None
         with pytest.raises(seb.SebError):

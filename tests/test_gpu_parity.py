@@ -1435,6 +1435,16 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
             lists.append(lst.cpu().numpy().view(np.uint16))
     assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
     assert np.array_equal(lists[0], lists[1]) and np.array_equal(lists[0], lists[2])
+    # a batch walked in ordered pieces (multiget_piece_mib 1: 64K-key pieces, the last ragged)
+    with seb.option("multiget_order", 1), seb.option("multiget_piece_mib", 1):
+        out = torch.zeros(nf, dtype=torch.int64, device="cuda")
+        reg.multiget_dev(dk, out)
+        lst = torch.zeros((nf, want_list.shape[1]), dtype=torch.int16, device="cuda")
+        reg.multiget_list_dev(dk, lst, want_list.shape[1])
+        torch.cuda.synchronize()
+        assert nf > 65536 and np.array_equal(out.cpu().numpy(), outs[0])
+        assert np.array_equal(lst.cpu().numpy().view(np.uint16), lists[0])
+        assert np.array_equal(reg.multiget(probes), want_mask)
     # The order's scratch cannot be had (a 1 MiB workspace cap; its first request is ~2.6 MB):
     # MultiGet falls back to batch order and answers the same.  A failed HIP call made just before
     # (the caller's hipMalloc of 2^60 B, its error left unread) must not leak into the MultiGet's
@@ -1443,6 +1453,7 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
 
     seb.workspace_release()
     hip = ctypes.CDLL("libamdhip64.so")
+    fell = int(seb.lib().seb_multiget_order_fallbacks())
     with seb.option("multiget_order", 1), seb.option("workspace_limit_mib", 1):
         out = torch.zeros(nf, dtype=torch.int64, device="cuda")
         torch.cuda.synchronize()
@@ -1453,6 +1464,7 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
         assert np.array_equal(out.cpu().numpy(), outs[0])
         assert np.array_equal(reg.multiget(probes), want_mask)
         assert np.array_equal(reg.multiget_list(probes), want_list)
+        assert int(seb.lib().seb_multiget_order_fallbacks()) >= fell + 3  # each counted as batch order
         with pytest.raises(seb.SebError):  # a build whose scratch is over the cap fails loudly
             big = seb.dev_keys(to_dev(torch, kg.key16(np.arange(1_000_000))), n=1_000_000, stride=16)
             with seb.option("build_algo", 2):
