@@ -133,10 +133,10 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         // k_mg_scatter or are read through key_order, and k_mg_unpermute brings the answers back
         // to batch order as whole lines.
         const uint64_t j = jw + (threadIdx.x & 63u);
-        const uint64_t segkey = seg.segrow ? mg_seg_key(seg, jw, j < kb.n ? j : kb.n - 1) : 0;
+        const uint64_t segkey = seg.seg ? mg_seg_key(seg, jw, j < kb.n ? j : kb.n - 1) : 0;
         if (j >= kb.n) continue;
         const uint64_t oi = j;
-        const uint64_t i = seg.segrow ? segkey : key_order ? (uint64_t)key_order[j] : j;
+        const uint64_t i = seg.seg ? segkey : key_order ? (uint64_t)key_order[j] : j;
         const uint8_t *key;
         uint32_t klen;
         if (kb.offsets) {
@@ -583,39 +583,44 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const B *__restr
 // sorted rows are those k_mg_scatter produced (bucket-major, batch order within a bucket), but no
 // pass moves the keys across the batch:
 //   k_mg_bucket_sort  chunk c: each key's bucket, the chunk's stable ranks (chunk_positions) and its
-//                     keys written back sorted by bucket inside the chunk's own 32 KB (keys_cs), its
-//                     bucket counts cnt[b * C + c] and chunk-local offsets cloc[c * nb + b]
-//   k_mg_rows         scans each bucket's row of C chunk counts
-//   k_mg_segrows      segment (b, c) = bucket b's run of chunk c: its first sorted row segrow[b * C + c]
-//                     (non-decreasing in b * C + c), runs[c * nb + b] for k_mg_unpermute, and the
+//                     keys written back sorted by bucket inside the chunk's own 32 KB (keys_cs); per
+//                     segment s = b * C + c (bucket b's run of chunk c) its count cnt[s] and where the
+//                     run starts in keys_cs, seghi[s] = chunk << 11 | offset in the chunk
+//   k_mg_rows_pieces  scans each bucket's row of C counts in pieces of kMgPiece chunks
+//   k_mg_bases        bucket bases (scan of the bucket totals) plus the pieces' prefixes
+//   k_mg_segrows      seg[s] = first sorted row | seghi[s] << 32 (rows non-decreasing in s) and the
 //                     segment holding row 64 w of every wave w (wstart)
-// k_multiget finds each row's segment from its wave's start and a 64-entry window of segrow
-// (mg_seg_key) and reads the key from keys_cs: each segment's keys are contiguous there.
+// k_multiget finds each row's segment from its wave's start and a 64-entry window of seg
+// (mg_seg_key): three dependent loads (wstart, the window, the key) and no division; every
+// segment's keys are contiguous in keys_cs.  k_mg_unpermute reads each chunk's run starts from seg.
 __device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uint64_t j) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t r = (uint32_t)j;
     const uint32_t s0 = sg.wstart[jw >> 6];
-    const uint32_t e = s0 + lane < sg.nseg ? sg.segrow[s0 + lane] : 0xFFFFFFFFu;
-    uint32_t i = 0;  // the last window entry <= r (entry 0 is: it holds row jw <= r)
+    const uint64_t e = s0 + lane < sg.nseg ? sg.seg[s0 + lane] : ~0ull;
+    const uint32_t er = (uint32_t)e;
+    uint32_t i = 0;  // the last window entry whose row <= r (entry 0's is: it holds row jw <= r)
 #pragma unroll
     for (uint32_t step = 32; step; step >>= 1) {
-        const uint32_t v = (uint32_t)__shfl((int)e, (int)(i + step), 64);
+        const uint32_t v = (uint32_t)__shfl((int)er, (int)(i + step), 64);
         if (v <= r) i += step;
     }
-    uint32_t sgi = s0 + i;
+    const uint32_t lo = (uint32_t)__shfl((int)er, (int)i, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(e >> 32), (int)i, 64);
+    uint64_t ent = (uint64_t)lo | ((uint64_t)hi << 32);
     if (i == 63) {  // the row may lie past the window (a run of empty segments): bisect the rest
-        uint32_t a = sgi, b = sg.nseg;
+        uint32_t a = s0 + 63, b = sg.nseg;
         while (b - a > 1) {
             const uint32_t mid = (a + b) >> 1;
-            if (sg.segrow[mid] <= r)
+            if ((uint32_t)sg.seg[mid] <= r)
                 a = mid;
             else
                 b = mid;
         }
-        sgi = a;
+        ent = sg.seg[a];
     }
-    const uint32_t bk = sgi / sg.C, c = sgi - bk * sg.C;
-    return (uint64_t)c * kMgChunk + sg.cloc[(uint64_t)c * sg.nb + bk] + (r - sg.segrow[sgi]);
+    const uint32_t h = (uint32_t)(ent >> 32);
+    return (uint64_t)(h >> 11) * kMgChunk + (h & 2047u) + (r - (uint32_t)ent);
 }
 
 // LDS (dynamic): stage uint4[kMgChunk] | pmin u64[2 (nb - 1)] | cw u32[kMgWaves nb] | loc u32[nb + 1] | wsum u32[4]
@@ -628,7 +633,7 @@ __global__ __launch_bounds__(256) void k_mg_bucket_sort(uint64_t n, const uint4 
                                                         const RegSlot *__restrict__ slots, uint32_t lo, uint32_t hi,
                                                         const uint8_t *__restrict__ ranges, uint32_t bits,
                                                         B *__restrict__ bucket, uint32_t *__restrict__ cnt,
-                                                        uint16_t *__restrict__ cloc, uint4 *__restrict__ keys_cs,
+                                                        uint32_t *__restrict__ seghi, uint4 *__restrict__ keys_cs,
                                                         uint32_t C) {
     extern __shared__ uint4 mgb_lds[];
     const uint32_t nb = hi - lo + 1;
@@ -667,54 +672,66 @@ __global__ __launch_bounds__(256) void k_mg_bucket_sort(uint64_t n, const uint4 
         }
     for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {
         cnt[(uint64_t)u * C + blockIdx.x] = loc[u + 1] - loc[u];
-        cloc[(uint64_t)blockIdx.x * nb + u] = (uint16_t)loc[u];
+        seghi[(uint64_t)u * C + blockIdx.x] = (blockIdx.x << 11) | (loc[u] & 2047u);  // (empty runs at 2048: unused)
     }
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < cn; q += blockDim.x) keys_cs[c0 + q] = stage[q];
 }
 
-// block b: exclusive scan of row b (len entries) in place, in LDS-sized pieces; totals[b] = its sum
-constexpr uint32_t kMgRowPiece = 4096;
-__global__ __launch_bounds__(256) void k_mg_rows_long(uint32_t *__restrict__ rows, uint32_t len,
-                                                      uint32_t *__restrict__ totals) {
-    __shared__ uint32_t row[kMgRowPiece];
+// block (p, b): exclusive scan of bucket b's counts of chunks [p * kMgPiece, ...) in place;
+// ptot[b * P + p] = the piece's total
+constexpr uint32_t kMgPiece = 1024;
+__global__ __launch_bounds__(256) void k_mg_rows_pieces(uint32_t *__restrict__ cnt, uint32_t C, uint32_t P,
+                                                        uint32_t *__restrict__ ptot) {
+    __shared__ uint32_t row[kMgPiece];
     __shared__ uint32_t wsum[4];
-    uint32_t *g = rows + (uint64_t)blockIdx.x * len;
-    uint32_t carry = 0;
-    for (uint32_t p0 = 0; p0 < len; p0 += kMgRowPiece) {
-        const uint32_t pl = min(kMgRowPiece, len - p0);
-        for (uint32_t u = threadIdx.x; u < pl; u += blockDim.x) row[u] = g[p0 + u];
-        __syncthreads();
-        const uint32_t total = block_scan_lds(row, pl, wsum);
-        for (uint32_t u = threadIdx.x; u < pl; u += blockDim.x) g[p0 + u] = row[u] + carry;
-        carry += total;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+    const uint32_t b = blockIdx.y, p0 = blockIdx.x * kMgPiece, pl = min(kMgPiece, C - p0);
+    uint32_t *g = cnt + (uint64_t)b * C + p0;
+    for (uint32_t u = threadIdx.x; u < pl; u += blockDim.x) row[u] = g[u];
+    __syncthreads();
+    const uint32_t total = block_scan_lds(row, pl, wsum);
+    for (uint32_t u = threadIdx.x; u < pl; u += blockDim.x) g[u] = row[u];
+    if (threadIdx.x == 0) ptot[(uint64_t)b * P + blockIdx.x] = total;
 }
 
-// every segment s = b * C + c: its first sorted row, its runs entry, and the waves whose first row
-// it holds; each block first scans the bucket totals into bases
-__global__ __launch_bounds__(256) void k_mg_segrows(const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ totals,
-                                                    uint32_t nb, uint32_t C, uint32_t n, uint32_t *__restrict__ segrow,
-                                                    uint32_t *__restrict__ runs, uint32_t *__restrict__ wstart) {
-    __shared__ uint32_t base[kMgMaxBuckets + 1];
+// one block: bucket totals, their exclusive scan (the bucket bases), and in place of ptot each
+// piece's first sorted row
+__global__ __launch_bounds__(256) void k_mg_bases(uint32_t *__restrict__ ptot, uint32_t nb, uint32_t P) {
+    __shared__ uint32_t base[kMgMaxBuckets];
     __shared__ uint32_t wsum[4];
-    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) base[u] = totals[u];
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+        uint32_t t = 0;
+        for (uint32_t p = 0; p < P; ++p) t += ptot[(uint64_t)b * P + p];
+        base[b] = t;
+    }
     __syncthreads();
     block_scan_lds(base, nb, wsum);
-    const uint64_t nseg = (uint64_t)nb * C;
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nseg) return;
-    const uint32_t b = (uint32_t)(s / C), c = (uint32_t)(s - (uint64_t)b * C);
-    const uint32_t row = base[b] + cnt[s];
-    uint32_t next = n;
-    if (s + 1 < nseg) {
-        const uint32_t b1 = (uint32_t)((s + 1) / C);
-        next = base[b1] + cnt[s + 1];
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+        uint32_t t = base[b];
+        for (uint32_t p = 0; p < P; ++p) {
+            const uint32_t c = ptot[(uint64_t)b * P + p];
+            ptot[(uint64_t)b * P + p] = t;
+            t += c;
+        }
     }
-    segrow[s] = row;
-    runs[(uint64_t)c * nb + b] = row;
+}
+
+// grid (C / 256, nb): segment s = b * C + c: seg[s] = its first sorted row | seghi[s] << 32, and
+// the waves whose first row it holds
+__global__ __launch_bounds__(256) void k_mg_segrows(const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ seghi,
+                                                    const uint32_t *__restrict__ pbase, uint32_t nb, uint32_t C,
+                                                    uint32_t P, uint32_t n, uint64_t *__restrict__ seg,
+                                                    uint32_t *__restrict__ wstart) {
+    const uint32_t b = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const uint64_t s = (uint64_t)b * C + c;
+    const uint32_t row = pbase[(uint64_t)b * P + c / kMgPiece] + cnt[s];
+    uint32_t next = n;
+    if (c + 1 < C)
+        next = pbase[(uint64_t)b * P + (c + 1) / kMgPiece] + cnt[s + 1];
+    else if (b + 1 < nb)
+        next = pbase[(uint64_t)(b + 1) * P] + cnt[s + 1];
+    seg[s] = (uint64_t)row | ((uint64_t)seghi[s] << 32);
     for (uint32_t w = (row + 63) / 64; w < (next + 63) / 64; ++w) wstart[w] = (uint32_t)s;
 }
 
@@ -740,7 +757,7 @@ template <typename G, typename B>
 __global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const B *__restrict__ bucket,
                                                       const uint32_t *__restrict__ runs, uint32_t nb, uint32_t bits,
                                                       const G *__restrict__ answers, G *__restrict__ out,
-                                                      uint32_t ge) {
+                                                      uint32_t ge, const uint64_t *__restrict__ seg, uint32_t C) {
     extern __shared__ uint4 mgu_lds[];
     constexpr uint32_t kSlice = sizeof(G) >= kMgStage ? 1 : kMgStage / sizeof(G);  // granules per key per pass
     uint32_t *loc = (uint32_t *)mgu_lds;
@@ -752,7 +769,10 @@ __global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const B *__res
                      ((((size_t)nb + 1 + (size_t)kMgWaves * nb + 4 + nb) * 4 + 2 * kMgChunk + 15) & ~(size_t)15));
     const uint64_t c0 = (uint64_t)blockIdx.x * kMgChunk;
     const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, n - c0);
-    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) rbase[u] = runs[(uint64_t)blockIdx.x * nb + u];
+    // the chunk's run starts: from the scatter's runs table, or the segment table's rows (the
+    // scatter-free order; bucket-major, so strided, but a line holds 16 neighbouring chunks)
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x)
+        rbase[u] = seg ? (uint32_t)seg[(uint64_t)u * C + blockIdx.x] : runs[(uint64_t)blockIdx.x * nb + u];
     uint32_t bk[kMgSteps], pos[kMgSteps];
     load_chunk_buckets(bucket, c0, c0 + cnt, nb, bk);
     chunk_positions(bk, cnt, nb, bits, cw, loc, wsum, pos);  // synchronises (rbase is visible after it)
@@ -837,36 +857,38 @@ static uint64_t run_bytes(uint64_t n) { return al256(4ull * kMgMaxBuckets * ((n 
 
 static bool order_segments(const KeyBatch &kb) { return multiget_order_moves(kb) && options().multiget_order != 2; }
 
-// The segment path's tables after the bucket ids: cnt, segrow (+1), cloc, wstart, totals.
+static uint32_t seg_pieces(uint64_t C) { return (uint32_t)((C + kMgPiece - 1) / kMgPiece); }
+
+// The segment path's tables after the bucket ids: cnt, seghi, seg, wstart, piece totals.
 static uint64_t seg_bytes(uint64_t n, uint32_t nb) {
     const uint64_t C = (n + kMgChunk - 1) / kMgChunk, ns = C * nb;
-    return al256(4 * ns) + al256(4 * (ns + 1)) + al256(2 * ns) + al256(4 * ((n + 63) / 64)) + al256(4 * kMgMaxBuckets);
+    return al256(4 * ns) + al256(4 * ns) + al256(8 * ns) + al256(4 * ((n + 63) / 64)) + al256(4ull * nb * seg_pieces(C));
 }
 
 uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes, uint32_t nb) {
     const uint64_t n = kb.n;
-    const uint64_t C = (n + kMgChunk - 1) / kMgChunk;
-    if (order_segments(kb))  // bucket ids | tables | bucket-sorted keys | runs | answers
-        return al256(n * 2) + seg_bytes(n, nb) + al256(n * 16) + al256(4ull * nb * C) + al256(n * answer_bytes);
+    if (order_segments(kb))  // bucket ids | tables | bucket-sorted keys | answers
+        return al256(n * 2) + seg_bytes(n, nb) + al256(n * 16) + al256(n * answer_bytes);
     return al256(n * 2) + al256(4ull * kMgMaxBuckets * order_tiles(n)) + al256(4 * kMgMaxBuckets) +
            al256(multiget_order_moves(kb) ? n * 16 : n * 4) + run_bytes(n) + al256(n * answer_bytes);
 }
 
-// multiget_order 1 for aligned fixed 16-B keys: k_mg_bucket_sort, k_mg_rows_long, k_mg_segrows.
+// multiget_order 1 for aligned fixed 16-B keys: k_mg_bucket_sort, k_mg_rows_pieces, k_mg_bases,
+// k_mg_segrows.
 static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
                                             const uint8_t *ranges, void *ws, MgOrder *mo, hipStream_t s) {
     const uint32_t nb = hi - lo + 1;
     const uint64_t n = kb.n, C = (n + kMgChunk - 1) / kMgChunk, ns = C * nb;
+    const uint32_t P = seg_pieces(C);
     uint8_t *p = (uint8_t *)ws;
     void *bucket = p;
     uint32_t *cnt = (uint32_t *)(p += al256(n * 2));
-    uint32_t *segrow = (uint32_t *)(p += al256(4 * ns));
-    uint16_t *cloc = (uint16_t *)(p += al256(4 * (ns + 1)));
-    uint32_t *wstart = (uint32_t *)(p += al256(2 * ns));
-    uint32_t *totals = (uint32_t *)(p += al256(4 * ((n + 63) / 64)));
-    uint4 *keys_cs = (uint4 *)(p += al256(4 * kMgMaxBuckets));
-    uint32_t *runs = (uint32_t *)(p += al256(n * 16));
-    void *answers = p + al256(4ull * nb * C);
+    uint32_t *seghi = (uint32_t *)(p += al256(4 * ns));
+    uint64_t *seg = (uint64_t *)(p += al256(4 * ns));
+    uint32_t *wstart = (uint32_t *)(p += al256(8 * ns));
+    uint32_t *ptot = (uint32_t *)(p += al256(4 * ((n + 63) / 64)));
+    uint4 *keys_cs = (uint4 *)(p += al256(4ull * nb * P));
+    void *answers = p + al256(n * 16);
     const bool b8 = nb <= 256;
     uint32_t bits = 0;
     while ((1u << bits) <= nb) ++bits;
@@ -877,14 +899,15 @@ static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *s
                                            (int)lds);
         if (a != hipSuccess) return a;
         hipLaunchKernelGGL(k_mg_bucket_sort<B>, dim3((unsigned)C), dim3(256), lds, s, n, (const uint4 *)kb.data, slots, lo,
-                           hi, ranges, bits, (B *)bucket, cnt, cloc, keys_cs, (uint32_t)C);
+                           hi, ranges, bits, (B *)bucket, cnt, seghi, keys_cs, (uint32_t)C);
         return hipGetLastError();
     };
     hipError_t e = b8 ? sort(uint8_t{}) : sort(uint16_t{});
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_mg_rows_long, dim3(nb), dim3(256), 0, s, cnt, (uint32_t)C, totals);
-    hipLaunchKernelGGL(k_mg_segrows, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, cnt, totals, nb, (uint32_t)C,
-                       (uint32_t)n, segrow, runs, wstart);
+    hipLaunchKernelGGL(k_mg_rows_pieces, dim3(P, nb), dim3(256), 0, s, cnt, (uint32_t)C, P, ptot);
+    hipLaunchKernelGGL(k_mg_bases, dim3(1), dim3(256), 0, s, ptot, nb, P);
+    hipLaunchKernelGGL(k_mg_segrows, dim3((unsigned)((C + 255) / 256), nb), dim3(256), 0, s, cnt, seghi, ptot, nb,
+                       (uint32_t)C, P, (uint32_t)n, seg, wstart);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     mo->active = true;
     mo->n = n;
@@ -892,12 +915,10 @@ static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *s
     mo->bits = bits;
     mo->bucket = bucket;
     mo->bucket8 = b8;
-    mo->runs = runs;
     mo->keys = (const uint8_t *)keys_cs;
     mo->answers = answers;
-    mo->seg.segrow = segrow;
+    mo->seg.seg = seg;
     mo->seg.wstart = wstart;
-    mo->seg.cloc = cloc;
     mo->seg.nseg = (uint32_t)ns;
     mo->seg.C = (uint32_t)C;
     mo->seg.nb = nb;
@@ -970,7 +991,7 @@ hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answ
                                            (int)lds);
         if (a != hipSuccess) return a;
         hipLaunchKernelGGL((k_mg_unpermute<G, B>), dim3((unsigned)chunks), dim3(256), lds, s, mo.n, (const B *)mo.bucket,
-                           mo.runs, mo.nb, mo.bits, (const G *)mo.answers, (G *)out, ge);
+                           mo.runs, mo.nb, mo.bits, (const G *)mo.answers, (G *)out, ge, mo.seg.seg, mo.seg.C);
         return hipGetLastError();
     };
     auto go = [&](auto g, uint32_t ge) { return mo.bucket8 ? go_b(g, uint8_t{}, ge) : go_b(g, uint16_t{}, ge); };
