@@ -1591,8 +1591,9 @@ def cpu_baseline(args, n, m, k):
            "sample": f"{sample} build + {sample} probe keys ({args.config}), oracle/bloom_oracle.c (C restatement of "
                      f"lsm/bloom.go; Go toolchain absent), {host['model']}",
            "method": f"per leg 1 warm-up + median of {CPU_REPS} (build then probe each rep); multi-threaded legs: "
-                     "key-sharded probe, build into at most 16 private filters (one per thread up to 16) OR-merged "
-                     "by byte range; every leg's filter and answers equal the 1-thread leg's",
+                     "key-sharded probe, build into at most 16 private filters (one per thread up to 16; their "
+                     "memory kept across builds, zeroed in each) OR-merged by byte range; every leg's filter and "
+                     "answers equal the 1-thread leg's",
            "cgroup_throttle": one["cgroup_throttle"],
            "reps": CPU_REPS, "host": host,
            **{x: one[x] for x in ("build_mkeys_s", "probe_mkeys_s", "build_ms", "probe_ms")}}

