@@ -584,8 +584,8 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const B *__restr
 // pass moves the keys across the batch:
 //   k_mg_bucket_sort  chunk c: each key's bucket, the chunk's stable ranks (chunk_positions) and its
 //                     keys written back sorted by bucket inside the chunk's own 32 KB (keys_cs); per
-//                     segment (b, c) (bucket b's run of chunk c), chunk-major at c * nb + b, its
-//                     count cnt and where the run starts in keys_cs, seghi = chunk << 11 | offset
+//                     segment s = b * C + c (bucket b's run of chunk c) its count cnt[s] and where the
+//                     run starts in keys_cs, seghi[s] = chunk << 11 | offset in the chunk
 //   k_mg_rows_pieces  scans each bucket's row of C counts in pieces of kMgPiece chunks
 //   k_mg_bases        bucket bases (scan of the bucket totals) plus the pieces' prefixes
 //   k_mg_segrows      seg[s] = first sorted row | seghi[s] << 32 (rows non-decreasing in s) and the
@@ -670,28 +670,27 @@ __global__ __launch_bounds__(256) void k_mg_bucket_sort(uint64_t n, const uint4 
             stage[pos[s]] = v[s];
             bucket[c0 + chunk_key(s)] = (B)bk[s];
         }
-    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {  // chunk-major: one contiguous row per chunk
-        cnt[(uint64_t)blockIdx.x * nb + u] = loc[u + 1] - loc[u];
-        seghi[(uint64_t)blockIdx.x * nb + u] = (blockIdx.x << 11) | (loc[u] & 2047u);  // (empty runs at 2048: unused)
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {
+        cnt[(uint64_t)u * C + blockIdx.x] = loc[u + 1] - loc[u];
+        seghi[(uint64_t)u * C + blockIdx.x] = (blockIdx.x << 11) | (loc[u] & 2047u);  // (empty runs at 2048: unused)
     }
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < cn; q += blockDim.x) keys_cs[c0 + q] = stage[q];
 }
 
-// block (p, b): exclusive scan of bucket b's counts of chunks [p * kMgPiece, ...) in place (the
-// counts are chunk-major, cnt[c * nb + b]: a strided column, L2-resident); ptot[b * P + p] = the
-// piece's total
+// block (p, b): exclusive scan of bucket b's counts of chunks [p * kMgPiece, ...) in place;
+// ptot[b * P + p] = the piece's total
 constexpr uint32_t kMgPiece = 1024;
-__global__ __launch_bounds__(256) void k_mg_rows_pieces(uint32_t *__restrict__ cnt, uint32_t C, uint32_t nb,
-                                                        uint32_t P, uint32_t *__restrict__ ptot) {
+__global__ __launch_bounds__(256) void k_mg_rows_pieces(uint32_t *__restrict__ cnt, uint32_t C, uint32_t P,
+                                                        uint32_t *__restrict__ ptot) {
     __shared__ uint32_t row[kMgPiece];
     __shared__ uint32_t wsum[4];
     const uint32_t b = blockIdx.y, p0 = blockIdx.x * kMgPiece, pl = min(kMgPiece, C - p0);
-    uint32_t *g = cnt + (uint64_t)p0 * nb + b;
-    for (uint32_t u = threadIdx.x; u < pl; u += blockDim.x) row[u] = g[(uint64_t)u * nb];
+    uint32_t *g = cnt + (uint64_t)b * C + p0;
+    for (uint32_t u = threadIdx.x; u < pl; u += blockDim.x) row[u] = g[u];
     __syncthreads();
     const uint32_t total = block_scan_lds(row, pl, wsum);
-    for (uint32_t u = threadIdx.x; u < pl; u += blockDim.x) g[(uint64_t)u * nb] = row[u];
+    for (uint32_t u = threadIdx.x; u < pl; u += blockDim.x) g[u] = row[u];
     if (threadIdx.x == 0) ptot[(uint64_t)b * P + blockIdx.x] = total;
 }
 
@@ -725,14 +724,14 @@ __global__ __launch_bounds__(256) void k_mg_segrows(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ wstart) {
     const uint32_t b = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
-    const uint64_t s = (uint64_t)b * C + c, t = (uint64_t)c * nb + b;  // bucket-major / chunk-major index
-    const uint32_t row = pbase[(uint64_t)b * P + c / kMgPiece] + cnt[t];
+    const uint64_t s = (uint64_t)b * C + c;
+    const uint32_t row = pbase[(uint64_t)b * P + c / kMgPiece] + cnt[s];
     uint32_t next = n;
     if (c + 1 < C)
-        next = pbase[(uint64_t)b * P + (c + 1) / kMgPiece] + cnt[t + nb];
+        next = pbase[(uint64_t)b * P + (c + 1) / kMgPiece] + cnt[s + 1];
     else if (b + 1 < nb)
-        next = pbase[(uint64_t)(b + 1) * P] + cnt[b + 1];
-    seg[s] = (uint64_t)row | ((uint64_t)seghi[t] << 32);
+        next = pbase[(uint64_t)(b + 1) * P] + cnt[s + 1];
+    seg[s] = (uint64_t)row | ((uint64_t)seghi[s] << 32);
     for (uint32_t w = (row + 63) / 64; w < (next + 63) / 64; ++w) wstart[w] = (uint32_t)s;
 }
 
@@ -905,7 +904,7 @@ static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *s
     };
     hipError_t e = b8 ? sort(uint8_t{}) : sort(uint16_t{});
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_mg_rows_pieces, dim3(P, nb), dim3(256), 0, s, cnt, (uint32_t)C, nb, P, ptot);
+    hipLaunchKernelGGL(k_mg_rows_pieces, dim3(P, nb), dim3(256), 0, s, cnt, (uint32_t)C, P, ptot);
     hipLaunchKernelGGL(k_mg_bases, dim3(1), dim3(256), 0, s, ptot, nb, P);
     hipLaunchKernelGGL(k_mg_segrows, dim3((unsigned)((C + 255) / 256), nb), dim3(256), 0, s, cnt, seghi, ptot, nb,
                        (uint32_t)C, P, (uint32_t)n, seg, wstart);
