@@ -22,7 +22,6 @@
 namespace seb {
 
 constexpr uint32_t kMaxSlots = 64;  // slot tables up to this size are staged in LDS
-constexpr uint32_t kMgBoundsMax = 1024;  // MODE 2: key-range prefixes of up to this many files staged in LDS (32 KB)
 
 __device__ __forceinline__ uint64_t be64(const uint8_t *p, uint32_t len) {  // first min(len,8) bytes, big-endian
     uint64_t v = 0;
@@ -107,25 +106,8 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                                                   uint32_t xcd, MgSeg seg) {
     constexpr bool kLds = MODE < 2, kList = MODE > 0;
     __shared__ RegSlot lslots[kLds ? kMaxSlots : 1];
-    // MODE 2 with up to kMgBoundsMax files: the files' MinKey / MaxKey prefixes in LDS (32 B per
-    // file, dynamic), so the per-level bisections and cover checks read LDS instead of issuing
-    // ~15 dependent L2 loads of slot structs per key; only the tested file's slot and key-prefix
-    // ties (the full compare) go to global memory
-    extern __shared__ uint64_t mg_bounds[];
-    const uint64_t *lb = nullptr;
     if constexpr (kLds) {
         for (uint32_t s = threadIdx.x; s < nslots; s += blockDim.x) lslots[s] = gslots[s];
-        __syncthreads();
-    } else {
-        if (nslots <= kMgBoundsMax) {
-            for (uint32_t s = threadIdx.x; s < nslots; s += blockDim.x) {
-                mg_bounds[4 * s] = gslots[s].min_be[0];
-                mg_bounds[4 * s + 1] = gslots[s].min_be[1];
-                mg_bounds[4 * s + 2] = gslots[s].max_be[0];
-                mg_bounds[4 * s + 3] = gslots[s].max_be[1];
-            }
-            lb = mg_bounds;
-        }
         __syncthreads();
     }
     const RegSlot *slots = kLds ? lslots : gslots;
@@ -168,26 +150,6 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         src.hash(i, h1, h2);
         uint64_t k0, k1;
         key_prefix(kb, key, klen, k0, k1);
-        // Go string order of the key against slot s's MinKey / MaxKey: the 16-byte prefixes from
-        // LDS (staged bounds or slots), the full compare only when they tie
-        auto cmp_min = [&](uint32_t s) -> int {
-            if (lb) {
-                const uint64_t p0 = lb[4 * s], p1 = lb[4 * s + 1];
-                if (k0 != p0) return k0 < p0 ? -1 : 1;
-                if (k1 != p1) return k1 < p1 ? -1 : 1;
-            }
-            const RegSlot &sl = slots[s];
-            return cmp_key(key, klen, k0, k1, sl.min_be, ranges + sl.min_off, sl.min_len);
-        };
-        auto cmp_max = [&](uint32_t s) -> int {
-            if (lb) {
-                const uint64_t p0 = lb[4 * s + 2], p1 = lb[4 * s + 3];
-                if (k0 != p0) return k0 < p0 ? -1 : 1;
-                if (k1 != p1) return k1 < p1 ? -1 : 1;
-            }
-            const RegSlot &sl = slots[s];
-            return cmp_key(key, klen, k0, k1, sl.max_be, ranges + sl.max_off, sl.max_len);
-        };
         uint64_t mask = 0;
         uint16_t *row = kList ? cand + oi * (uint64_t)cap : nullptr;
         uint32_t nc = 0;
@@ -232,15 +194,23 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                 uint32_t a = lo, b = hi;
                 while (a < b) {
                     const uint32_t mid = (a + b) >> 1;
-                    if (cmp_min(mid) >= 0)
+                    const RegSlot &sl = slots[mid];
+                    if (cmp_key(key, klen, k0, k1, sl.min_be, ranges + sl.min_off, sl.min_len) >= 0)
                         a = mid + 1;
                     else
                         b = mid;
                 }
-                if (a > lo && cmp_max(a - 1) <= 0) hit = (int)a - 1;
+                if (a > lo) {
+                    const RegSlot &sl = slots[a - 1];
+                    if (cmp_key(key, klen, k0, k1, sl.max_be, ranges + sl.max_off, sl.max_len) <= 0) hit = (int)a - 1;
+                }
             } else {
-                for (uint32_t s = lo; s < hi && hit < 0; ++s)
-                    if (cmp_min(s) >= 0 && cmp_max(s) <= 0) hit = (int)s;
+                for (uint32_t s = lo; s < hi && hit < 0; ++s) {
+                    const RegSlot &sl = slots[s];
+                    if (cmp_key(key, klen, k0, k1, sl.min_be, ranges + sl.min_off, sl.min_len) >= 0 &&
+                        cmp_key(key, klen, k0, k1, sl.max_be, ranges + sl.max_off, sl.max_len) <= 0)
+                        hit = (int)s;
+                }
             }
             if (hit >= 0) take(slots[hit]);
         }
@@ -1044,10 +1014,9 @@ hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t ns
     const int mode = !cand ? 0 : nslots <= kMaxSlots ? 1 : 2;
     return with_src(kb, [&](auto src) {
         using S = decltype(src);
-        const size_t lds = mode == 2 && nslots <= kMgBoundsMax ? (size_t)nslots * 32 : 0;
         auto go = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), lds, s, src, kb, slots, nslots, lay, ranges, maybe,
-                               cand, cap, key_order, (uint32_t)options().multiget_xcd, seg);
+            hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe, cand,
+                               cap, key_order, (uint32_t)options().multiget_xcd, seg);
             return hipGetLastError();
         };
         if (lay.all_k7_m32) {
