@@ -99,10 +99,12 @@ def parse():
                          "launcher spawns the N rank processes itself (launch_ranks)")
     ap.add_argument("--launch-check", action="store_true",
                     help="spawn/join the ranks and check the process group only (gloo, no GPU); CPU tests")
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--time-every", type=int, default=4,
                     help="record the build/probe launch timers on every Nth timed step (and the last)")
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=50,
+                    help="untimed steps first: the GPU's clocks rise over the first ~50 steps of this load "
+                         "(0.467-0.470 ms per step after 3, 0.439-0.442 after 50-200: profiles/r06m_warmup_steps.json)")
     ap.add_argument("--kernel-reps", type=int, default=20,
                     help="after the timed steps (outside their wall clock), this many more steps with every launch "
                          "timed by HIP events: the kernel_timing median / min (SURVEY 8(d)); 0 skips; one GPU only")
@@ -1172,7 +1174,7 @@ def roofline_of(st, kern_ms: dict, config: str) -> dict:
                       for d, v in kern.items()}}
 
 
-C5_VARIANT_STEPS = {"steps": 10, "warmup": 3}  # at most: a shorter headline run shortens them too
+C5_VARIANT_STEPS = {"steps": 20, "warmup": 10}  # at most: a shorter headline run shortens them too
 
 
 def dist_variants(args, world: int) -> list:
@@ -1403,9 +1405,9 @@ def timed_run(args, st, seb, torch, dist, world, rank, dev):
             "kernel_timing": kernel_timing, **wait}
 
 
-SECONDARY = (("c4", ["--steps", "10", "--warmup", "3"]),
-             ("c5", ["--steps", "10", "--warmup", "3"]),
-             ("lsm", ["--steps", "10", "--warmup", "3"]), ("lsm_wide", ["--steps", "10", "--warmup", "3"]),
+SECONDARY = (("c4", ["--steps", "20", "--warmup", "30"]),  # each child a fresh context: clocks ramp again
+             ("c5", ["--steps", "20", "--warmup", "30"]),
+             ("lsm", ["--steps", "20", "--warmup", "30"]), ("lsm_wide", ["--steps", "20", "--warmup", "30"]),
              ("flush", []))
 
 
