@@ -88,8 +88,8 @@ hipError_t launch_route_partition(const KeyBatch &kb, uint32_t bits, uint32_t *p
 hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mode, uint32_t *crc, uint8_t *ok,
                           hipStream_t s);
 // The scatter-free order's segment tables (multiget_order 1): segment s = b * C + c is bucket b's
-// run of chunk c; seg[s] = its first sorted row (low 32 bits, non-decreasing in s) | (c << 11 |
-// the run's offset in the chunk's bucket-sorted keys) << 32; wstart[w] = the segment of row 64 w.
+// run of chunk c; seg[s] = its first sorted row (low 32 bits, non-decreasing in s) | (c / 2 << 12 |
+// the run's offset in the chunk pair's bucket-sorted keys) << 32; wstart[w] = the segment of row 64 w.
 struct MgSeg {
     const uint64_t *seg = nullptr;  // null: rows are read linearly (or through key_order)
     const uint32_t *wstart = nullptr;

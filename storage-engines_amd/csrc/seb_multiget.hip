@@ -582,17 +582,17 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const B *__restr
 // ---- the scatter-free order (multiget_order 1, aligned 16-B keys; round 6).  The
 // sorted rows are those k_mg_scatter produced (bucket-major, batch order within a bucket), but no
 // pass moves the keys across the batch:
-//   k_mg_bucket_sort  chunk c: each key's bucket, the chunk's stable ranks (chunk_positions) and its
-//                     keys written back sorted by bucket inside the chunk's own 32 KB (keys_cs); per
-//                     segment s = b * C + c (bucket b's run of chunk c) its count cnt[s] and where the
-//                     run starts in keys_cs, seghi[s] = chunk << 11 | offset in the chunk
+//   k_mg_bucket_sort  a pair of chunks: each key's bucket, each chunk's stable ranks (chunk_positions)
+//                     and the pair's keys written back sorted by bucket inside the pair's own 64 KB
+//                     (keys_cs); per segment s = b * C + c (bucket b's run of chunk c) its count
+//                     cnt[s] and where the run starts in keys_cs, seghi[s] = pair << 12 | offset
 //   k_mg_rows_pieces  scans each bucket's row of C counts in pieces of kMgPiece chunks
 //   k_mg_bases        bucket bases (scan of the bucket totals) plus the pieces' prefixes
 //   k_mg_segrows      seg[s] = first sorted row | seghi[s] << 32 (rows non-decreasing in s) and the
 //                     segment holding row 64 w of every wave w (wstart)
 // k_multiget finds each row's segment from its wave's start and a 64-entry window of seg
 // (mg_seg_key): three dependent loads (wstart, the window, the key) and no division; every
-// segment's keys are contiguous in keys_cs.  k_mg_unpermute reads each chunk's run starts from seg.
+// segment's keys are contiguous in keys_cs, and a bucket's runs of a chunk pair adjacent.  k_mg_unpermute reads each chunk's run starts from seg.
 __device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uint64_t j) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t r = (uint32_t)j;
@@ -620,14 +620,20 @@ __device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uin
         ent = sg.seg[a];
     }
     const uint32_t h = (uint32_t)(ent >> 32);
-    return (uint64_t)(h >> 11) * kMgChunk + (h & 2047u) + (r - (uint32_t)ent);
+    return (uint64_t)(h >> 12) * (2 * kMgChunk) + (h & 4095u) + (r - (uint32_t)ent);
 }
 
-// LDS (dynamic): stage uint4[kMgChunk] | pmin u64[2 (nb - 1)] | cw u32[kMgWaves nb] | loc u32[nb + 1] | wsum u32[4]
+// LDS (dynamic): stage uint4[2 kMgChunk] | pmin u64[2 (nb - 1)] | cw u32[kMgWaves nb] | loc u32[nb + 1]
+// | loca u32[nb + 1] | wsum u32[4]
 static size_t mg_bucket_sort_lds(uint32_t nb) {
-    return (size_t)kMgChunk * 16 + (size_t)16 * (nb - 1) + 4 * ((size_t)kMgWaves * nb + nb + 1 + 4);
+    return (size_t)2 * kMgChunk * 16 + (size_t)16 * (nb - 1) + 4 * ((size_t)kMgWaves * nb + 2 * (nb + 1) + 4);
 }
 
+// One workgroup per pair of chunks (a 4096-key super-chunk): each chunk ranked on its own (its
+// segments, counts and the unpermute's ranks stay per 2048-key chunk), but the pair's keys are
+// written back sorted by bucket across both, so bucket b's runs of the two chunks are adjacent in
+// keys_cs (chunk A's run, then B's): a segment of a 161-file level holds ≈13 keys, a pair's ≈25.
+// Key of A at rank p (bucket b): p + locB[b]; key of B at rank p: p + locA[b + 1].
 template <typename B>
 __global__ __launch_bounds__(256) void k_mg_bucket_sort(uint64_t n, const uint4 *__restrict__ keys,
                                                         const RegSlot *__restrict__ slots, uint32_t lo, uint32_t hi,
@@ -638,44 +644,78 @@ __global__ __launch_bounds__(256) void k_mg_bucket_sort(uint64_t n, const uint4 
     extern __shared__ uint4 mgb_lds[];
     const uint32_t nb = hi - lo + 1;
     uint4 *stage = mgb_lds;
-    uint64_t *pmin = (uint64_t *)(stage + kMgChunk);
+    uint64_t *pmin = (uint64_t *)(stage + 2 * kMgChunk);
     uint32_t *cw = (uint32_t *)(pmin + 2 * (nb - 1));
     uint32_t *loc = cw + kMgWaves * nb;
-    uint32_t *wsum = loc + nb + 1;
+    uint32_t *loca = loc + nb + 1;
+    uint32_t *wsum = loca + nb + 1;
     for (uint32_t u = threadIdx.x; u < nb - 1; u += blockDim.x) {
         pmin[2 * u] = slots[lo + u].min_be[0];
         pmin[2 * u + 1] = slots[lo + u].min_be[1];
     }
-    const uint64_t c0 = (uint64_t)blockIdx.x * kMgChunk;
-    const uint32_t cn = (uint32_t)min((uint64_t)kMgChunk, n - c0);
-    uint4 v[kMgSteps];
+    const uint32_t ca = 2 * blockIdx.x;
+    const bool has_b = ca + 1 < C;
+    const uint64_t s0 = (uint64_t)ca * kMgChunk;
+    const uint32_t cna = (uint32_t)min((uint64_t)kMgChunk, n - s0);
+    const uint32_t cnb = has_b ? (uint32_t)min((uint64_t)kMgChunk, n - s0 - kMgChunk) : 0u;
+    uint4 va[kMgSteps], vb[kMgSteps];
 #pragma unroll
-    for (uint32_t s = 0; s < kMgSteps; ++s) v[s] = keys[c0 + min(chunk_key(s), cn - 1)];  // clamped: no branch
-    __syncthreads();
-    uint32_t bk[kMgSteps], pos[kMgSteps];
+    for (uint32_t s = 0; s < kMgSteps; ++s) va[s] = keys[s0 + min(chunk_key(s), cna - 1)];  // clamped: no branch
+    if (has_b) {
 #pragma unroll
-    for (uint32_t s = 0; s < kMgSteps; ++s) {
-        const uint32_t q = chunk_key(s);
-        bk[s] = nb;
-        if (q < cn) {
-            const uint64_t k0 = __builtin_bswap64((uint64_t)v[s].x | ((uint64_t)v[s].y << 32));
-            const uint64_t k1 = __builtin_bswap64((uint64_t)v[s].z | ((uint64_t)v[s].w << 32));
-            bk[s] = mg_bisect((const uint8_t *)(keys + c0 + q), 16, k0, k1, slots, lo, hi, ranges, pmin) - lo;
-        }
+        for (uint32_t s = 0; s < kMgSteps; ++s) vb[s] = keys[s0 + kMgChunk + min(chunk_key(s), cnb - 1)];
     }
-    chunk_positions(bk, cn, nb, bits, cw, loc, wsum, pos);
+    __syncthreads();
+    auto buckets = [&](const uint4 (&v)[kMgSteps], uint64_t c0, uint32_t cn, uint32_t (&bk)[kMgSteps]) {
+#pragma unroll
+        for (uint32_t s = 0; s < kMgSteps; ++s) {
+            const uint32_t q = chunk_key(s);
+            bk[s] = nb;
+            if (q < cn) {
+                const uint64_t k0 = __builtin_bswap64((uint64_t)v[s].x | ((uint64_t)v[s].y << 32));
+                const uint64_t k1 = __builtin_bswap64((uint64_t)v[s].z | ((uint64_t)v[s].w << 32));
+                bk[s] = mg_bisect((const uint8_t *)(keys + c0 + q), 16, k0, k1, slots, lo, hi, ranges, pmin) - lo;
+            }
+        }
+    };
+    uint32_t bka[kMgSteps], posa[kMgSteps], bkb[kMgSteps], posb[kMgSteps];
+    buckets(va, s0, cna, bka);
+    chunk_positions(bka, cna, nb, bits, cw, loc, wsum, posa);
+    for (uint32_t u = threadIdx.x; u <= nb; u += blockDim.x) loca[u] = loc[u];
+    __syncthreads();
+    if (has_b) {
+        buckets(vb, s0 + kMgChunk, cnb, bkb);
+        chunk_positions(bkb, cnb, nb, bits, cw, loc, wsum, posb);
+    } else {
+        for (uint32_t u = threadIdx.x; u <= nb; u += blockDim.x) loc[u] = 0;
+        __syncthreads();
+    }
 #pragma unroll
     for (uint32_t s = 0; s < kMgSteps; ++s)
-        if (bk[s] < nb) {
-            stage[pos[s]] = v[s];
-            bucket[c0 + chunk_key(s)] = (B)bk[s];
+        if (bka[s] < nb) {
+            stage[posa[s] + loc[bka[s]]] = va[s];
+            bucket[s0 + chunk_key(s)] = (B)bka[s];
         }
+    if (has_b) {
+#pragma unroll
+        for (uint32_t s = 0; s < kMgSteps; ++s)
+            if (bkb[s] < nb) {
+                stage[posb[s] + loca[bkb[s] + 1]] = vb[s];
+                bucket[s0 + kMgChunk + chunk_key(s)] = (B)bkb[s];
+            }
+    }
+    // per segment: its count and where its run starts in keys_cs, pair << 12 | offset in the pair
+    // (an empty run may sit at offset 4096: masked, never read)
     for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {
-        cnt[(uint64_t)u * C + blockIdx.x] = loc[u + 1] - loc[u];
-        seghi[(uint64_t)u * C + blockIdx.x] = (blockIdx.x << 11) | (loc[u] & 2047u);  // (empty runs at 2048: unused)
+        cnt[(uint64_t)u * C + ca] = loca[u + 1] - loca[u];
+        seghi[(uint64_t)u * C + ca] = (blockIdx.x << 12) | ((loca[u] + loc[u]) & 4095u);
+        if (has_b) {
+            cnt[(uint64_t)u * C + ca + 1] = loc[u + 1] - loc[u];
+            seghi[(uint64_t)u * C + ca + 1] = (blockIdx.x << 12) | ((loca[u + 1] + loc[u]) & 4095u);
+        }
     }
     __syncthreads();
-    for (uint32_t q = threadIdx.x; q < cn; q += blockDim.x) keys_cs[c0 + q] = stage[q];
+    for (uint32_t q = threadIdx.x; q < cna + cnb; q += blockDim.x) keys_cs[s0 + q] = stage[q];
 }
 
 // block (p, b): exclusive scan of bucket b's counts of chunks [p * kMgPiece, ...) in place;
@@ -898,7 +938,7 @@ static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *s
         hipError_t a = hipFuncSetAttribute((const void *)k_mg_bucket_sort<B>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds);
         if (a != hipSuccess) return a;
-        hipLaunchKernelGGL(k_mg_bucket_sort<B>, dim3((unsigned)C), dim3(256), lds, s, n, (const uint4 *)kb.data, slots, lo,
+        hipLaunchKernelGGL(k_mg_bucket_sort<B>, dim3((unsigned)((C + 1) / 2)), dim3(256), lds, s, n, (const uint4 *)kb.data, slots, lo,
                            hi, ranges, bits, (B *)bucket, cnt, seghi, keys_cs, (uint32_t)C);
         return hipGetLastError();
     };
