@@ -87,12 +87,14 @@ hipError_t launch_route_partition(const KeyBatch &kb, uint32_t bits, uint32_t *p
                                   uint16_t *shard_out, void *ws, uint64_t ws_bytes, hipStream_t s);
 hipError_t launch_wal_crc(uint8_t *data, const uint64_t *off, uint64_t n, int mode, uint32_t *crc, uint8_t *ok,
                           hipStream_t s);
-// The scatter-free order's segment tables (multiget_order 1): segment s = b * C + c is bucket b's
-// run of chunk c; seg[s] = its first sorted row (low 32 bits, non-decreasing in s) | (c / 2 << 12 |
-// the run's offset in the chunk pair's bucket-sorted keys) << 32; wstart[w] = the segment of row 64 w.
+// The scatter-free order's segment tables (multiget_order 1): segment s = b * C + sc is bucket b's
+// run of 4096-key super-chunk sc; seg[s] = its first sorted row (low 32 bits, non-decreasing in s)
+// | (sc << 12 | the run's offset in the super-chunk's bucket-sorted keys) << 32; half[s] = its keys
+// in the super-chunk's first 2048-key chunk; wstart[w] = the segment of row 64 w.
 struct MgSeg {
     const uint64_t *seg = nullptr;  // null: rows are read linearly (or through key_order)
     const uint32_t *wstart = nullptr;
+    const uint32_t *half = nullptr;
     uint32_t nseg = 0, C = 0, nb = 0, pad = 0;
 };
 // cand != null: the list form (cap u16 slots per key, any nslots) instead of masks.

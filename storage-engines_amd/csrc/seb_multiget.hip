@@ -264,6 +264,8 @@ constexpr uint32_t kMgBucketThreads = 1024;
 
 constexpr uint32_t kMgWaves = 4;                      // 256-thread ordering blocks
 constexpr uint32_t kMgSteps = kMgChunk / kMgWaves / 64;  // 64-key steps of one wave's chunk segment
+constexpr uint32_t kMgSuper = 2 * kMgChunk;              // the scatter-free order's bucket-sort unit
+constexpr uint32_t kMgSuperWaves = 2 * kMgWaves;         // its 512-thread blocks
 
 __device__ __forceinline__ void key_at(const KeyBatch &kb, uint64_t i, const uint8_t *&key, uint32_t &klen) {
     if (kb.offsets) {
@@ -275,10 +277,11 @@ __device__ __forceinline__ void key_at(const KeyBatch &kb, uint64_t i, const uin
     }
 }
 
-// Exclusive scan of a[0..n) in LDS by a 256-thread block; returns the total.  Every thread must
-// call it; it synchronises before returning.
+// Exclusive scan of a[0..n) in LDS by an NT-thread block (wsum: NT / 64 words); returns the total.
+// Every thread must call it; it synchronises before returning.
+template <uint32_t NT = 256>
 __device__ uint32_t block_scan_lds(uint32_t *a, uint32_t n, uint32_t *wsum) {
-    const uint32_t per = (n + 255) / 256;
+    const uint32_t per = (n + NT - 1) / NT;
     const uint32_t b0 = min(threadIdx.x * per, n), b1 = min(b0 + per, n);
     uint32_t own = 0;
     for (uint32_t t = b0; t < b1; ++t) own += a[t];
@@ -293,7 +296,9 @@ __device__ uint32_t block_scan_lds(uint32_t *a, uint32_t n, uint32_t *wsum) {
     __syncthreads();
     uint32_t run = x - own;
     for (uint32_t v = 0; v < w; ++v) run += wsum[v];
-    const uint32_t total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    uint32_t total = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < NT / 64; ++v) total += wsum[v];
     for (uint32_t t = b0; t < b1; ++t) {
         const uint32_t c = a[t];
         a[t] = run;
@@ -322,11 +327,14 @@ __device__ __forceinline__ uint32_t chunk_key(uint32_t s) {
 // count per bucket (cw[w][b]); then the buckets' chunk offsets (loc) and the waves before it.
 // bk[s]: bucket of key chunk_key(s) (>= nb for keys past cnt).  loc[0..nb] ends as the exclusive
 // scan of the chunk's bucket counts, loc[nb] = cnt.  Every thread calls it; it synchronises.
+// WAVES: the block's waves (4: a 2048-key chunk; 8: the 4096-key super-chunk of k_mg_bucket_sort);
+// each wave ranks 512 keys.
+template <uint32_t WAVES = kMgWaves>
 __device__ __forceinline__ void chunk_positions(const uint32_t (&bk)[kMgSteps], uint32_t cnt, uint32_t nb,
                                                 uint32_t bits, uint32_t *cw, uint32_t *loc, uint32_t *wsum,
                                                 uint32_t (&pos)[kMgSteps]) {
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (uint32_t u = threadIdx.x; u < kMgWaves * nb; u += blockDim.x) cw[u] = 0;
+    for (uint32_t u = threadIdx.x; u < WAVES * nb; u += blockDim.x) cw[u] = 0;
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
     uint32_t *mine = cw + w * nb;
@@ -353,7 +361,7 @@ __device__ __forceinline__ void chunk_positions(const uint32_t (&bk)[kMgSteps], 
     __syncthreads();
     for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {
         uint32_t t = 0;
-        for (uint32_t v = 0; v < kMgWaves; ++v) {  // cw[v][u] becomes the waves-before offset
+        for (uint32_t v = 0; v < WAVES; ++v) {  // cw[v][u] becomes the waves-before offset
             const uint32_t c = cw[v * nb + u];
             cw[v * nb + u] = t;
             t += c;
@@ -361,7 +369,7 @@ __device__ __forceinline__ void chunk_positions(const uint32_t (&bk)[kMgSteps], 
         loc[u] = t;
     }
     __syncthreads();
-    block_scan_lds(loc, nb, wsum);
+    block_scan_lds<64 * WAVES>(loc, nb, wsum);
     if (threadIdx.x == 0) loc[nb] = cnt;
 #pragma unroll
     for (uint32_t s = 0; s < kMgSteps; ++s) {
@@ -582,17 +590,18 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const B *__restr
 // ---- the scatter-free order (multiget_order 1, aligned 16-B keys; round 6).  The
 // sorted rows are those k_mg_scatter produced (bucket-major, batch order within a bucket), but no
 // pass moves the keys across the batch:
-//   k_mg_bucket_sort  a pair of chunks: each key's bucket, each chunk's stable ranks (chunk_positions)
-//                     and the pair's keys written back sorted by bucket inside the pair's own 64 KB
-//                     (keys_cs); per segment s = b * C + c (bucket b's run of chunk c) its count
-//                     cnt[s] and where the run starts in keys_cs, seghi[s] = pair << 12 | offset
+//   k_mg_bucket_sort  a 4096-key super-chunk (two chunks): each key's bucket, its stable rank in the
+//                     super-chunk (chunk_positions over 8 waves) and the keys written back sorted by
+//                     bucket inside the super-chunk's own 64 KB (keys_cs); per segment s = b * C2 + sc
+//                     (bucket b's run of super-chunk sc) its count cnt[s], where the run starts in
+//                     keys_cs, seghi[s] = sc << 12 | offset, and its keys in the first chunk, half[s]
 //   k_mg_rows_pieces  scans each bucket's row of C counts in pieces of kMgPiece chunks
 //   k_mg_bases        bucket bases (scan of the bucket totals) plus the pieces' prefixes
 //   k_mg_segrows      seg[s] = first sorted row | seghi[s] << 32 (rows non-decreasing in s) and the
 //                     segment holding row 64 w of every wave w (wstart)
 // k_multiget finds each row's segment from its wave's start and a 64-entry window of seg
 // (mg_seg_key): three dependent loads (wstart, the window, the key) and no division; every
-// segment's keys are contiguous in keys_cs, and a bucket's runs of a chunk pair adjacent.  k_mg_unpermute reads each chunk's run starts from seg.
+// segment's keys are contiguous in keys_cs.  k_mg_unpermute reads each chunk's run starts from seg.
 __device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uint64_t j) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t r = (uint32_t)j;
@@ -620,102 +629,74 @@ __device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uin
         ent = sg.seg[a];
     }
     const uint32_t h = (uint32_t)(ent >> 32);
-    return (uint64_t)(h >> 12) * (2 * kMgChunk) + (h & 4095u) + (r - (uint32_t)ent);
+    return (uint64_t)(h >> 12) * kMgSuper + (h & 4095u) + (r - (uint32_t)ent);
 }
 
-// LDS (dynamic): stage uint4[2 kMgChunk] | pmin u64[2 (nb - 1)] | cw u32[kMgWaves nb] | loc u32[nb + 1]
-// | loca u32[nb + 1] | wsum u32[4]
+// The bucket sort's unit: a super-chunk of two 2048-key chunks, ranked as one by a 512-thread block
+// (8 waves of 512 keys), so a bucket's run of it holds twice the keys of a chunk's run: on a
+// 161-file level ≈25 keys instead of ≈13, which halves the fragments k_multiget reads its keys in.
+// The rows are unchanged: within a bucket, super-chunk order then stable rank = chunk order then
+// rank, so k_mg_unpermute keeps its 2048-key chunks and finds chunk 2sc+1's run start past the
+// first half's keys of the bucket (half[]).
+
+// LDS (dynamic): stage uint4[kMgSuper] | pmin u64[2 (nb - 1)] | cw u32[8 nb] | loc u32[nb + 1] | wsum u32[8]
 static size_t mg_bucket_sort_lds(uint32_t nb) {
-    return (size_t)2 * kMgChunk * 16 + (size_t)16 * (nb - 1) + 4 * ((size_t)kMgWaves * nb + 2 * (nb + 1) + 4);
+    return (size_t)kMgSuper * 16 + (size_t)16 * (nb - 1) + 4 * ((size_t)kMgSuperWaves * nb + nb + 1 + 8);
 }
 
-// One workgroup per pair of chunks (a 4096-key super-chunk): each chunk ranked on its own (its
-// segments, counts and the unpermute's ranks stay per 2048-key chunk), but the pair's keys are
-// written back sorted by bucket across both, so bucket b's runs of the two chunks are adjacent in
-// keys_cs (chunk A's run, then B's): a segment of a 161-file level holds ≈13 keys, a pair's ≈25.
-// Key of A at rank p (bucket b): p + locB[b]; key of B at rank p: p + locA[b + 1].
 template <typename B>
-__global__ __launch_bounds__(256) void k_mg_bucket_sort(uint64_t n, const uint4 *__restrict__ keys,
+__global__ __launch_bounds__(512) void k_mg_bucket_sort(uint64_t n, const uint4 *__restrict__ keys,
                                                         const RegSlot *__restrict__ slots, uint32_t lo, uint32_t hi,
                                                         const uint8_t *__restrict__ ranges, uint32_t bits,
                                                         B *__restrict__ bucket, uint32_t *__restrict__ cnt,
-                                                        uint32_t *__restrict__ seghi, uint4 *__restrict__ keys_cs,
-                                                        uint32_t C) {
+                                                        uint32_t *__restrict__ seghi, uint32_t *__restrict__ half,
+                                                        uint4 *__restrict__ keys_cs, uint32_t C2) {
     extern __shared__ uint4 mgb_lds[];
     const uint32_t nb = hi - lo + 1;
     uint4 *stage = mgb_lds;
-    uint64_t *pmin = (uint64_t *)(stage + 2 * kMgChunk);
+    uint64_t *pmin = (uint64_t *)(stage + kMgSuper);
     uint32_t *cw = (uint32_t *)(pmin + 2 * (nb - 1));
-    uint32_t *loc = cw + kMgWaves * nb;
-    uint32_t *loca = loc + nb + 1;
-    uint32_t *wsum = loca + nb + 1;
+    uint32_t *loc = cw + kMgSuperWaves * nb;
+    uint32_t *wsum = loc + nb + 1;
     for (uint32_t u = threadIdx.x; u < nb - 1; u += blockDim.x) {
         pmin[2 * u] = slots[lo + u].min_be[0];
         pmin[2 * u + 1] = slots[lo + u].min_be[1];
     }
-    const uint32_t ca = 2 * blockIdx.x;
-    const bool has_b = ca + 1 < C;
-    const uint64_t s0 = (uint64_t)ca * kMgChunk;
-    const uint32_t cna = (uint32_t)min((uint64_t)kMgChunk, n - s0);
-    const uint32_t cnb = has_b ? (uint32_t)min((uint64_t)kMgChunk, n - s0 - kMgChunk) : 0u;
-    uint4 va[kMgSteps], vb[kMgSteps];
+    const uint64_t c0 = (uint64_t)blockIdx.x * kMgSuper;
+    const uint32_t cn = (uint32_t)min((uint64_t)kMgSuper, n - c0);
+    uint4 v[kMgSteps];
 #pragma unroll
-    for (uint32_t s = 0; s < kMgSteps; ++s) va[s] = keys[s0 + min(chunk_key(s), cna - 1)];  // clamped: no branch
-    if (has_b) {
-#pragma unroll
-        for (uint32_t s = 0; s < kMgSteps; ++s) vb[s] = keys[s0 + kMgChunk + min(chunk_key(s), cnb - 1)];
-    }
+    for (uint32_t s = 0; s < kMgSteps; ++s) v[s] = keys[c0 + min(chunk_key(s), cn - 1)];  // clamped: no branch
     __syncthreads();
-    auto buckets = [&](const uint4 (&v)[kMgSteps], uint64_t c0, uint32_t cn, uint32_t (&bk)[kMgSteps]) {
+    uint32_t bk[kMgSteps], pos[kMgSteps];
 #pragma unroll
-        for (uint32_t s = 0; s < kMgSteps; ++s) {
-            const uint32_t q = chunk_key(s);
-            bk[s] = nb;
-            if (q < cn) {
-                const uint64_t k0 = __builtin_bswap64((uint64_t)v[s].x | ((uint64_t)v[s].y << 32));
-                const uint64_t k1 = __builtin_bswap64((uint64_t)v[s].z | ((uint64_t)v[s].w << 32));
-                bk[s] = mg_bisect((const uint8_t *)(keys + c0 + q), 16, k0, k1, slots, lo, hi, ranges, pmin) - lo;
-            }
+    for (uint32_t s = 0; s < kMgSteps; ++s) {
+        const uint32_t q = chunk_key(s);
+        bk[s] = nb;
+        if (q < cn) {
+            const uint64_t k0 = __builtin_bswap64((uint64_t)v[s].x | ((uint64_t)v[s].y << 32));
+            const uint64_t k1 = __builtin_bswap64((uint64_t)v[s].z | ((uint64_t)v[s].w << 32));
+            bk[s] = mg_bisect((const uint8_t *)(keys + c0 + q), 16, k0, k1, slots, lo, hi, ranges, pmin) - lo;
         }
-    };
-    uint32_t bka[kMgSteps], posa[kMgSteps], bkb[kMgSteps], posb[kMgSteps];
-    buckets(va, s0, cna, bka);
-    chunk_positions(bka, cna, nb, bits, cw, loc, wsum, posa);
-    for (uint32_t u = threadIdx.x; u <= nb; u += blockDim.x) loca[u] = loc[u];
-    __syncthreads();
-    if (has_b) {
-        buckets(vb, s0 + kMgChunk, cnb, bkb);
-        chunk_positions(bkb, cnb, nb, bits, cw, loc, wsum, posb);
-    } else {
-        for (uint32_t u = threadIdx.x; u <= nb; u += blockDim.x) loc[u] = 0;
-        __syncthreads();
     }
+    chunk_positions<kMgSuperWaves>(bk, cn, nb, bits, cw, loc, wsum, pos);
 #pragma unroll
     for (uint32_t s = 0; s < kMgSteps; ++s)
-        if (bka[s] < nb) {
-            stage[posa[s] + loc[bka[s]]] = va[s];
-            bucket[s0 + chunk_key(s)] = (B)bka[s];
+        if (bk[s] < nb) {
+            stage[pos[s]] = v[s];
+            bucket[c0 + chunk_key(s)] = (B)bk[s];
         }
-    if (has_b) {
-#pragma unroll
-        for (uint32_t s = 0; s < kMgSteps; ++s)
-            if (bkb[s] < nb) {
-                stage[posb[s] + loca[bkb[s] + 1]] = vb[s];
-                bucket[s0 + kMgChunk + chunk_key(s)] = (B)bkb[s];
-            }
-    }
-    // per segment: its count and where its run starts in keys_cs, pair << 12 | offset in the pair
-    // (an empty run may sit at offset 4096: masked, never read)
+    // per segment s = b * C2 + sc: its count, where its run starts in keys_cs (sc << 12 | offset;
+    // an empty run may sit at 4096: masked, never read) and its keys in the first 2048-key chunk
+    // (waves 0-3: cw[4][b], the waves-before offset chunk_positions left there)
     for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {
-        cnt[(uint64_t)u * C + ca] = loca[u + 1] - loca[u];
-        seghi[(uint64_t)u * C + ca] = (blockIdx.x << 12) | ((loca[u] + loc[u]) & 4095u);
-        if (has_b) {
-            cnt[(uint64_t)u * C + ca + 1] = loc[u + 1] - loc[u];
-            seghi[(uint64_t)u * C + ca + 1] = (blockIdx.x << 12) | ((loca[u + 1] + loc[u]) & 4095u);
-        }
+        const uint64_t sg = (uint64_t)u * C2 + blockIdx.x;
+        cnt[sg] = loc[u + 1] - loc[u];
+        seghi[sg] = (blockIdx.x << 12) | (loc[u] & 4095u);
+        half[sg] = cw[kMgWaves * nb + u];
     }
     __syncthreads();
-    for (uint32_t q = threadIdx.x; q < cna + cnb; q += blockDim.x) keys_cs[s0 + q] = stage[q];
+    for (uint32_t q = threadIdx.x; q < cn; q += blockDim.x) keys_cs[c0 + q] = stage[q];
 }
 
 // block (p, b): exclusive scan of bucket b's counts of chunks [p * kMgPiece, ...) in place;
@@ -797,7 +778,8 @@ template <typename G, typename B>
 __global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const B *__restrict__ bucket,
                                                       const uint32_t *__restrict__ runs, uint32_t nb, uint32_t bits,
                                                       const G *__restrict__ answers, G *__restrict__ out,
-                                                      uint32_t ge, const uint64_t *__restrict__ seg, uint32_t C) {
+                                                      uint32_t ge, const uint64_t *__restrict__ seg,
+                                                      const uint32_t *__restrict__ half, uint32_t C2) {
     extern __shared__ uint4 mgu_lds[];
     constexpr uint32_t kSlice = sizeof(G) >= kMgStage ? 1 : kMgStage / sizeof(G);  // granules per key per pass
     uint32_t *loc = (uint32_t *)mgu_lds;
@@ -811,8 +793,14 @@ __global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const B *__res
     const uint32_t cnt = (uint32_t)min((uint64_t)kMgChunk, n - c0);
     // the chunk's run starts: from the scatter's runs table, or the segment table's rows (the
     // scatter-free order; bucket-major, so strided, but a line holds 16 neighbouring chunks)
-    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x)
-        rbase[u] = seg ? (uint32_t)seg[(uint64_t)u * C + blockIdx.x] : runs[(uint64_t)blockIdx.x * nb + u];
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {
+        if (seg) {  // super-chunk sc = chunk / 2: its bucket run, past the first chunk's keys for an odd chunk
+            const uint64_t sg = (uint64_t)u * C2 + (blockIdx.x >> 1);
+            rbase[u] = (uint32_t)seg[sg] + ((blockIdx.x & 1u) ? half[sg] : 0u);
+        } else {
+            rbase[u] = runs[(uint64_t)blockIdx.x * nb + u];
+        }
+    }
     uint32_t bk[kMgSteps], pos[kMgSteps];
     load_chunk_buckets(bucket, c0, c0 + cnt, nb, bk);
     chunk_positions(bk, cnt, nb, bits, cw, loc, wsum, pos);  // synchronises (rbase is visible after it)
@@ -899,10 +887,11 @@ static bool order_segments(const KeyBatch &kb) { return multiget_order_moves(kb)
 
 static uint32_t seg_pieces(uint64_t C) { return (uint32_t)((C + kMgPiece - 1) / kMgPiece); }
 
-// The segment path's tables after the bucket ids: cnt, seghi, seg, wstart, piece totals.
+// The segment path's tables after the bucket ids, per super-chunk segment: cnt, seghi, half, seg,
+// then wstart and the piece totals.
 static uint64_t seg_bytes(uint64_t n, uint32_t nb) {
-    const uint64_t C = (n + kMgChunk - 1) / kMgChunk, ns = C * nb;
-    return al256(4 * ns) + al256(4 * ns) + al256(8 * ns) + al256(4 * ((n + 63) / 64)) + al256(4ull * nb * seg_pieces(C));
+    const uint64_t C2 = (n + kMgSuper - 1) / kMgSuper, ns = C2 * nb;
+    return 3 * al256(4 * ns) + al256(8 * ns) + al256(4 * ((n + 63) / 64)) + al256(4ull * nb * seg_pieces(C2));
 }
 
 uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes, uint32_t nb) {
@@ -914,16 +903,17 @@ uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes, uint32_
 }
 
 // multiget_order 1 for aligned fixed 16-B keys: k_mg_bucket_sort, k_mg_rows_pieces, k_mg_bases,
-// k_mg_segrows.
+// k_mg_segrows, over super-chunk segments.
 static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
                                             const uint8_t *ranges, void *ws, MgOrder *mo, hipStream_t s) {
     const uint32_t nb = hi - lo + 1;
-    const uint64_t n = kb.n, C = (n + kMgChunk - 1) / kMgChunk, ns = C * nb;
-    const uint32_t P = seg_pieces(C);
+    const uint64_t n = kb.n, C2 = (n + kMgSuper - 1) / kMgSuper, ns = C2 * nb;
+    const uint32_t P = seg_pieces(C2);
     uint8_t *p = (uint8_t *)ws;
     void *bucket = p;
     uint32_t *cnt = (uint32_t *)(p += al256(n * 2));
     uint32_t *seghi = (uint32_t *)(p += al256(4 * ns));
+    uint32_t *half = (uint32_t *)(p += al256(4 * ns));
     uint64_t *seg = (uint64_t *)(p += al256(4 * ns));
     uint32_t *wstart = (uint32_t *)(p += al256(8 * ns));
     uint32_t *ptot = (uint32_t *)(p += al256(4 * ((n + 63) / 64)));
@@ -938,16 +928,16 @@ static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *s
         hipError_t a = hipFuncSetAttribute((const void *)k_mg_bucket_sort<B>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)lds);
         if (a != hipSuccess) return a;
-        hipLaunchKernelGGL(k_mg_bucket_sort<B>, dim3((unsigned)((C + 1) / 2)), dim3(256), lds, s, n, (const uint4 *)kb.data, slots, lo,
-                           hi, ranges, bits, (B *)bucket, cnt, seghi, keys_cs, (uint32_t)C);
+        hipLaunchKernelGGL(k_mg_bucket_sort<B>, dim3((unsigned)C2), dim3(512), lds, s, n, (const uint4 *)kb.data, slots,
+                           lo, hi, ranges, bits, (B *)bucket, cnt, seghi, half, keys_cs, (uint32_t)C2);
         return hipGetLastError();
     };
     hipError_t e = b8 ? sort(uint8_t{}) : sort(uint16_t{});
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_mg_rows_pieces, dim3(P, nb), dim3(256), 0, s, cnt, (uint32_t)C, P, ptot);
+    hipLaunchKernelGGL(k_mg_rows_pieces, dim3(P, nb), dim3(256), 0, s, cnt, (uint32_t)C2, P, ptot);
     hipLaunchKernelGGL(k_mg_bases, dim3(1), dim3(256), 0, s, ptot, nb, P);
-    hipLaunchKernelGGL(k_mg_segrows, dim3((unsigned)((C + 255) / 256), nb), dim3(256), 0, s, cnt, seghi, ptot, nb,
-                       (uint32_t)C, P, (uint32_t)n, seg, wstart);
+    hipLaunchKernelGGL(k_mg_segrows, dim3((unsigned)((C2 + 255) / 256), nb), dim3(256), 0, s, cnt, seghi, ptot, nb,
+                       (uint32_t)C2, P, (uint32_t)n, seg, wstart);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     mo->active = true;
     mo->n = n;
@@ -958,9 +948,10 @@ static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *s
     mo->keys = (const uint8_t *)keys_cs;
     mo->answers = answers;
     mo->seg.seg = seg;
+    mo->seg.half = half;
     mo->seg.wstart = wstart;
     mo->seg.nseg = (uint32_t)ns;
-    mo->seg.C = (uint32_t)C;
+    mo->seg.C = (uint32_t)C2;
     mo->seg.nb = nb;
     return hipSuccess;
 }
@@ -1031,7 +1022,8 @@ hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answ
                                            (int)lds);
         if (a != hipSuccess) return a;
         hipLaunchKernelGGL((k_mg_unpermute<G, B>), dim3((unsigned)chunks), dim3(256), lds, s, mo.n, (const B *)mo.bucket,
-                           mo.runs, mo.nb, mo.bits, (const G *)mo.answers, (G *)out, ge, mo.seg.seg, mo.seg.C);
+                           mo.runs, mo.nb, mo.bits, (const G *)mo.answers, (G *)out, ge, mo.seg.seg, mo.seg.half,
+                           mo.seg.C);
         return hipGetLastError();
     };
     auto go = [&](auto g, uint32_t ge) { return mo.bucket8 ? go_b(g, uint8_t{}, ge) : go_b(g, uint16_t{}, ge); };
