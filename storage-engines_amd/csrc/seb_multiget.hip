@@ -596,8 +596,8 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const B *__restr
 //                     (bucket b's run of super-chunk sc) its count cnt[s], where the run starts in
 //                     keys_cs, seghi[s] = sc << 12 | offset, and its keys in the first chunk, half[s]
 //   k_mg_rows_pieces  scans each bucket's row of C counts in pieces of kMgPiece chunks
-//   k_mg_bases        bucket bases (scan of the bucket totals) plus the pieces' prefixes
-//   k_mg_segrows      seg[s] = first sorted row | seghi[s] << 32 (rows non-decreasing in s) and the
+//   k_mg_segrows      (bucket bases from the piece totals, per block) seg[s] = first sorted row |
+//                     seghi[s] << 32 (rows non-decreasing in s) and the
 //                     segment holding row 64 w of every wave w (wstart)
 // k_multiget finds each row's segment from its wave's start and a 64-entry window of seg
 // (mg_seg_key): three dependent loads (wstart, the window, the key) and no division; every
@@ -715,43 +715,36 @@ __global__ __launch_bounds__(256) void k_mg_rows_pieces(uint32_t *__restrict__ c
     if (threadIdx.x == 0) ptot[(uint64_t)b * P + blockIdx.x] = total;
 }
 
-// one block: bucket totals, their exclusive scan (the bucket bases), and in place of ptot each
-// piece's first sorted row
-__global__ __launch_bounds__(256) void k_mg_bases(uint32_t *__restrict__ ptot, uint32_t nb, uint32_t P) {
+// grid (C / 256, nb): segment s = b * C + c: seg[s] = its first sorted row | seghi[s] << 32, and
+// the waves whose first row it holds.  Each block first scans the bucket totals (sums of the piece
+// totals ptot) into the bucket bases; a piece's first row adds the pieces before it.
+__global__ __launch_bounds__(256) void k_mg_segrows(const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ seghi,
+                                                    const uint32_t *__restrict__ ptot, uint32_t nb, uint32_t C,
+                                                    uint32_t P, uint32_t n, uint64_t *__restrict__ seg,
+                                                    uint32_t *__restrict__ wstart) {
     __shared__ uint32_t base[kMgMaxBuckets];
     __shared__ uint32_t wsum[4];
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+    for (uint32_t u = threadIdx.x; u < nb; u += blockDim.x) {
         uint32_t t = 0;
-        for (uint32_t p = 0; p < P; ++p) t += ptot[(uint64_t)b * P + p];
-        base[b] = t;
+        for (uint32_t p = 0; p < P; ++p) t += ptot[(uint64_t)u * P + p];
+        base[u] = t;
     }
     __syncthreads();
     block_scan_lds(base, nb, wsum);
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
-        uint32_t t = base[b];
-        for (uint32_t p = 0; p < P; ++p) {
-            const uint32_t c = ptot[(uint64_t)b * P + p];
-            ptot[(uint64_t)b * P + p] = t;
-            t += c;
-        }
-    }
-}
-
-// grid (C / 256, nb): segment s = b * C + c: seg[s] = its first sorted row | seghi[s] << 32, and
-// the waves whose first row it holds
-__global__ __launch_bounds__(256) void k_mg_segrows(const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ seghi,
-                                                    const uint32_t *__restrict__ pbase, uint32_t nb, uint32_t C,
-                                                    uint32_t P, uint32_t n, uint64_t *__restrict__ seg,
-                                                    uint32_t *__restrict__ wstart) {
     const uint32_t b = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
+    auto first_row = [&](uint32_t bb, uint32_t cc) {  // of piece cc / kMgPiece of bucket bb
+        uint32_t t = base[bb];
+        for (uint32_t p = 0; p < cc / kMgPiece; ++p) t += ptot[(uint64_t)bb * P + p];
+        return t;
+    };
     const uint64_t s = (uint64_t)b * C + c;
-    const uint32_t row = pbase[(uint64_t)b * P + c / kMgPiece] + cnt[s];
+    const uint32_t row = first_row(b, c) + cnt[s];
     uint32_t next = n;
     if (c + 1 < C)
-        next = pbase[(uint64_t)b * P + (c + 1) / kMgPiece] + cnt[s + 1];
+        next = first_row(b, c + 1) + cnt[s + 1];
     else if (b + 1 < nb)
-        next = pbase[(uint64_t)(b + 1) * P] + cnt[s + 1];
+        next = base[b + 1] + cnt[s + 1];
     seg[s] = (uint64_t)row | ((uint64_t)seghi[s] << 32);
     for (uint32_t w = (row + 63) / 64; w < (next + 63) / 64; ++w) wstart[w] = (uint32_t)s;
 }
@@ -902,8 +895,8 @@ uint64_t multiget_order_bytes(const KeyBatch &kb, uint64_t answer_bytes, uint32_
            al256(multiget_order_moves(kb) ? n * 16 : n * 4) + run_bytes(n) + al256(n * answer_bytes);
 }
 
-// multiget_order 1 for aligned fixed 16-B keys: k_mg_bucket_sort, k_mg_rows_pieces, k_mg_bases,
-// k_mg_segrows, over super-chunk segments.
+// multiget_order 1 for aligned fixed 16-B keys: k_mg_bucket_sort, k_mg_rows_pieces, k_mg_segrows,
+// over super-chunk segments.
 static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *slots, uint32_t lo, uint32_t hi,
                                             const uint8_t *ranges, void *ws, MgOrder *mo, hipStream_t s) {
     const uint32_t nb = hi - lo + 1;
@@ -935,7 +928,6 @@ static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *s
     hipError_t e = b8 ? sort(uint8_t{}) : sort(uint16_t{});
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_mg_rows_pieces, dim3(P, nb), dim3(256), 0, s, cnt, (uint32_t)C2, P, ptot);
-    hipLaunchKernelGGL(k_mg_bases, dim3(1), dim3(256), 0, s, ptot, nb, P);
     hipLaunchKernelGGL(k_mg_segrows, dim3((unsigned)((C2 + 255) / 256), nb), dim3(256), 0, s, cnt, seghi, ptot, nb,
                        (uint32_t)C2, P, (uint32_t)n, seg, wstart);
     if ((e = hipGetLastError()) != hipSuccess) return e;
