@@ -1230,10 +1230,13 @@ def run_variant(args, cfg, over, note, seb, kg, torch, dist, world, rank, local,
     a2.config = cfg
     for key, v in over.items():
         setattr(a2, key, min(v, getattr(args, key)) if key in C5_VARIANT_STEPS else v)
+    t_setup = time.perf_counter()
     st2 = SETUPS[cfg](a2, seb, kg, torch, dev, rank, world, dist)
+    t_run = time.perf_counter()
     r2 = timed_run(a2, st2, seb, torch, dist, world, rank, dev)
     torch.cuda.synchronize()
     parity = st2.parity(a2.warmup + a2.steps - 1)
+    t_done = time.perf_counter()
     rec = rr.rank_record(rank, local, world, args.dist_backend, None, world, r2["kern_ms"], r2["wait_ms"],
                          r2["wait_host_ms"], r2["elapsed_own"])
     recs = rr.gather_records(dist, rec, world)
@@ -1247,7 +1250,9 @@ def run_variant(args, cfg, over, note, seb, kg, torch, dist, world, rank, local,
                "wait_ms": None if r2["wait_ms"] is None else round(r2["wait_ms"], 4),
                "per_rank": [{"rank": r["rank"], "kernel_ms": r["kernel_ms"], "wait_ms": r["wait_ms"],
                              "wait_host_ms": r["wait_host_ms"], "elapsed_s": r["elapsed_s"]} for r in recs],
-               "parity": parity, "workload": st2.workload, "parallelism": st2.parallelism, "note": note}
+               "parity": parity, "workload": st2.workload, "parallelism": st2.parallelism, "note": note,
+               # rank 0's wall clock for this variant (the N > 1 line's added runtime)
+               "wall_s": {"setup": round(t_run - t_setup, 3), "timed_and_parity": round(t_done - t_run, 3)}}
         if r2["bcast"]:
             out["broadcast"] = r2["bcast"]
     del st2
