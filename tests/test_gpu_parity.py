@@ -925,6 +925,42 @@ def test_fuzz_against_oracle(seb, ctx, build_algo):
                               oc.probe(ref, m, k, probes.data, probes.n, offsets=probes.offsets))
 
 
+def shared_prefix_keys(rng, n):
+    """(n, 16) u8 keys in blocks of 64 whose keys share their first L words (L = 0..4 per block;
+    4: the block is one key repeated), with blocks where one lane breaks the prefix: the shapes a
+    sorted flush batch gives a wave (the scalar-prefix hashing measured on them)."""
+    keys = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    for b0 in range(0, n, 64):
+        blk = keys[b0:b0 + 64]
+        L = int(rng.integers(0, 5))
+        blk[:, :4 * L] = blk[0, :4 * L]
+        if L and rng.random() < 0.25:  # one lane differs in the shared words
+            j = int(rng.integers(0, blk.shape[0]))
+            blk[j, int(rng.integers(0, 4 * L))] ^= 0x5A
+    return keys
+
+
+@pytest.mark.parametrize("n", [1, 63, 64 * 37 + 13, 300_001])
+def test_keys16_shared_prefix_waves(seb, torch_cuda, build_algo, probe_compact, n):
+    """Fixed 16-B keys whose waves share 0-4 leading words (a sorted batch), ragged tails and
+    duplicate keys: build bits and probe answers equal the oracle's for every build path and
+    both probe layouts."""
+    torch = torch_cuda
+    rng = np.random.default_rng(n)
+    keys = shared_prefix_keys(rng, n)
+    m, k = seb.params(max(n, 2), 0.01)
+    words = seb.new_words(m)
+    seb.dev_build(seb.dev_keys(to_dev(torch, keys), n=n, stride=16), words, m, k)
+    torch.cuda.synchronize()
+    ref = oc.build(m, k, keys, n, stride=16)
+    assert np.array_equal(seb.words_to_bits(words, m), ref)
+    probes = np.concatenate([keys[::2], shared_prefix_keys(rng, n)])
+    out = torch.empty(probes.shape[0], dtype=torch.uint8, device="cuda")
+    seb.dev_probe(seb.dev_keys(to_dev(torch, probes), n=probes.shape[0], stride=16), words, m, k, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), oc.probe(ref, m, k, probes, probes.shape[0], stride=16))
+
+
 # ------------------------------------------------------------- multi-filter (C5) ------------
 
 @pytest.mark.parametrize("which", [0, 1])
