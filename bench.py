@@ -901,11 +901,19 @@ def launch_check(args, world, rank):
     import dist_probe as dp
 
     rec["c5_plan"] = [dp.c5_rank_plan(args.keys, world, rank, form, 6) for form in ("root", "spread", "grid")]
+    # the variant loop with a stand-in for each variant's run (a collective, as the real ones use)
+    def stand_in(cfg, over, note):
+        x = torch.ones(1)
+        dist.all_reduce(x)
+        return {"config": cfg, "ranks": int(x.item())}
+
+    results = run_variants(dist_variants(args, world), dist, world, rank, stand_in)
     recs = rr.gather_records(dist, rec, world)
     if rank == 0:
         print(json.dumps({"n_gpus": dist.get_world_size(), "rank_sum": int(t.item()),
                           "variants": [{"key": key, "config": cfg, "overrides": over}
                                        for key, cfg, over, _ in dist_variants(args, world)],
+                          "variant_results": results,
                           "master": f"{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}",
                           "per_rank": recs, **rr.summarize(recs, world, "gloo")}), flush=True)
     dist.barrier()
@@ -1068,10 +1076,10 @@ def main():
     records = rr.gather_records(dist, rec, world)
     report = rr.summarize(records, world, backend)
     value = st.units_per_step * args.steps / elapsed / 1e6
-    extra = {}
-    for key, cfg, over, note in dist_variants(args, world):
-        # the same processes, after the headline: another form of the job or the north star's C5
-        extra[key] = run_variant(args, cfg, over, note, seb, kg, torch, dist, world, rank, local, dev)
+    # the same processes, after the headline: another form of the job or the north star's C5
+    extra = run_variants(dist_variants(args, world), dist, world, rank,
+                         lambda cfg, over, note: run_variant(args, cfg, over, note, seb, kg, torch, dist, world, rank,
+                                                             local, dev))
     result = None
     if rank == 0:
         result = {
@@ -1172,6 +1180,42 @@ def roofline_of(st, kern_ms: dict, config: str) -> dict:
                            "timed steps (launch_timers), on its launch stream; not the wall-clock step",
             "other": {d: {"ms": round(v[0], 4), "GB/s": round(v[1] / (v[0] * 1e-3) / 1e9, 2)}
                       for d, v in kern.items()}}
+
+
+VARIANT_VOTE_S = float(os.environ.get("SEB_BENCH_VARIANT_VOTE_S", "120"))
+
+
+def run_variants(variants: list, dist, world: int, rank: int, runner) -> dict:
+    """Run the N > 1 line's variants in order; {key: rank 0's summary}.  A variant that raises on
+    every rank (an operation the backend rejects, the same on all of them) is reported in the line
+    as {"error": ...} and the next one runs, so the headline and the other forms still print.  The
+    ranks confirm such a failure on a gloo side group with a bounded barrier: a rank that failed
+    while its peers went on (and wait in a collective it will never join) times out there and ends
+    the run, as an uncaught error would, instead of leaving the job hung until RCCL's own timeout.
+    SEB_BENCH_FAIL_VARIANT=key[@rank] makes that variant raise (on every rank, or one): the fault
+    the tests inject (tests/test_bench_launch.py)."""
+    import datetime
+
+    out = {}
+    if not variants:
+        return out
+    vote = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=VARIANT_VOTE_S)) if world > 1 else None
+    inject = os.environ.get("SEB_BENCH_FAIL_VARIANT", "")
+    fail_key, _, fail_rank = inject.partition("@")
+    for key, cfg, over, note in variants:
+        try:
+            if key == fail_key and (not fail_rank or int(fail_rank) == rank):
+                raise RuntimeError(f"injected failure of variant {key} (SEB_BENCH_FAIL_VARIANT)")
+            out[key] = runner(cfg, over, note)
+        except Exception as e:  # noqa: BLE001 - reported in the line; see the docstring
+            msg = f"{type(e).__name__}: {e}"[:400]
+            print(f"bench.py: rank {rank}: variant {key} failed: {msg}", file=sys.stderr, flush=True)
+            if vote is not None:
+                dist.barrier(group=vote)  # every rank failed here too, or this times out
+            out[key] = {"config": cfg, "error": msg, "note": note} if rank == 0 else None
+    if vote is not None:
+        dist.destroy_process_group(vote)
+    return out
 
 
 C5_VARIANT_STEPS = {"steps": 20, "warmup": 10}  # at most: a shorter headline run shortens them too

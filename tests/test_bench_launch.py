@@ -68,6 +68,30 @@ def test_gpus_n_spawns_n_ranks(n):
     assert all(p["recv_bytes"] % blk == 0 for p in plans["grid"])
 
 
+def test_variant_failing_on_every_rank_is_reported_and_the_line_prints():
+    """A variant that raises on every rank (e.g. an operation the backend rejects) becomes an
+    error entry; the variants after it still run and rank 0 still prints its one line."""
+    r = _run(["--gpus", "2", "--launch-check"], env=_env(SEB_BENCH_FAIL_VARIANT="c5"))
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    res = json.loads(lines[0])["variant_results"]
+    assert "injected failure" in res["c5"]["error"] and res["c5"]["config"] == "c5"
+    for key in ("all_gather_spread", "resident_batch", "c5_spread", "c5_2d"):
+        assert res[key]["ranks"] == 2, key  # the stand-in's all-reduce over both ranks
+    assert "variant c5 failed" in r.stderr
+
+
+def test_variant_failing_on_one_rank_ends_the_run():
+    """A variant that fails on one rank only leaves its peers in a collective it never joins: the
+    failing rank's bounded barrier on the gloo side group times out and the run exits non-zero
+    (as an uncaught error would) instead of hanging."""
+    r = _run(["--gpus", "2", "--launch-check"],
+             env=_env(SEB_BENCH_FAIL_VARIANT="c5@1", SEB_BENCH_VARIANT_VOTE_S="5"), timeout=180)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
 def test_c5_plan_alignment():
     """The 6-byte form's slices start at multiples of 64 keys at every world size the driver runs;
     the 8-byte form keeps key-granular slices."""
