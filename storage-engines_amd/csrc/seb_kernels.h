@@ -102,7 +102,7 @@ constexpr uint32_t kRegMaxFiles = 4096;  // registry capacity (u16 slot ids, 0xF
 // Answer j goes to row j of maybe / cand; key_order != null: key j is read as key key_order[j] of kb.
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
                            const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap, hipStream_t s,
-                           const uint32_t *key_order, const MgSeg &seg = MgSeg{});
+                           const uint32_t *key_order, const MgSeg &seg = MgSeg{}, bool narrow = false);
 // Key-range order for MultiGet: buckets = files of slots [lo, hi) (a disjoint, MinKey-ordered
 // level) with MinKey <= key.  The MultiGet then answers into mo.answers (sorted rows) and
 // launch_multiget_unpermute writes them to the caller's output in batch order.
@@ -118,6 +118,7 @@ struct MgOrder {
     const uint8_t *keys = nullptr;        // aligned fixed 16-B batches: the keys moved into that order
     void *answers = nullptr;              // n * answer_bytes: the MultiGet's answers in sorted rows
     MgSeg seg;                            // the scatter-free order: keys read through segments
+    bool narrow = false;                  // masks of registries whose slots are all < 32: sorted rows of u32
 };
 // Aligned fixed 16-B batches are sorted by bucket inside each chunk and read through the segment
 // tables (multiget_order 1) or moved into that order (multiget_order 2; 16 B more per key), others

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                                                   uint32_t nslots, RegLayout lay, const uint8_t *__restrict__ ranges,
                                                   uint64_t *__restrict__ maybe, uint16_t *__restrict__ cand,
                                                   uint32_t cap, const uint32_t *__restrict__ key_order,
-                                                  uint32_t xcd, MgSeg seg) {
+                                                  uint32_t xcd, MgSeg seg, uint32_t narrow) {
     constexpr bool kLds = MODE < 2, kList = MODE > 0;
     __shared__ RegSlot lslots[kLds ? kMaxSlots : 1];
     if constexpr (kLds) {
@@ -230,6 +230,8 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
             } else {
                 for (uint32_t t = nc; t < cap; ++t) row[t] = 0xFFFFu;
             }
+        } else if (narrow) {  // sorted rows of a registry whose slots are all < 32: half the bytes
+            ((uint32_t *)maybe)[oi] = (uint32_t)mask;
         } else {
             maybe[oi] = mask;
         }
@@ -767,7 +769,7 @@ static size_t mg_unpermute_lds(uint32_t nb) {
     return ((head + 15) & ~(size_t)15) + (size_t)kMgChunk * slice * sizeof(G);
 }
 
-template <typename G, typename B>
+template <typename G, typename B, bool NARROW = false>
 __global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const B *__restrict__ bucket,
                                                       const uint32_t *__restrict__ runs, uint32_t nb, uint32_t bits,
                                                       const G *__restrict__ answers, G *__restrict__ out,
@@ -811,7 +813,10 @@ __global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const B *__res
                 const uint32_t b = min((uint32_t)sb[p], nb - 1);
                 uint64_t row = (uint64_t)rbase[b] + (p - loc[b]);
                 row = row < n ? row : n - 1;  // always true when the runs are the scatter's; a guard
-                v[r] = answers[row * ge + g0 + g];
+                if constexpr (NARROW)  // u32 sorted masks widened to the caller's u64 (G = uint2, ge = 1)
+                    v[r] = make_uint2(((const uint32_t *)answers)[row], 0u);
+                else
+                    v[r] = answers[row * ge + g0 + g];
             }
 #pragma unroll
             for (uint32_t r = 0; r < 8; ++r) {
@@ -1006,19 +1011,26 @@ hipError_t launch_multiget_order(const KeyBatch &kb, const RegSlot *slots, uint3
 hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answer_bytes, hipStream_t s) {
     if (!mo.active || mo.n == 0) return hipSuccess;
     const uint64_t chunks = (mo.n + kMgChunk - 1) / kMgChunk;
-    auto go_b = [&](auto g, auto bt, uint32_t ge) -> hipError_t {
+    auto go_b = [&](auto g, auto bt, uint32_t ge, auto nw) -> hipError_t {
         using G = decltype(g);
         using B = decltype(bt);
+        constexpr bool NW = decltype(nw)::value;
         const size_t lds = mg_unpermute_lds<G>(mo.nb);
-        hipError_t a = hipFuncSetAttribute((const void *)k_mg_unpermute<G, B>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds);
+        hipError_t a = hipFuncSetAttribute((const void *)k_mg_unpermute<G, B, NW>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (a != hipSuccess) return a;
-        hipLaunchKernelGGL((k_mg_unpermute<G, B>), dim3((unsigned)chunks), dim3(256), lds, s, mo.n, (const B *)mo.bucket,
-                           mo.runs, mo.nb, mo.bits, (const G *)mo.answers, (G *)out, ge, mo.seg.seg, mo.seg.half,
-                           mo.seg.C);
+        hipLaunchKernelGGL((k_mg_unpermute<G, B, NW>), dim3((unsigned)chunks), dim3(256), lds, s, mo.n,
+                           (const B *)mo.bucket, mo.runs, mo.nb, mo.bits, (const G *)mo.answers, (G *)out, ge, mo.seg.seg,
+                           mo.seg.half, mo.seg.C);
         return hipGetLastError();
     };
-    auto go = [&](auto g, uint32_t ge) { return mo.bucket8 ? go_b(g, uint8_t{}, ge) : go_b(g, uint16_t{}, ge); };
+    auto go = [&](auto g, uint32_t ge) {
+        return mo.bucket8 ? go_b(g, uint8_t{}, ge, std::false_type{}) : go_b(g, uint16_t{}, ge, std::false_type{});
+    };
+    if (mo.narrow) {  // u32 sorted masks (launch_multiget narrow) into the caller's u64 masks
+        if (answer_bytes != 8 || ((uintptr_t)out & 7) != 0) return hipErrorInvalidValue;
+        return mo.bucket8 ? go_b(uint2{}, uint8_t{}, 1u, std::true_type{}) : go_b(uint2{}, uint16_t{}, 1u, std::true_type{});
+    }
     const bool a16 = ((uintptr_t)out & 15) == 0, a8 = ((uintptr_t)out & 7) == 0, a4 = ((uintptr_t)out & 3) == 0;
     if (answer_bytes == 16 && a16) return go(uint4{}, 1u);
     if (answer_bytes == 12 && a4) return go(uint3{}, 1u);  // 6-slot candidate rows
@@ -1030,7 +1042,7 @@ hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answ
 
 hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t nslots, const RegLayout &lay,
                            const uint8_t *ranges, uint64_t *maybe, uint16_t *cand, uint32_t cap, hipStream_t s,
-                           const uint32_t *key_order, const MgSeg &seg) {
+                           const uint32_t *key_order, const MgSeg &seg, bool narrow) {
     if (kb.n == 0) return hipSuccess;
     if (!cand && nslots > kMaxSlots) return hipErrorInvalidValue;  // the mask form stages slots in LDS
     uint64_t g = (kb.n + 255) / 256;
@@ -1040,7 +1052,7 @@ hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t ns
         using S = decltype(src);
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe, cand,
-                               cap, key_order, (uint32_t)options().multiget_xcd, seg);
+                               cap, key_order, (uint32_t)options().multiget_xcd, seg, (uint32_t)(narrow && maybe));
             return hipGetLastError();
         };
         if (lay.all_k7_m32) {

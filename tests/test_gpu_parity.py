@@ -1537,6 +1537,44 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
     reg.close()
 
 
+@pytest.mark.parametrize("nfiles", [31, 32])
+def test_registry_multiget_narrow_sorted_masks(seb, torch_cuda, nfiles):
+    """Registries whose slots are all < 32 carry the key-range order's sorted masks as u32 (one L0
+    file + 31 partition files: slots 0-31), one slot more keeps u64 rows: both equal the
+    batch-order walk, for device and host keys, ragged batches and both ordering forms."""
+    torch = torch_cuda
+    rng = np.random.default_rng(nfiles)
+    reg = seb.Registry(0)
+    universe = [kg.key16_bytes(int(i)) for i in range(1000, 61000, 2)]
+
+    def add(file_num, level, keys):
+        m, k = oc.params(len(keys), 0.01)
+        bits = oc.build(m, k, np.frombuffer(b"".join(keys), np.uint8), len(keys), stride=16)
+        return reg.put(file_num, level, bn.encode(bits, m, k), min(keys), max(keys))
+
+    slots = [add(100, 0, sorted(rng.choice(universe, 3000, replace=False).tolist()))]
+    for j, c in enumerate(np.array_split(np.array(universe, dtype=object), nfiles)):
+        slots.append(add(1000 + j, 1, list(c)[::3]))
+    assert max(slots) == nfiles  # 31 + 1 files: slots 0-31 (u32 rows); 32 + 1: slot 32 (u64 rows)
+    for n in (65_536, 200_003):
+        idx = rng.integers(0, 64000, n)
+        keys = kg.key16(idx)
+        dk = seb.dev_keys(to_dev(torch, keys), n=n, stride=16)
+        got = []
+        for order in (0, 1, 2):
+            with seb.option("multiget_order", order):
+                out = torch.full((n,), -1, dtype=torch.int64, device="cuda")
+                reg.multiget_dev(dk, out)
+                torch.cuda.synchronize()
+                got.append(out.cpu().numpy())
+                if order:
+                    assert np.array_equal(reg.multiget(keys), got[0])  # host keys, staged and moved
+        assert np.array_equal(got[0], got[1]) and np.array_equal(got[0], got[2])
+        if nfiles == 32:
+            assert (got[0] >> 32 != 0).any()  # slot 32 answers: the u64 rows carry bits past 31
+    reg.close()
+
+
 def test_registry_l0_group_table(seb, torch_cuda):
     """The L0 files sharing (m, k) are tested through one bit-interleaved table (multiget_l0_group):
     every answer, mask and list form, equals the per-file walk (option off) and the Python model of
