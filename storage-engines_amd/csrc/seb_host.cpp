@@ -2177,13 +2177,17 @@ static int multiget_piece(seb_registry *r, KeyBatch kb, uint64_t *maybe, uint16_
     MgOrder mo;
     int rc;
     if ((rc = multiget_order(r, kb, answer_bytes, s, &mo))) return rc;
-    // masks of a registry whose slots are all < 32 travel through the sorted rows as u32: 40 MB
-    // less written and read per 10M keys (the caller's output stays u64)
-    mo.narrow = mo.active && maybe && r->max_slot <= 32 && ((uintptr_t)maybe & 7) == 0;
+    // masks of a registry whose slots are all < 32 travel through the sorted rows as u32 (40 MB
+    // less written and read per 10M keys), list rows of 2/4/6/8 slots all < 255 as u8 (6-slot rows:
+    // 60 MB); the caller's output keeps its u64 masks / u16 rows
+    if (mo.active && maybe && r->max_slot <= 32 && ((uintptr_t)maybe & 7) == 0) mo.narrow = 1;
+    if (mo.active && !maybe && r->max_slot <= 255 && cap <= 8 && cap % 2 == 0 &&
+        ((uintptr_t)cand & (cap == 6 ? 3 : 2 * cap - 1)) == 0)
+        mo.narrow = 2;
     HIP_OR_FAIL(launch_multiget(kb, (const RegSlot *)r->dslots.p, r->nslots, mg_layout(r), (const uint8_t *)r->dranges.p,
                                 mo.active ? (maybe ? (uint64_t *)mo.answers : nullptr) : maybe,
                                 mo.active ? (maybe ? nullptr : (uint16_t *)mo.answers) : cand, cap, s, mo.key_order,
-                                mo.seg, mo.narrow));
+                                mo.seg, mo.narrow != 0));
     if (mo.active)
         HIP_OR_FAIL(launch_multiget_unpermute(mo, maybe ? (void *)maybe : (void *)cand, answer_bytes, s));
     return SEB_OK;

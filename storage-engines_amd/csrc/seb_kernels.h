@@ -118,7 +118,7 @@ struct MgOrder {
     const uint8_t *keys = nullptr;        // aligned fixed 16-B batches: the keys moved into that order
     void *answers = nullptr;              // n * answer_bytes: the MultiGet's answers in sorted rows
     MgSeg seg;                            // the scatter-free order: keys read through segments
-    bool narrow = false;                  // masks of registries whose slots are all < 32: sorted rows of u32
+    int narrow = 0;  // sorted rows held narrow: 1 u32 masks (slots all < 32), 2 u8 list rows (slots all < 255)
 };
 // Aligned fixed 16-B batches are sorted by bucket inside each chunk and read through the segment
 // tables (multiget_order 1) or moved into that order (multiget_order 2; 16 B more per key), others

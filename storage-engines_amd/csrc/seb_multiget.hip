@@ -157,7 +157,14 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         auto record = [&](const RegSlot &sl) {  // in Get's visiting order
             if constexpr (kList) {
                 if (nc < cap) {  // the host checks cap >= the walk's length
-                    if (rowpack) {
+                    if (narrow) {  // u8 slots (0xFF = none), 8 per register word
+#pragma unroll
+                        for (uint32_t q = 0; q < 2; ++q)
+                            if (q == (nc >> 3)) {
+                                const uint32_t sh = (nc & 7) * 8;
+                                rw[q] = (rw[q] & ~(0xFFull << sh)) | ((uint64_t)sl.slot << sh);
+                            }
+                    } else if (rowpack) {
 #pragma unroll
                         for (uint32_t q = 0; q < 4; ++q)
                             if (q == (nc >> 2)) {
@@ -215,7 +222,12 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
             if (hit >= 0) take(slots[hit]);
         }
         if constexpr (kList) {
-            if (rowpack == 8) {  // the row as whole words: cap % 4 == 0 / cap % 2 == 0, aligned
+            if (narrow) {  // sorted rows of cap u8 slots (cap even, <= 16): cap / 2 u16 words
+                uint16_t *row8 = (uint16_t *)((uint8_t *)cand + oi * (uint64_t)cap);
+#pragma unroll
+                for (uint32_t q = 0; q < 8; ++q)
+                    if (2 * q < cap) row8[q] = (uint16_t)(rw[q >> 2] >> ((q & 3) * 16));
+            } else if (rowpack == 8) {  // the row as whole words: cap % 4 == 0 / cap % 2 == 0, aligned
 #pragma unroll
                 for (uint32_t q = 0; q < 4; ++q)
                     if (4 * q < cap) ((uint64_t *)row)[q] = rw[q];
@@ -769,7 +781,10 @@ static size_t mg_unpermute_lds(uint32_t nb) {
     return ((head + 15) & ~(size_t)15) + (size_t)kMgChunk * slice * sizeof(G);
 }
 
-template <typename G, typename B, bool NARROW = false>
+// NARROW 1: u32 sorted masks widened to u64 (G = uint2, ge = 1); 2: sorted rows of cap = 2 W u8
+// slots widened to the caller's u16 rows, 0xFF -> 0xFFFF (G = the whole row of W u32 words,
+// W <= 4, ge = 1; the input row is read as the <= 2 aligned u32 words that cover it).
+template <typename G, typename B, int NARROW = 0>
 __global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const B *__restrict__ bucket,
                                                       const uint32_t *__restrict__ runs, uint32_t nb, uint32_t bits,
                                                       const G *__restrict__ answers, G *__restrict__ out,
@@ -813,10 +828,27 @@ __global__ __launch_bounds__(256) void k_mg_unpermute(uint64_t n, const B *__res
                 const uint32_t b = min((uint32_t)sb[p], nb - 1);
                 uint64_t row = (uint64_t)rbase[b] + (p - loc[b]);
                 row = row < n ? row : n - 1;  // always true when the runs are the scatter's; a guard
-                if constexpr (NARROW)  // u32 sorted masks widened to the caller's u64 (G = uint2, ge = 1)
+                if constexpr (NARROW == 1) {
                     v[r] = make_uint2(((const uint32_t *)answers)[row], 0u);
-                else
+                } else if constexpr (NARROW == 2) {
+                    constexpr uint32_t W = sizeof(G) / 4;
+                    static_assert(W >= 1 && W <= 4, "narrow list rows of 2..8 slots");
+                    const uint64_t off = row * (2 * W);  // even: the row starts 0 or 2 bytes into a word
+                    const uint32_t *wp = (const uint32_t *)((const uint8_t *)answers + (off & ~3ull));
+                    const uint32_t sh = (uint32_t)(off & 3u) * 8u;
+                    const uint32_t a = wp[0], b = (W + 1) / 2 > 1 ? wp[1] : 0u;
+                    uint32_t o[W];
+#pragma unroll
+                    for (uint32_t w = 0; w < W; ++w) {
+                        const uint32_t bp = sh + 16 * w;
+                        const uint32_t x = ((bp < 32 ? a : b) >> (bp & 31u)) & 0xFFFFu;
+                        const uint32_t s0 = x & 0xFFu, s1 = x >> 8;
+                        o[w] = (s0 == 0xFFu ? 0xFFFFu : s0) | (s1 == 0xFFu ? 0xFFFFu : s1) << 16;
+                    }
+                    __builtin_memcpy(&v[r], o, sizeof(G));
+                } else {
                     v[r] = answers[row * ge + g0 + g];
+                }
             }
 #pragma unroll
             for (uint32_t r = 0; r < 8; ++r) {
@@ -1014,7 +1046,7 @@ hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answ
     auto go_b = [&](auto g, auto bt, uint32_t ge, auto nw) -> hipError_t {
         using G = decltype(g);
         using B = decltype(bt);
-        constexpr bool NW = decltype(nw)::value;
+        constexpr int NW = decltype(nw)::value;
         const size_t lds = mg_unpermute_lds<G>(mo.nb);
         hipError_t a = hipFuncSetAttribute((const void *)k_mg_unpermute<G, B, NW>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1025,11 +1057,23 @@ hipError_t launch_multiget_unpermute(const MgOrder &mo, void *out, uint64_t answ
         return hipGetLastError();
     };
     auto go = [&](auto g, uint32_t ge) {
-        return mo.bucket8 ? go_b(g, uint8_t{}, ge, std::false_type{}) : go_b(g, uint16_t{}, ge, std::false_type{});
+        using N0 = std::integral_constant<int, 0>;
+        return mo.bucket8 ? go_b(g, uint8_t{}, ge, N0{}) : go_b(g, uint16_t{}, ge, N0{});
     };
-    if (mo.narrow) {  // u32 sorted masks (launch_multiget narrow) into the caller's u64 masks
+    if (mo.narrow == 1) {  // u32 sorted masks (launch_multiget narrow) into the caller's u64 masks
         if (answer_bytes != 8 || ((uintptr_t)out & 7) != 0) return hipErrorInvalidValue;
-        return mo.bucket8 ? go_b(uint2{}, uint8_t{}, 1u, std::true_type{}) : go_b(uint2{}, uint16_t{}, 1u, std::true_type{});
+        using N1 = std::integral_constant<int, 1>;
+        return mo.bucket8 ? go_b(uint2{}, uint8_t{}, 1u, N1{}) : go_b(uint2{}, uint16_t{}, 1u, N1{});
+    }
+    if (mo.narrow == 2) {  // u8 sorted list rows (2..8 slots) into the caller's u16 rows, one row per key
+        using N2 = std::integral_constant<int, 2>;
+        auto go2 = [&](auto g) { return mo.bucket8 ? go_b(g, uint8_t{}, 1u, N2{}) : go_b(g, uint16_t{}, 1u, N2{}); };
+        const bool a16 = ((uintptr_t)out & 15) == 0, a8 = ((uintptr_t)out & 7) == 0, a4 = ((uintptr_t)out & 3) == 0;
+        if (answer_bytes == 16 && a16) return go2(uint4{});
+        if (answer_bytes == 12 && a4) return go2(uint3{});
+        if (answer_bytes == 8 && a8) return go2(uint2{});
+        if (answer_bytes == 4 && a4) return go2(uint32_t{});
+        return hipErrorInvalidValue;
     }
     const bool a16 = ((uintptr_t)out & 15) == 0, a8 = ((uintptr_t)out & 7) == 0, a4 = ((uintptr_t)out & 3) == 0;
     if (answer_bytes == 16 && a16) return go(uint4{}, 1u);
@@ -1052,7 +1096,7 @@ hipError_t launch_multiget(const KeyBatch &kb, const RegSlot *slots, uint32_t ns
         using S = decltype(src);
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(256), 0, s, src, kb, slots, nslots, lay, ranges, maybe, cand,
-                               cap, key_order, (uint32_t)options().multiget_xcd, seg, (uint32_t)(narrow && maybe));
+                               cap, key_order, (uint32_t)options().multiget_xcd, seg, (uint32_t)narrow);
             return hipGetLastError();
         };
         if (lay.all_k7_m32) {

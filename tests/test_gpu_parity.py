@@ -1537,11 +1537,13 @@ def test_registry_multiget_key_range_order(seb, torch_cuda):
     reg.close()
 
 
-@pytest.mark.parametrize("nfiles", [31, 32])
-def test_registry_multiget_narrow_sorted_masks(seb, torch_cuda, nfiles):
-    """Registries whose slots are all < 32 carry the key-range order's sorted masks as u32 (one L0
-    file + 31 partition files: slots 0-31), one slot more keeps u64 rows: both equal the
-    batch-order walk, for device and host keys, ragged batches and both ordering forms."""
+@pytest.mark.parametrize("nfiles", [31, 32, 254, 255])
+def test_registry_multiget_narrow_sorted_rows(seb, torch_cuda, nfiles):
+    """The key-range order's sorted rows travel narrow when the slots allow: masks as u32 when
+    every slot is < 32 (one L0 file + 31 partition files: slots 0-31), list rows of <= 16 slots as
+    u8 when every slot is < 255 (0xFF = none; 1 + 254 files: slots 0-254).  One slot more keeps
+    the wide rows.  Every form equals the batch-order walk, for device and host keys, two batch
+    sizes and both ordering forms; list caps 2 / 4 / 6 (narrow when even) and 5 / 20 (wide)."""
     torch = torch_cuda
     rng = np.random.default_rng(nfiles)
     reg = seb.Registry(0)
@@ -1555,23 +1557,35 @@ def test_registry_multiget_narrow_sorted_masks(seb, torch_cuda, nfiles):
     slots = [add(100, 0, sorted(rng.choice(universe, 3000, replace=False).tolist()))]
     for j, c in enumerate(np.array_split(np.array(universe, dtype=object), nfiles)):
         slots.append(add(1000 + j, 1, list(c)[::3]))
-    assert max(slots) == nfiles  # 31 + 1 files: slots 0-31 (u32 rows); 32 + 1: slot 32 (u64 rows)
+    assert max(slots) == nfiles  # the largest slot id in use
+    masks = nfiles < 64
     for n in (65_536, 200_003):
-        idx = rng.integers(0, 64000, n)
-        keys = kg.key16(idx)
+        keys = kg.key16(rng.integers(0, 64000, n))
         dk = seb.dev_keys(to_dev(torch, keys), n=n, stride=16)
-        got = []
+        got, lists = [], {}
         for order in (0, 1, 2):
             with seb.option("multiget_order", order):
-                out = torch.full((n,), -1, dtype=torch.int64, device="cuda")
-                reg.multiget_dev(dk, out)
-                torch.cuda.synchronize()
-                got.append(out.cpu().numpy())
-                if order:
-                    assert np.array_equal(reg.multiget(keys), got[0])  # host keys, staged and moved
-        assert np.array_equal(got[0], got[1]) and np.array_equal(got[0], got[2])
-        if nfiles == 32:
-            assert (got[0] >> 32 != 0).any()  # slot 32 answers: the u64 rows carry bits past 31
+                if masks:
+                    out = torch.full((n,), -1, dtype=torch.int64, device="cuda")
+                    reg.multiget_dev(dk, out)
+                    torch.cuda.synchronize()
+                    got.append(out.cpu().numpy())
+                    if order:
+                        assert np.array_equal(reg.multiget(keys), got[0])  # host keys, staged and moved
+                for cap in (2, 4, 5, 6, 20):
+                    lst = torch.full((n, cap), -7, dtype=torch.int16, device="cuda")
+                    reg.multiget_list_dev(dk, lst, cap)
+                    torch.cuda.synchronize()
+                    lists.setdefault(cap, []).append(lst.cpu().numpy().view(np.uint16))
+        if masks:
+            assert np.array_equal(got[0], got[1]) and np.array_equal(got[0], got[2])
+            if nfiles == 32:
+                assert (got[0] >> 32 != 0).any()  # slot 32 answers: the u64 rows carry bits past 31
+        for cap, ls in lists.items():
+            assert np.array_equal(ls[0], ls[1]) and np.array_equal(ls[0], ls[2]), cap
+            assert np.array_equal(ls[0][:, :2], lists[2][0]), cap  # a longer row extends the short one
+        if nfiles == 255:
+            assert (lists[4][0] == 255).any()  # slot 255 answers: the u16 rows carry it
     reg.close()
 
 
