@@ -1543,7 +1543,8 @@ def test_registry_multiget_narrow_sorted_rows(seb, torch_cuda, nfiles):
     every slot is < 32 (one L0 file + 31 partition files: slots 0-31), list rows of <= 16 slots as
     u8 when every slot is < 255 (0xFF = none; 1 + 254 files: slots 0-254).  One slot more keeps
     the wide rows.  Every form equals the batch-order walk, for device and host keys, two batch
-    sizes and both ordering forms; list caps 2 / 4 / 6 (narrow when even) and 5 / 20 (wide)."""
+    sizes, both ordering forms and ordered pieces; list caps 2 / 4 / 6 (narrow when even) and
+    5 / 20 (wide)."""
     torch = torch_cuda
     rng = np.random.default_rng(nfiles)
     reg = seb.Registry(0)
@@ -1563,8 +1564,9 @@ def test_registry_multiget_narrow_sorted_rows(seb, torch_cuda, nfiles):
         keys = kg.key16(rng.integers(0, 64000, n))
         dk = seb.dev_keys(to_dev(torch, keys), n=n, stride=16)
         got, lists = [], {}
-        for order in (0, 1, 2):
-            with seb.option("multiget_order", order):
+        # order 1 also in ordered pieces of 64K keys (multiget_piece_mib 1), the last one ragged
+        for order, piece in ((0, 1024), (1, 1024), (2, 1024), (1, 1)):
+            with seb.option("multiget_order", order), seb.option("multiget_piece_mib", piece):
                 if masks:
                     out = torch.full((n,), -1, dtype=torch.int64, device="cuda")
                     reg.multiget_dev(dk, out)
@@ -1578,11 +1580,11 @@ def test_registry_multiget_narrow_sorted_rows(seb, torch_cuda, nfiles):
                     torch.cuda.synchronize()
                     lists.setdefault(cap, []).append(lst.cpu().numpy().view(np.uint16))
         if masks:
-            assert np.array_equal(got[0], got[1]) and np.array_equal(got[0], got[2])
+            assert all(np.array_equal(got[0], g) for g in got[1:])
             if nfiles == 32:
                 assert (got[0] >> 32 != 0).any()  # slot 32 answers: the u64 rows carry bits past 31
         for cap, ls in lists.items():
-            assert np.array_equal(ls[0], ls[1]) and np.array_equal(ls[0], ls[2]), cap
+            assert all(np.array_equal(ls[0], x) for x in ls[1:]), cap
             assert np.array_equal(ls[0][:, :2], lists[2][0]), cap  # a longer row extends the short one
         if nfiles == 255:
             assert (lists[4][0] == 255).any()  # slot 255 answers: the u16 rows carry it
