@@ -524,38 +524,42 @@ __global__ __launch_bounds__(256) void k_interleave(MultiArg ma, uint64_t m, Mas
     table[p] = e;
 }
 
-// The same table by wave ballots: a wave covers 128 bit positions (4 words), lane f holds those 4
-// words of filter f (one 16-B load), and for each position one ballot over the lanes IS the entry
-// (bit f = filter f).  Lane L stores entries 2L and 2L+1.  Needs 16-B aligned word arrays of
-// seb_words_bytes(m) bytes (whole 16-B units).
+// Lane r holds row r of a 64 x 64 bit matrix (bit c = column c); returns column `lane` (bit r = row
+// r's bit `lane`).  Six butterfly stages: stage j exchanges the off-diagonal j x j blocks of the
+// lane pairs (r, r ^ j), one 64-bit shuffle and a masked merge each.
+__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x, uint32_t lane) {
+    constexpr uint64_t kLow[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                                  0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+    for (int st = 0; st < 6; ++st) {
+        const uint32_t j = 32u >> st;
+        const uint64_t lo = kLow[st];  // bit positions c with (c & j) == 0
+        const uint32_t ylo = (uint32_t)__shfl_xor((int)(uint32_t)x, (int)j, 64);
+        const uint32_t yhi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), (int)j, 64);
+        const uint64_t y = (uint64_t)yhi << 32 | ylo;
+        x = (lane & j) ? (x & ~lo) | ((y & ~lo) >> j) : (x & lo) | ((y & lo) << j);
+    }
+    return x;
+}
+
+// The same table by a bit transpose per wave: a wave covers 128 bit positions (4 words), lane f
+// holds those 4 words of filter f (one 16-B load), and each 64-position half, transposed across
+// the wave, leaves lane c holding entry p0 + 64 h + c (bit f = filter f): 64 consecutive entries
+// per store.  Round 3 built each entry by a ballot (≈4 VALU per entry to move it into its lane);
+// the transpose costs ≈1.5.  Needs 16-B aligned word arrays of seb_words_bytes(m) bytes.
 template <typename MaskT>
-__global__ __launch_bounds__(256) void k_interleave_ballot(MultiArg ma, uint64_t m, MaskT *__restrict__ table) {
+__global__ __launch_bounds__(256) void k_interleave_xpose(MultiArg ma, uint64_t m, MaskT *__restrict__ table) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t p0 = (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 128;
     if (p0 >= m) return;  // wave-uniform
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (lane < ma.nf) v = *(const uint4 *)(ma.f[lane].words + (p0 >> 5));
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    MaskT e0 = 0, e1 = 0;
 #pragma unroll
-    for (int i = 0; i < 128; ++i) {
-        const MaskT b = (MaskT)__ballot((w[i >> 5] >> (i & 31)) & 1u);
-        if (lane == (uint32_t)(i >> 1)) {
-            if (i & 1)
-                e1 = b;
-            else
-                e0 = b;
-        }
-    }
-    const uint64_t p = p0 + 2 * lane;
-    if (p + 1 < m) {
-        typedef MaskT pair_t __attribute__((ext_vector_type(2)));
-        pair_t pr;
-        pr.x = e0;
-        pr.y = e1;
-        *(pair_t *)(table + p) = pr;
-    } else if (p < m) {
-        table[p] = e0;
+    for (int h = 0; h < 2; ++h) {
+        const uint64_t x = h ? (uint64_t)v.w << 32 | v.z : (uint64_t)v.y << 32 | v.x;
+        const uint64_t e = wave_transpose64(x, lane);
+        const uint64_t p = p0 + 64 * h + lane;
+        if (p < m) table[p] = (MaskT)e;
     }
 }
 
@@ -564,7 +568,7 @@ static void launch_interleave(const MultiArg &ma, uint64_t m, MaskT *table, hipS
     bool aligned = true;
     for (uint32_t f = 0; f < ma.nf; ++f) aligned &= ((uintptr_t)ma.f[f].words & 15) == 0;
     if (aligned)  // (one 4-B load per filter per entry otherwise: 22 vs 17 us for the C5 table)
-        hipLaunchKernelGGL((k_interleave_ballot<MaskT>), dim3((unsigned)((m + 511) / 512)), dim3(256), 0, s, ma, m, table);
+        hipLaunchKernelGGL((k_interleave_xpose<MaskT>), dim3((unsigned)((m + 511) / 512)), dim3(256), 0, s, ma, m, table);
     else
         hipLaunchKernelGGL((k_interleave<MaskT>), dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, ma, m, table);
 }

@@ -64,12 +64,12 @@ def shapes():
     types = {8: "unsigned char", 16: "unsigned short", 32: "unsigned int", 64: "unsigned long"}
     for w in WORLDS:
         f = NF // w
-        out.append((f"c5p6_f{f}", (f"k_probe_interleaved_packed<{types[f]}, 6>", f"k_interleave_ballot<{types[f]}>"),
+        out.append((f"c5p6_f{f}", (f"k_probe_interleaved_packed<{types[f]}, 6>", f"k_interleave_xpose<{types[f]}>"),
                     None))
     for w in WORLDS:
         cnt = c2d_keys(w)
         out.append((f"c5_2d6_w{w}", ("k_probe_interleaved_packed<unsigned long, 6>",
-                                     "k_interleave_ballot<unsigned long>"), grid_threads((cnt + 1) // 2)))
+                                     "k_interleave_xpose<unsigned long>"), grid_threads((cnt + 1) // 2)))
     return out
 
 
@@ -168,14 +168,14 @@ def summarize(tag: str, pmc_json: str) -> None:
 
     # Per call = the sum over a shape's dispatches / the dispatches of its first kernel (once per
     # call): setup calls of the same kernels (the first pack6) then count as calls too.
-    # The 64-filter table build (k_interleave_ballot<unsigned long>) is the same work for every
+    # The 64-filter table build (k_interleave_xpose<unsigned long>) is the same work for every
     # c5_2d shape: its mean is added to each.
     dur, calls_t = collections.defaultdict(float), collections.defaultdict(int)
     tab_ns = []
     for r in csv.DictReader(open(glob.glob(os.path.join(src, "trace", "*kernel_trace.csv"))[0])):
         name, grid = r["Kernel_Name"], int(r["Grid_Size_X"])
         ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        if "k_interleave_ballot<unsigned long>" in name:
+        if "k_interleave_xpose<unsigned long>" in name:
             tab_ns.append(ns)
             continue
         s, first = shape_of(name, grid)
@@ -188,7 +188,7 @@ def summarize(tag: str, pmc_json: str) -> None:
     for fn in glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv")):
         for r in csv.DictReader(open(fn)):
             name, grid, c, v = r["Kernel_Name"], int(r["Grid_Size"]), r["Counter_Name"], float(r["Counter_Value"])
-            if "k_interleave_ballot<unsigned long>" in name:
+            if "k_interleave_xpose<unsigned long>" in name:
                 tab[c].append(v)
                 continue
             s, first = shape_of(name, grid)
