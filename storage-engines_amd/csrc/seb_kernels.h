@@ -96,6 +96,7 @@ struct MgSeg {
     const uint32_t *wstart = nullptr;
     const uint32_t *half = nullptr;
     uint32_t nseg = 0, C = 0, nb = 0, pad = 0;
+    uint32_t part_lo = 0;  // the partition level's first lookup-ordered slot: bucket b >= 1's file is part_lo + b - 1
 };
 // cand != null: the list form (cap u16 slots per key, any nslots) instead of masks.
 constexpr uint32_t kRegMaxFiles = 4096;  // registry capacity (u16 slot ids, 0xFFFF = none)

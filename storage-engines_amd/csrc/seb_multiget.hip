@@ -92,7 +92,7 @@ __device__ __forceinline__ uint32_t test_l0_group(const RegLayout &lay, uint64_t
 }
 
 struct MgSeg;
-__device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uint64_t j);
+__device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uint64_t j, uint32_t &sidx);
 
 // MODE 0: u64 mask, slot table in LDS.  MODE 1: candidate list, slot table in LDS.  MODE 2:
 // candidate list, slot table read from HBM/L2 (more than kMaxSlots files: an LSM past L1 holds
@@ -133,8 +133,12 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
         // k_mg_scatter or are read through key_order, and k_mg_unpermute brings the answers back
         // to batch order as whole lines.
         const uint64_t j = jw + (threadIdx.x & 63u);
-        const uint64_t segkey = seg.seg ? mg_seg_key(seg, jw, j < kb.n ? j : kb.n - 1) : 0;
+        uint32_t sidx = 0;
+        const uint64_t segkey = seg.seg ? mg_seg_key(seg, jw, j < kb.n ? j : kb.n - 1, sidx) : 0;
         if (j >= kb.n) continue;
+        // segment order: the row's bucket (its segment is b * C + sc) names its partition-level
+        // file, so that level needs no bisection, only the MaxKey cover check
+        const int pb = seg.seg ? (int)(sidx / seg.C) : -1;
         const uint64_t oi = j;
         const uint64_t i = seg.seg ? segkey : key_order ? (uint64_t)key_order[j] : j;
         const uint8_t *key;
@@ -196,7 +200,13 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
             const uint32_t lo = lay.lo[L], hi = lay.hi[L];
             if (lo == hi) continue;
             int hit = -1;
-            if (lay.nonoverlap >> L & 1u) {
+            if (pb >= 0 && lo == seg.part_lo) {  // bucket b >= 1: the last file with MinKey <= key
+                if (pb >= 1) {
+                    const RegSlot &sl = slots[lo + (uint32_t)pb - 1];
+                    if (cmp_key(key, klen, k0, k1, sl.max_be, ranges + sl.max_off, sl.max_len) <= 0)
+                        hit = (int)(lo + (uint32_t)pb - 1);
+                }
+            } else if (lay.nonoverlap >> L & 1u) {
                 // last file with MinKey <= key; it is the only one that can cover the key
                 uint32_t a = lo, b = hi;
                 while (a < b) {
@@ -616,7 +626,7 @@ __global__ __launch_bounds__(256) void k_mg_scatter(uint64_t n, const B *__restr
 // k_multiget finds each row's segment from its wave's start and a 64-entry window of seg
 // (mg_seg_key): three dependent loads (wstart, the window, the key) and no division; every
 // segment's keys are contiguous in keys_cs.  k_mg_unpermute reads each chunk's run starts from seg.
-__device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uint64_t j) {
+__device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uint64_t j, uint32_t &sidx) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t r = (uint32_t)j;
     const uint32_t s0 = sg.wstart[jw >> 6];
@@ -631,6 +641,7 @@ __device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uin
     const uint32_t lo = (uint32_t)__shfl((int)er, (int)i, 64);
     const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(e >> 32), (int)i, 64);
     uint64_t ent = (uint64_t)lo | ((uint64_t)hi << 32);
+    sidx = s0 + i;
     if (i == 63) {  // the row may lie past the window (a run of empty segments): bisect the rest
         uint32_t a = s0 + 63, b = sg.nseg;
         while (b - a > 1) {
@@ -641,6 +652,7 @@ __device__ __forceinline__ uint64_t mg_seg_key(const MgSeg &sg, uint64_t jw, uin
                 b = mid;
         }
         ent = sg.seg[a];
+        sidx = a;
     }
     const uint32_t h = (uint32_t)(ent >> 32);
     return (uint64_t)(h >> 12) * kMgSuper + (h & 4095u) + (r - (uint32_t)ent);
@@ -982,6 +994,7 @@ static hipError_t launch_multiget_order_seg(const KeyBatch &kb, const RegSlot *s
     mo->seg.nseg = (uint32_t)ns;
     mo->seg.C = (uint32_t)C2;
     mo->seg.nb = nb;
+    mo->seg.part_lo = lo;
     return hipSuccess;
 }
 
