@@ -1893,6 +1893,8 @@ struct seb_registry {
     bool dirty = true;
     DevBuf dslots, dranges;
     DevBuf dl0;                    // the L0 group's interleaved table (RegLayout::l0tab)
+    DevBuf dbrange;                // per partition bucket, each disjoint level's bisection range (MgSeg::brange)
+    bool has_brange = false;
     uint32_t nslots = 0;
     uint32_t max_cand = 0;         // longest Get walk: every L0 file + one file per non-empty level 1..4
     uint32_t max_slot = 0;         // 1 + the largest slot id in use (the mask form needs <= 64)
@@ -2089,6 +2091,33 @@ static int sync_registry_locked(seb_registry *r) {
             r->part_lo = lay.lo[L];
             r->part_hi = lay.hi[L];
         }
+    // Per bucket b (keys K with MinKey_P[b-1] <= K < MinKey_P[b] of the partition files P) and
+    // disjoint level L: A = its files with MinKey <= MinKey_P[b-1], B = those with MinKey <
+    // MinKey_P[b]; K's bisection result lies in [A, B].
+    r->has_brange = false;
+    if (r->part_hi > r->part_lo) {
+        const uint32_t nb = r->part_hi - r->part_lo + 1;
+        std::vector<uint32_t> br((size_t)nb * 4, 0u);
+        for (uint32_t b = 0; b < nb; ++b) {
+            const std::string *low = b ? &order[r->part_lo + b - 1]->min_key : nullptr;
+            const std::string *high = b + 1 < nb ? &order[r->part_lo + b]->min_key : nullptr;
+            for (int L = 1; L < 5; ++L) {
+                uint32_t A = 0, B = lay.hi[L] - lay.lo[L];
+                if ((lay.nonoverlap >> L & 1u) && lay.hi[L] > lay.lo[L]) {  // MinKey-ordered files
+                    const auto f0 = order.begin() + lay.lo[L], f1 = order.begin() + lay.hi[L];
+                    if (low)
+                        A = (uint32_t)(std::partition_point(f0, f1, [&](const RegEntry *e) { return e->min_key <= *low; }) - f0);
+                    if (high)
+                        B = (uint32_t)(std::partition_point(f0, f1, [&](const RegEntry *e) { return e->min_key < *high; }) - f0);
+                }
+                br[(size_t)b * 4 + L - 1] = A | B << 16;
+            }
+        }
+        int brc;
+        if ((brc = r->dbrange.reserve(br.size() * 4))) return brc;
+        HIP_OR_FAIL(hipMemcpy(r->dbrange.p, br.data(), br.size() * 4, hipMemcpyHostToDevice));
+        r->has_brange = true;
+    }
     r->dirty = false;
     return SEB_OK;
 }
@@ -2181,6 +2210,7 @@ static int multiget_piece(seb_registry *r, KeyBatch kb, uint64_t *maybe, uint16_
     // less written and read per 10M keys), list rows of 2/4/6/8 slots all < 255 as u8 (6-slot rows:
     // 60 MB); the caller's output keeps its u64 masks / u16 rows
     if (mo.active && maybe && r->max_slot <= 32 && ((uintptr_t)maybe & 7) == 0) mo.narrow = 1;
+    if (mo.seg.seg && r->has_brange) mo.seg.brange = (const uint32_t *)r->dbrange.p;
     if (mo.active && !maybe && r->max_slot <= 255 && cap <= 8 && cap % 2 == 0 &&
         ((uintptr_t)cand & (cap == 6 ? 3 : 2 * cap - 1)) == 0)
         mo.narrow = 2;

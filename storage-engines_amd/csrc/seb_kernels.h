@@ -97,6 +97,9 @@ struct MgSeg {
     const uint32_t *half = nullptr;
     uint32_t nseg = 0, C = 0, nb = 0, pad = 0;
     uint32_t part_lo = 0;  // the partition level's first lookup-ordered slot: bucket b >= 1's file is part_lo + b - 1
+    // per bucket b and level L = 1..4, brange[4 b + L - 1] = A | B << 16: a disjoint level's bisection for a
+    // key of bucket b ends in [lo + A, lo + B] (the files whose MinKey can bound the bucket's keys); null: none
+    const uint32_t *brange = nullptr;
 };
 // cand != null: the list form (cap u16 slots per key, any nslots) instead of masks.
 constexpr uint32_t kRegMaxFiles = 4096;  // registry capacity (u16 slot ids, 0xFFFF = none)

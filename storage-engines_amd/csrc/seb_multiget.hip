@@ -207,8 +207,15 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
                         hit = (int)(lo + (uint32_t)pb - 1);
                 }
             } else if (lay.nonoverlap >> L & 1u) {
-                // last file with MinKey <= key; it is the only one that can cover the key
+                // last file with MinKey <= key; it is the only one that can cover the key.  In
+                // segment order the bucket bounds the key, so the search starts on the few files
+                // whose MinKey can fall in the bucket's key range
                 uint32_t a = lo, b = hi;
+                if (pb >= 0 && seg.brange) {
+                    const uint32_t e = seg.brange[4 * (uint32_t)pb + L - 1];
+                    a = lo + (e & 0xFFFFu);
+                    b = lo + (e >> 16);
+                }
                 while (a < b) {
                     const uint32_t mid = (a + b) >> 1;
                     const RegSlot &sl = slots[mid];
