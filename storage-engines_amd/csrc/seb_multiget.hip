@@ -150,10 +150,16 @@ __global__ __launch_bounds__(256) void k_multiget(Src src, KeyBatch kb, const Re
             key = kb.data + i * (uint64_t)kb.stride;
             klen = kb.stride;
         }
-        uint64_t h1, h2;
-        src.hash(i, h1, h2);
-        uint64_t k0, k1;
-        key_prefix(kb, key, klen, k0, k1);
+        uint64_t h1, h2, k0, k1;
+        if constexpr (std::is_same<Src, Keys16>::value) {  // one 16-B load feeds the hash and the compares
+            const uint4 v = src.load(i);
+            Src::hash_raw(v, h1, h2);
+            k0 = __builtin_bswap64((uint64_t)v.x | ((uint64_t)v.y << 32));
+            k1 = __builtin_bswap64((uint64_t)v.z | ((uint64_t)v.w << 32));
+        } else {
+            src.hash(i, h1, h2);
+            key_prefix(kb, key, klen, k0, k1);
+        }
         uint64_t mask = 0;
         uint16_t *row = kList ? cand + oi * (uint64_t)cap : nullptr;
         uint32_t nc = 0;
